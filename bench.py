@@ -1,0 +1,197 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident 2D Reed-Solomon EDS encode on MI355X.
+
+Metric (BASELINE.json): GiB/s of device-resident 2D RS encode, k=128 square,
+512 B shares (config 2: 128x128 -> 256x256, GF(2^8)), plus % of HBM peak.
+
+A "step" = ComputeExtendedDataSquare's arithmetic (erasureExtendSquare,
+extendeddatasquare.go:154-227) over one batch of `--batch` independent squares
+already resident in HBM (the EDS buffer holds each ODS in its top-left quadrant,
+as the Go EDS aliases its input).  The batch (16 x 32 MiB = 512 MiB by default) is
+larger than the 256 MiB Infinity Cache, so steps do not run out of cache.
+value = ODS bytes encoded per second over all ranks (GiB/s).
+
+N > 1 GPUs (one process per GPU, torch.distributed): every rank encodes its own
+batch of independent squares -- the work partitions by square with no data-path
+exchange, so scaling is "weak".
+
+Extra JSON objects: "roofline" (dominant kernel, HIP-event timed on the launch
+stream), "step_roofline" (whole 2D encode vs SURVEY's algorithmic bytes 4k^2 S),
+"cpu_baseline" (the C oracle restatement -- kind "port" -- on this host's cores),
+"host_path" (PCIe-inclusive rate through rsm_extend_square; never `value`).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+WORKLOADS = {
+    "c2": dict(k=128, S=512, desc="128x128->256x256 square, 512 B shares, GF(2^8)"),
+    "c4": dict(k=256, S=2048, desc="256x256->512x512 square, 2048 B shares, GF(2^16)"),
+}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    p.add_argument("--batch", type=int, default=0, help="squares per step (default: >= 512 MiB of EDS)")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=3.0)
+    return p.parse_args()
+
+
+def cpu_baseline(k, S, seconds):
+    """The oracle's C restatement of the reference path, multithreaded over codewords."""
+    import numpy as np
+    import oracle
+    threads = min(16, os.cpu_count() or 1)
+    ods = oracle.splitmix64_bytes(k * k * S).reshape(k, k, S)
+    oracle.extend_square(ods, nthreads=threads)  # warm
+    n, t0 = 0, time.perf_counter()
+    while True:
+        oracle.extend_square(ods, nthreads=threads)
+        n += 1
+        dt = time.perf_counter() - t0
+        if dt >= seconds:
+            break
+    return {"value": round(n * k * k * S / dt / 2**30, 4), "unit": "GiB/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{n} squares k={k} S={S} through oracle/leopard_oracle.c (scalar C restatement of "
+                      f"klauspost leopard, {threads} threads over codewords); the Go reference cannot run here"}
+
+
+def main():
+    a = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import rsmt2d_amd as R
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group(backend="nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    wl = WORKLOADS[a.workload]
+    k, S = wl["k"], wl["S"]
+    W = 2 * k
+    sq_bytes = W * W * S
+    B = a.batch or max(1, (512 << 20) // sq_bytes)
+    L = R.library()
+    ctx = R.device_context(local)
+
+    # synthetic ODS (seeded uniform bytes) placed in the top-left quadrant of each square
+    g = torch.Generator(device=dev)
+    g.manual_seed(0x52534D543244 + rank)
+    eds = torch.empty((B, W, W, S), dtype=torch.uint8, device=dev)
+    eds[:, :k, :k] = torch.randint(0, 256, (B, k, k, S), dtype=torch.uint8, device=dev, generator=g)
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+
+    def step():
+        R._check(L.rsm_extend_squares_dev(ctx, eds.data_ptr(), k, S, B, sh))
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    # correctness gate on one square before timing (oracle is test infra; bench only checks)
+    if rank == 0:
+        import oracle
+        got = eds[0].cpu().numpy()
+        want = oracle.extend_square(got[:k, :k].copy(), nthreads=min(16, os.cpu_count() or 1))
+        if not np.array_equal(got, want):
+            raise SystemExit("bench: GPU EDS differs from oracle -- refusing to report")
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # per-kernel durations on the launch stream (HIP events), separate short run
+    nrep = max(5, min(a.steps, 20))
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(nrep)]
+    for i in range(nrep):
+        ev[i][0].record(stream)
+        R._check(L.rsm_extend_squares_phase_dev(ctx, eds.data_ptr(), k, S, B, 1, sh))
+        ev[i][1].record(stream)
+        R._check(L.rsm_extend_squares_phase_dev(ctx, eds.data_ptr(), k, S, B, 2, sh))
+        ev[i][2].record(stream)
+    torch.cuda.synchronize()
+    t_row = sum(e[0].elapsed_time(e[1]) for e in ev) / nrep / 1e3
+    t_col = sum(e[1].elapsed_time(e[2]) for e in ev) / nrep / 1e3
+
+    ods_bytes = k * k * S
+    total = world * B * a.steps * ods_bytes
+    value = total / elapsed / 2**30
+    ms_per_step = elapsed / a.steps * 1e3
+    algo_step = 4 * ods_bytes * B  # read Q0 once, write Q1+Q2+Q3
+    col_bytes = 4 * ods_bytes * B  # column pass moves [Q0|Q1] in and [Q2|Q3] out
+    row_bytes = 2 * ods_bytes * B  # row pass: Q0 in, Q1 out
+    dominant = ("encode_gf8_kernel<128> column pass" if k == 128 else f"encode kernel column pass (k={k})",
+                col_bytes, t_col) if t_col >= t_row else ("row pass", row_bytes, t_row)
+    ach = dominant[1] / dominant[2] / 1e9
+    out = {
+        "metric": "GiB/s device-resident 2D RS encode, k=128 square, 512 B shares; % HBM peak",
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8" if k <= 128 else "u16",
+        "data": "synthetic (seeded uniform bytes, device-generated)",
+        "config": {"workload": f"{a.workload}: {wl['desc']}", "k": k, "share_size": S,
+                   "squares_per_step": B, "eds_bytes_per_step": B * sq_bytes,
+                   "parallelism": f"independent squares per GPU x{world}"},
+        "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel": dominant[0], "avg_launch_us": round(dominant[2] * 1e6, 2),
+                     "bytes_per_launch": dominant[1]},
+        "step_roofline": {"algorithmic_bytes": algo_step, "achieved": round(algo_step / (elapsed / a.steps) / 1e9, 1),
+                          "frac": round(algo_step / (elapsed / a.steps) / 1e9 / HBM_PEAK_GBS, 4),
+                          "row_pass_us": round(t_row * 1e6, 2), "col_pass_us": round(t_col * 1e6, 2)},
+    }
+    if rank == 0 and world == 1:
+        # PCIe-inclusive host-memory rate (ComputeExtendedDataSquare from host buffers)
+        ods = np.random.default_rng(1).integers(0, 256, (k, k, S), dtype=np.uint8)
+        eh = np.empty((W, W, S), np.uint8)
+        R._check(L.rsm_extend_square(ctx, ods.ctypes.data, k, S, eh.ctypes.data))
+        t1, n = time.perf_counter(), 0
+        while time.perf_counter() - t1 < 1.0:
+            R._check(L.rsm_extend_square(ctx, ods.ctypes.data, k, S, eh.ctypes.data))
+            n += 1
+        out["host_path"] = {"value": round(n * ods_bytes / (time.perf_counter() - t1) / 2**30, 3), "unit": "GiB/s",
+                            "note": "rsm_extend_square: pageable host ODS -> H2D -> extend -> D2H EDS, one square"}
+        out["cpu_baseline"] = None if a.no_cpu_baseline else cpu_baseline(k, S, a.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,161 @@
+/*
+ * rsmt2d_hip.h -- C ABI of the MI355X-native 2D Reed-Solomon EDS engine.
+ *
+ * Drop-in boundary for celestiaorg/rsmt2d's hot path: the Codec plugin
+ * (codecs.go:14-30, implemented by LeoRSCodec in leopard.go:16-103) and the
+ * two-dimensional schedule / crossword solver built on it
+ * (extendeddatasquare.go:50-243, extendeddatacrossword.go:74-502).
+ * Everything is plain pointers and sizes so a cgo shim can bind
+ * it directly; no call ever aborts or throws across the ABI.
+ *
+ * Return codes: 0 on success, a negative RSM_E* code on failure;
+ * rsm_last_error() gives a thread-local human-readable message.
+ */
+#ifndef RSMT2D_HIP_H
+#define RSMT2D_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RSM_OK 0
+#define RSM_EINVAL (-1)        /* bad argument */
+#define RSM_ESHARESIZE (-2)    /* share size not a multiple of 64 (leopard.go:92-99) */
+#define RSM_ETOOFEW (-3)       /* Decode: fewer than k of 2k shares present */
+#define RSM_ESHAPE (-4)        /* non-square count, uneven shares, odd EDS width, > MaxChunks */
+#define RSM_EDEVICE (-5)       /* HIP runtime failure / no GPU: never a silent CPU fallback */
+#define RSM_ENOMEM (-6)
+#define RSM_EUNSUPPORTED (-7)  /* configuration this build does not implement */
+#define RSM_EUNREPAIRABLE (-8) /* ErrUnrepairableDataSquare (extendeddatacrossword.go:37) */
+#define RSM_EBYZANTINE (-9)    /* ErrByzantineData (extendeddatacrossword.go:42-58) */
+#define RSM_ECELL (-10)        /* SetCell on a non-nil cell or wrong size (datasquare.go:341-353) */
+#define RSM_ETREE (-11)        /* tree callback error / root of an incomplete vector */
+
+#define RSM_AXIS_ROW 0 /* rsmt2d.Row (extendeddatacrossword.go:15-18) */
+#define RSM_AXIS_COL 1 /* rsmt2d.Col */
+
+typedef struct rsm_ctx rsm_ctx;
+typedef struct rsm_eds rsm_eds;
+
+/* ---- context --------------------------------------------------------------- */
+/* One context per GPU (device ordinal).  Thread-safe: calls on one context are
+ * serialised internally (rsmt2d calls the Codec from up to 2k goroutines,
+ * extendeddatasquare.go:186-224). */
+int rsm_ctx_create(int device, rsm_ctx** out);
+void rsm_ctx_destroy(rsm_ctx* ctx);
+const char* rsm_last_error(void);
+const char* rsm_version(void);
+int rsm_device_count(void);
+
+/* ---- Codec (codecs.go:14-30; LeoRSCodec leopard.go:16-103) ------------------- */
+/* Name() -- "Leopard" (codecs.go:11): EDS.Equals and JSON compare codec names. */
+const char* rsm_codec_name(void);
+/* MaxChunks() -- 32768 * 32768 (leopard.go:76-84). */
+int64_t rsm_codec_max_chunks(void);
+/* ValidateChunkSize(shareSize) -- RSM_ESHARESIZE unless a multiple of 64. */
+int rsm_codec_validate_chunk_size(int64_t share_size);
+/* 8 when 2k <= 256 (GF(2^8)), else 16 (GF(2^16)) -- codecs.go:6-10. */
+int rsm_codec_field_bits(uint32_t k);
+/* Encode(data) (leopard.go:28-45): k complete shares of share_size bytes in host
+ * memory -> k parity shares written to parity[0..k). */
+int rsm_encode(rsm_ctx* ctx, const uint8_t* const* data, uint32_t k, uint32_t share_size,
+               uint8_t* const* parity);
+/* Decode(data) (leopard.go:51-59, klauspost Reconstruct): n = 2k slots; slot i is
+ * present iff present[i] != 0; every missing slot's buffer shares[i] (caller
+ * allocated, share_size bytes) is filled.  RSM_ETOOFEW if fewer than k present;
+ * all present is a no-op. */
+int rsm_decode(rsm_ctx* ctx, uint8_t* const* shares, const uint8_t* present, uint32_t n,
+               uint32_t share_size);
+
+/* ---- batched 2D extension (erasureExtendSquare, extendeddatasquare.go:154-227) -- */
+/* Host memory: ods = k*k shares row-major, eds = (2k)^2 shares row-major. */
+int rsm_extend_square(rsm_ctx* ctx, const uint8_t* ods, uint32_t k, uint32_t share_size,
+                      uint8_t* eds);
+/* Device-resident, in place: d_eds holds `count` consecutive [2k][2k][S] squares
+ * whose top-left quadrant already holds the ODS (the EDS aliases the ODS, as in
+ * ComputeExtendedDataSquare).  Enqueued on `stream` (a hipStream_t, NULL =
+ * the context stream); asynchronous. */
+int rsm_extend_squares_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size, uint32_t count,
+                           void* stream);
+/* One phase of the above: phase 1 = row pass (Q0 -> Q1), phase 2 = column pass
+ * ([Q0|Q1] -> [Q2|Q3]); for per-kernel timing/profiling.  Asynchronous. */
+int rsm_extend_squares_phase_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size,
+                                 uint32_t count, int phase, void* stream);
+/* Device-resident batched reconstruct of whole rows (axis 0) or columns (axis 1)
+ * of one [2k][2k][S] square: d_presence is one byte per cell, d_indices the
+ * vectors to rebuild (each must have >= k cells present).  Asynchronous. */
+int rsm_decode_vectors_dev(rsm_ctx* ctx, void* d_eds, const uint8_t* d_presence, uint32_t k,
+                           uint32_t share_size, int axis, const uint32_t* d_indices, uint32_t count,
+                           void* stream);
+
+/* ---- Tree plugin (tree.go:11-28) ------------------------------------------------ */
+/* Computes the root of one row/column: Push(leaves[0..n)) then Root().  Writes
+ * the root to root_out (capacity *root_len on entry), sets *root_len, returns 0;
+ * non-zero = tree error (treated as byzantine by Repair, as in the reference). */
+typedef int (*rsm_tree_root_fn)(void* user, int axis, uint32_t index, const uint8_t* const* leaves,
+                                uint32_t n_leaves, uint32_t leaf_size, uint8_t* root_out,
+                                uint32_t* root_len);
+/* NewDefaultTree restatement: celestiaorg/merkletree over SHA-256 (leaf
+ * H(0x00||d), node H(0x01||l||r)).  Passed as NULL tree_fn below. */
+int rsm_default_tree_root(void* user, int axis, uint32_t index, const uint8_t* const* leaves,
+                          uint32_t n_leaves, uint32_t leaf_size, uint8_t* root_out,
+                          uint32_t* root_len);
+
+/* ---- ExtendedDataSquare (extendeddatasquare.go, datasquare.go) ------------------ */
+/* ComputeExtendedDataSquare(data, codec, tree) (:50-77): n shares (lens[i] bytes). */
+int rsm_eds_compute(rsm_ctx* ctx, const uint8_t* const* data, const uint32_t* lens, uint64_t n,
+                    rsm_eds** out);
+/* ImportExtendedDataSquare (:95-124): data[i] == NULL marks a missing share.
+ * Import/New are host-only and accept ctx == NULL (a context is then needed,
+ * via rsm_eds_set_context, before Repair). */
+int rsm_eds_import(rsm_ctx* ctx, const uint8_t* const* data, const uint32_t* lens, uint64_t n,
+                   rsm_eds** out);
+/* NewExtendedDataSquare(codec, tree, edsWidth, shareSize) (:129-152). */
+int rsm_eds_new(rsm_ctx* ctx, uint32_t eds_width, uint32_t share_size, rsm_eds** out);
+void rsm_eds_free(rsm_eds* eds);
+int rsm_eds_set_context(rsm_eds* eds, rsm_ctx* ctx);
+uint32_t rsm_eds_width(const rsm_eds* eds);
+uint32_t rsm_eds_original_width(const rsm_eds* eds);
+uint32_t rsm_eds_share_size(const rsm_eds* eds);
+/* GetCell: copies the share to out and returns 1, or returns 0 for nil. */
+int rsm_eds_get_cell(const rsm_eds* eds, uint32_t row, uint32_t col, uint8_t* out);
+/* SetCell: RSM_ECELL if the cell is non-nil or len != share size. */
+int rsm_eds_set_cell(rsm_eds* eds, uint32_t row, uint32_t col, const uint8_t* share, uint32_t len);
+/* Test hook mirroring the reference's unexported setCell (datasquare_test.go:735-739):
+ * overwrites a cell without the nil check; share == NULL makes it nil. */
+int rsm_eds_overwrite_cell(rsm_eds* eds, uint32_t row, uint32_t col, const uint8_t* share, uint32_t len);
+/* Flattened(): width^2 * share_size bytes row-major + width^2 presence bytes. */
+int rsm_eds_flattened(const rsm_eds* eds, uint8_t* out, uint8_t* present);
+/* RowRoots()/ColRoots() (:258-280): width roots of root_cap bytes each. */
+int rsm_eds_roots(rsm_eds* eds, int axis, rsm_tree_root_fn tree_fn, void* user, uint8_t* roots_out,
+                  uint32_t root_cap, uint32_t* root_len);
+
+typedef struct {
+    int32_t axis;   /* RSM_AXIS_ROW / RSM_AXIS_COL */
+    uint32_t index; /* row or column index */
+} rsm_byzantine;
+
+/* Repair(rowRoots, colRoots) (extendeddatacrossword.go:74-84): roots are
+ * width * root_len bytes each.  Returns 0, RSM_EUNREPAIRABLE, or RSM_EBYZANTINE
+ * (then *byz names the axis/index; rsm_eds_byzantine_shares() returns the
+ * vector's shares as they were before repair, missing shares absent). */
+int rsm_eds_repair(rsm_eds* eds, const uint8_t* row_roots, const uint8_t* col_roots, uint32_t root_len,
+                   rsm_tree_root_fn tree_fn, void* user, rsm_byzantine* byz);
+int rsm_eds_byzantine_shares(const rsm_eds* eds, uint8_t* out, uint8_t* present);
+
+/* Diagnostics: counters of the last Repair (fast device path taken or not,
+ * device decode sweeps, codewords decoded). */
+typedef struct {
+    int32_t fast_path;
+    uint32_t sweeps;
+    uint32_t decoded_vectors;
+    uint32_t fallback_reason;
+} rsm_repair_stats;
+int rsm_eds_repair_stats(const rsm_eds* eds, rsm_repair_stats* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RSMT2D_HIP_H */

@@ -89,7 +89,9 @@ def decode(shares):
     list with the missing slots filled (the reference fills in place)."""
     n = len(shares)
     k = n // 2
-    S = next(len(s) for s in shares if s is not None)
+    S = next((len(s) for s in shares if s is not None), None)
+    if S is None:
+        raise TooFewShards("too few shards given")
     bufs = [np.frombuffer(bytes(s), dtype=np.uint8).copy() if s is not None
             else np.zeros(S, dtype=np.uint8) for s in shares]
     present = bytes(1 if s is not None else 0 for s in shares)

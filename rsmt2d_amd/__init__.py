@@ -1,0 +1,497 @@
+"""rsmt2d_amd -- Python mirror of celestiaorg/rsmt2d's API over the MI355X engine.
+
+The product is ``librsmt2d_hip.so`` (HIP kernels for gfx950 + C++ host runtime,
+C ABI in ``include/rsmt2d_hip.h``).  This module is a thin ``ctypes`` binding
+that keeps the reference's names and semantics so tests read like the
+reference's own:
+
+    codec = NewLeoRSCodec()                                   # leopard.go:101
+    eds = ComputeExtendedDataSquare(shares, codec, NewDefaultTree)
+    row_roots, col_roots = eds.RowRoots(), eds.ColRoots()
+    eds2 = ImportExtendedDataSquare(flattened_with_nones, codec, NewDefaultTree)
+    eds2.Repair(row_roots, col_roots)    # raises ErrByzantineData / ErrUnrepairableDataSquare
+
+Every compute entry point runs the HIP path; with no GPU it raises
+``DeviceError`` -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import base64
+import ctypes
+import json
+import os
+import subprocess
+import threading
+from typing import Callable, List, Optional, Sequence
+
+__all__ = [
+    "Leopard", "Row", "Col", "Axis", "Codec", "LeoRSCodec", "NewLeoRSCodec",
+    "ExtendedDataSquare", "ComputeExtendedDataSquare", "ImportExtendedDataSquare",
+    "NewExtendedDataSquare", "NewDefaultTree", "Tree", "ErrByzantineData",
+    "ErrUnrepairableDataSquare", "ErrUnevenChunks", "RSMError", "DeviceError",
+    "library", "build", "device_context",
+]
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "librsmt2d_hip.so")
+
+Leopard = "Leopard"  # codecs.go:11
+Row = 0              # extendeddatacrossword.go:15-18
+Col = 1
+Axis = int
+
+# rsmt2d_hip.h return codes
+RSM_OK, RSM_EINVAL, RSM_ESHARESIZE, RSM_ETOOFEW, RSM_ESHAPE, RSM_EDEVICE = 0, -1, -2, -3, -4, -5
+RSM_ENOMEM, RSM_EUNSUPPORTED, RSM_EUNREPAIRABLE, RSM_EBYZANTINE, RSM_ECELL, RSM_ETREE = -6, -7, -8, -9, -10, -11
+
+
+class RSMError(Exception):
+    """Error returned by the C ABI (code = RSM_E*)."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(msg)
+        self.code = code
+
+
+class DeviceError(RSMError):
+    """No usable GPU / HIP failure.  The product never falls back to the CPU."""
+
+
+class _Unrepairable(RSMError):
+    pass
+
+
+#: ErrUnrepairableDataSquare (extendeddatacrossword.go:37) -- a singleton like the Go sentinel.
+ErrUnrepairableDataSquare = _Unrepairable(RSM_EUNREPAIRABLE, "failed to solve data square")
+
+#: ErrUnevenChunks (datasquare.go:14)
+ErrUnevenChunks = "non-nil shares not all of equal size"
+
+
+class ErrByzantineData(RSMError):
+    """ErrByzantineData (extendeddatacrossword.go:42-58): Axis, Index, Shares (None = missing)."""
+
+    def __init__(self, axis: int, index: int, shares: List[Optional[bytes]]):
+        super().__init__(RSM_EBYZANTINE, f"byzantine {'row' if axis == Row else 'col'}: {index}")
+        self.Axis = axis
+        self.Index = index
+        self.Shares = shares
+
+
+# ---------------------------------------------------------------------------
+# library loading
+# ---------------------------------------------------------------------------
+_lib = None
+_lib_lock = threading.Lock()
+_TREE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32,
+                            ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32, ctypes.c_uint32,
+                            ctypes.POINTER(ctypes.c_uint8), ctypes.POINTER(ctypes.c_uint32))
+
+
+class _Byz(ctypes.Structure):
+    _fields_ = [("axis", ctypes.c_int32), ("index", ctypes.c_uint32)]
+
+
+class RepairStats(ctypes.Structure):
+    _fields_ = [("fast_path", ctypes.c_int32), ("sweeps", ctypes.c_uint32),
+                ("decoded_vectors", ctypes.c_uint32), ("fallback_reason", ctypes.c_uint32)]
+
+
+# (name, restype, argtypes) of every symbol declared in include/rsmt2d_hip.h
+_VP, _U8P, _U32, _I32, _I64, _U64 = (ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                     ctypes.c_int, ctypes.c_int64, ctypes.c_uint64)
+SIGNATURES = {
+    "rsm_ctx_create": (_I32, [_I32, ctypes.POINTER(_VP)]),
+    "rsm_ctx_destroy": (None, [_VP]),
+    "rsm_last_error": (ctypes.c_char_p, []),
+    "rsm_version": (ctypes.c_char_p, []),
+    "rsm_device_count": (_I32, []),
+    "rsm_codec_name": (ctypes.c_char_p, []),
+    "rsm_codec_max_chunks": (_I64, []),
+    "rsm_codec_validate_chunk_size": (_I32, [_I64]),
+    "rsm_codec_field_bits": (_I32, [_U32]),
+    "rsm_encode": (_I32, [_VP, _VP, _U32, _U32, _VP]),
+    "rsm_decode": (_I32, [_VP, _VP, _VP, _U32, _U32]),
+    "rsm_extend_square": (_I32, [_VP, _VP, _U32, _U32, _VP]),
+    "rsm_extend_squares_dev": (_I32, [_VP, _VP, _U32, _U32, _U32, _VP]),
+    "rsm_extend_squares_phase_dev": (_I32, [_VP, _VP, _U32, _U32, _U32, _I32, _VP]),
+    "rsm_decode_vectors_dev": (_I32, [_VP, _VP, _VP, _U32, _U32, _I32, _VP, _U32, _VP]),
+    "rsm_default_tree_root": (_I32, [_VP, _I32, _U32, _VP, _U32, _U32, _VP, _VP]),
+    "rsm_eds_compute": (_I32, [_VP, _VP, _VP, _U64, ctypes.POINTER(_VP)]),
+    "rsm_eds_import": (_I32, [_VP, _VP, _VP, _U64, ctypes.POINTER(_VP)]),
+    "rsm_eds_new": (_I32, [_VP, _U32, _U32, ctypes.POINTER(_VP)]),
+    "rsm_eds_free": (None, [_VP]),
+    "rsm_eds_set_context": (_I32, [_VP, _VP]),
+    "rsm_eds_width": (_U32, [_VP]),
+    "rsm_eds_original_width": (_U32, [_VP]),
+    "rsm_eds_share_size": (_U32, [_VP]),
+    "rsm_eds_get_cell": (_I32, [_VP, _U32, _U32, _VP]),
+    "rsm_eds_set_cell": (_I32, [_VP, _U32, _U32, _VP, _U32]),
+    "rsm_eds_overwrite_cell": (_I32, [_VP, _U32, _U32, _VP, _U32]),
+    "rsm_eds_flattened": (_I32, [_VP, _VP, _VP]),
+    "rsm_eds_roots": (_I32, [_VP, _I32, _VP, _VP, _VP, _U32, ctypes.POINTER(_U32)]),
+    "rsm_eds_repair": (_I32, [_VP, _VP, _VP, _U32, _VP, _VP, ctypes.POINTER(_Byz)]),
+    "rsm_eds_byzantine_shares": (_I32, [_VP, _VP, _VP]),
+    "rsm_eds_repair_stats": (_I32, [_VP, ctypes.POINTER(RepairStats)]),
+}
+
+
+def build() -> str:
+    """Compile librsmt2d_hip.so for gfx950 (make in rsmt2d_amd/csrc)."""
+    subprocess.run(["make", "-s", "-j8", "-C", os.path.join(_HERE, "csrc")], check=True)
+    return LIB_PATH
+
+
+def library() -> ctypes.CDLL:
+    global _lib
+    with _lib_lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise DeviceError(RSM_EDEVICE, f"{LIB_PATH} is missing: run rsmt2d_amd.build() "
+                                               "(the HIP extension is required; there is no CPU path)")
+            L = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                f = getattr(L, name)
+                f.restype = res
+                f.argtypes = args
+            _lib = L
+    return _lib
+
+
+def _err(rc: int) -> RSMError:
+    msg = (library().rsm_last_error() or b"").decode(errors="replace")
+    if rc == RSM_EDEVICE:
+        return DeviceError(rc, msg)
+    return RSMError(rc, msg)
+
+
+def _check(rc: int) -> None:
+    if rc != RSM_OK:
+        raise _err(rc)
+
+
+_ctx = {}
+_ctx_lock = threading.Lock()
+
+
+def device_context(device: int = 0) -> int:
+    """The per-process rsm_ctx for a GPU (created on first use)."""
+    with _ctx_lock:
+        if device not in _ctx:
+            h = ctypes.c_void_p()
+            _check(library().rsm_ctx_create(device, ctypes.byref(h)))
+            _ctx[device] = h.value
+        return _ctx[device]
+
+
+def _bufs(shares: Sequence[Optional[bytes]]):
+    """Keeps the bytes objects alive; returns (keepalive, void* array, u32 lens)."""
+    n = len(shares)
+    ptrs = (ctypes.c_void_p * max(n, 1))()
+    lens = (ctypes.c_uint32 * max(n, 1))()
+    keep = []
+    for i, s in enumerate(shares):
+        if s is None:
+            ptrs[i] = None
+            lens[i] = 0
+        else:
+            b = ctypes.create_string_buffer(bytes(s), len(s))
+            keep.append(b)
+            ptrs[i] = ctypes.cast(b, ctypes.c_void_p)
+            lens[i] = len(s)
+    return keep, ptrs, lens
+
+
+# ---------------------------------------------------------------------------
+# Codec (codecs.go:14-30) and LeoRSCodec (leopard.go)
+# ---------------------------------------------------------------------------
+class Codec:
+    def Encode(self, data):  # pragma: no cover - interface
+        raise NotImplementedError
+
+    def Decode(self, data):  # pragma: no cover - interface
+        raise NotImplementedError
+
+    def MaxChunks(self) -> int:  # pragma: no cover - interface
+        raise NotImplementedError
+
+    def Name(self) -> str:  # pragma: no cover - interface
+        raise NotImplementedError
+
+    def ValidateChunkSize(self, chunkSize: int):  # pragma: no cover - interface
+        raise NotImplementedError
+
+
+class LeoRSCodec(Codec):
+    """HIP-backed drop-in for rsmt2d.LeoRSCodec (leopard.go:16-103)."""
+
+    def __init__(self, device: int = 0):
+        self.device = device
+
+    def Encode(self, data: Sequence[bytes]) -> List[bytes]:
+        k = len(data)
+        if k == 0:
+            raise RSMError(RSM_EINVAL, "no shares")
+        S = len(data[0])
+        if any(d is None or len(d) != S for d in data):
+            raise RSMError(RSM_ESHAPE, "shard sizes do not match")
+        keep, ptrs, _ = _bufs(data)
+        outs = [ctypes.create_string_buffer(S) for _ in range(k)]
+        optr = (ctypes.c_void_p * k)(*[ctypes.cast(o, ctypes.c_void_p) for o in outs])
+        _check(library().rsm_encode(device_context(self.device), ptrs, k, S, optr))
+        return [o.raw for o in outs]
+
+    def Decode(self, data: List[Optional[bytes]]) -> List[Optional[bytes]]:
+        """Fills the None entries of ``data`` in place (as klauspost Reconstruct does)
+        and returns the same list; raises RSMError(RSM_ETOOFEW) if < half present."""
+        n = len(data)
+        S = next((len(d) for d in data if d is not None), 0)
+        present = (ctypes.c_uint8 * n)(*[0 if d is None else 1 for d in data])
+        bufs = [ctypes.create_string_buffer(bytes(d) if d is not None else S, S) for d in data]
+        ptrs = (ctypes.c_void_p * n)(*[ctypes.cast(b, ctypes.c_void_p) for b in bufs])
+        _check(library().rsm_decode(device_context(self.device), ptrs, present, n, S))
+        for i in range(n):
+            if data[i] is None:
+                data[i] = bufs[i].raw
+        return data
+
+    def MaxChunks(self) -> int:
+        return int(library().rsm_codec_max_chunks())
+
+    def Name(self) -> str:
+        return library().rsm_codec_name().decode()
+
+    def ValidateChunkSize(self, chunkSize: int):
+        rc = library().rsm_codec_validate_chunk_size(int(chunkSize))
+        if rc != RSM_OK:
+            return _err(rc)
+        return None
+
+
+def NewLeoRSCodec(device: int = 0) -> LeoRSCodec:
+    return LeoRSCodec(device)
+
+
+# codecs registry (codecs.go:32-40), used by JSON unmarshalling
+codecs = {Leopard: NewLeoRSCodec()}
+
+
+# ---------------------------------------------------------------------------
+# Tree plugin (tree.go)
+# ---------------------------------------------------------------------------
+class Tree:
+    """Tree interface: Push(data) / Root() -> bytes."""
+
+    def Push(self, data: bytes):  # pragma: no cover - interface
+        raise NotImplementedError
+
+    def Root(self) -> bytes:  # pragma: no cover - interface
+        raise NotImplementedError
+
+
+def NewDefaultTree(axis: int = Row, index: int = 0):
+    """Marker for the built-in DefaultTree (SHA-256 merkletree, tree.go:38)."""
+    return None
+
+
+def _tree_callback(tree_fn):
+    """ctypes callback for a Python TreeConstructorFn, or NULL for NewDefaultTree."""
+    if tree_fn is None or tree_fn is NewDefaultTree:
+        return None, None
+
+    def cb(user, axis, index, leaves, n, leaf_size, root_out, root_len):
+        try:
+            t = tree_fn(axis, index)
+            for i in range(n):
+                t.Push(ctypes.string_at(leaves[i], leaf_size))
+            r = t.Root()
+            if len(r) > root_len[0]:
+                return RSM_EINVAL
+            ctypes.memmove(root_out, r, len(r))
+            root_len[0] = len(r)
+            return 0
+        except Exception:  # tree errors are byzantine evidence, as in the reference
+            return RSM_ETREE
+
+    c = _TREE_FN(cb)
+    return c, ctypes.cast(c, ctypes.c_void_p)
+
+
+def _default_root(leaves: Sequence[bytes]) -> bytes:
+    keep, ptrs, _ = _bufs(leaves)
+    out = (ctypes.c_uint8 * 64)()
+    ln = ctypes.c_uint32(64)
+    _check(library().rsm_default_tree_root(None, 0, 0, ptrs, len(leaves),
+                                           len(leaves[0]) if leaves else 0, out, ctypes.byref(ln)))
+    return bytes(out[:ln.value])
+
+
+# ---------------------------------------------------------------------------
+# ExtendedDataSquare (extendeddatasquare.go)
+# ---------------------------------------------------------------------------
+class ExtendedDataSquare:
+    def __init__(self, handle: int, codec: Codec, tree_fn, device: int = 0):
+        self._h = ctypes.c_void_p(handle)
+        self.codec = codec
+        self._tree_fn = tree_fn
+        self._device = device
+
+    def __del__(self):
+        try:
+            if self._h:
+                library().rsm_eds_free(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+    # --- geometry ---
+    def Width(self) -> int:
+        return int(library().rsm_eds_width(self._h))
+
+    @property
+    def width(self) -> int:
+        return self.Width()
+
+    @property
+    def originalDataWidth(self) -> int:
+        return int(library().rsm_eds_original_width(self._h))
+
+    @property
+    def shareSize(self) -> int:
+        return int(library().rsm_eds_share_size(self._h))
+
+    # --- cells ---
+    def GetCell(self, rowIdx: int, colIdx: int) -> Optional[bytes]:
+        buf = ctypes.create_string_buffer(max(self.shareSize, 1))
+        rc = library().rsm_eds_get_cell(self._h, rowIdx, colIdx, buf)
+        if rc < 0:
+            raise _err(rc)
+        return buf.raw[: self.shareSize] if rc == 1 else None
+
+    def SetCell(self, rowIdx: int, colIdx: int, newShare: bytes):
+        _check(library().rsm_eds_set_cell(self._h, rowIdx, colIdx, newShare, len(newShare)))
+
+    def setCell(self, rowIdx: int, colIdx: int, newShare: Optional[bytes]):
+        """Test hook mirroring the reference's unexported setCell (datasquare_test.go:735)."""
+        if newShare is None:
+            _check(library().rsm_eds_overwrite_cell(self._h, rowIdx, colIdx, None, 0))
+        else:
+            _check(library().rsm_eds_overwrite_cell(self._h, rowIdx, colIdx, newShare, len(newShare)))
+
+    def Flattened(self) -> List[Optional[bytes]]:
+        w, S = self.Width(), self.shareSize
+        out = ctypes.create_string_buffer(max(w * w * S, 1))
+        pres = ctypes.create_string_buffer(max(w * w, 1))
+        _check(library().rsm_eds_flattened(self._h, out, pres))
+        raw, p = out.raw, pres.raw
+        return [raw[i * S:(i + 1) * S] if p[i] else None for i in range(w * w)]
+
+    def FlattenedODS(self) -> List[Optional[bytes]]:
+        f, w, o = self.Flattened(), self.Width(), self.originalDataWidth
+        return [f[r * w + c] for r in range(o) for c in range(o)]
+
+    def Row(self, rowIdx: int) -> List[Optional[bytes]]:
+        w = self.Width()
+        return [self.GetCell(rowIdx, c) for c in range(w)]
+
+    def Col(self, colIdx: int) -> List[Optional[bytes]]:
+        w = self.Width()
+        return [self.GetCell(r, colIdx) for r in range(w)]
+
+    # --- roots ---
+    def _roots(self, axis: int) -> List[bytes]:
+        w = self.Width()
+        cap = 256
+        out = ctypes.create_string_buffer(max(w * cap, 1))
+        ln = ctypes.c_uint32(0)
+        keep, fn = _tree_callback(self._tree_fn)
+        _check(library().rsm_eds_roots(self._h, axis, fn, None, out, cap, ctypes.byref(ln)))
+        raw = out.raw
+        return [raw[i * cap: i * cap + ln.value] for i in range(w)]
+
+    def RowRoots(self) -> List[bytes]:
+        return self._roots(Row)
+
+    def ColRoots(self) -> List[bytes]:
+        return self._roots(Col)
+
+    def Roots(self) -> List[bytes]:
+        return self.RowRoots() + self.ColRoots()
+
+    # --- Repair (extendeddatacrossword.go:74-84) ---
+    def Repair(self, rowRoots: Sequence[bytes], colRoots: Sequence[bytes]) -> None:
+        L = library()
+        _check(L.rsm_eds_set_context(self._h, device_context(self._device)))
+        root_len = len(rowRoots[0]) if rowRoots else 0
+        rr = b"".join(bytes(r) for r in rowRoots)
+        cr = b"".join(bytes(c) for c in colRoots)
+        byz = _Byz()
+        keep, fn = _tree_callback(self._tree_fn)
+        rc = L.rsm_eds_repair(self._h, rr, cr, root_len, fn, None, ctypes.byref(byz))
+        if rc == RSM_OK:
+            return
+        if rc == RSM_EUNREPAIRABLE:
+            raise ErrUnrepairableDataSquare
+        if rc == RSM_EBYZANTINE:
+            w, S = self.Width(), self.shareSize
+            out = ctypes.create_string_buffer(max(w * S, 1))
+            pres = ctypes.create_string_buffer(max(w, 1))
+            _check(L.rsm_eds_byzantine_shares(self._h, out, pres))
+            raw, p = out.raw, pres.raw
+            raise ErrByzantineData(byz.axis, byz.index, [raw[i * S:(i + 1) * S] if p[i] else None for i in range(w)])
+        raise _err(rc)
+
+    def repair_stats(self) -> RepairStats:
+        st = RepairStats()
+        _check(library().rsm_eds_repair_stats(self._h, ctypes.byref(st)))
+        return st
+
+    # --- equality / JSON ---
+    def Equals(self, other: "ExtendedDataSquare") -> bool:
+        if self.originalDataWidth != other.originalDataWidth:
+            return False
+        if self.codec.Name() != other.codec.Name():
+            return False
+        if self.shareSize != other.shareSize or self.Width() != other.Width():
+            return False
+        return self.Flattened() == other.Flattened()
+
+    def MarshalJSON(self) -> bytes:
+        shares = [None if s is None else base64.b64encode(s).decode() for s in self.Flattened()]
+        return json.dumps({"data_square": shares, "codec": self.codec.Name()}).encode()
+
+    @staticmethod
+    def UnmarshalJSON(b: bytes) -> "ExtendedDataSquare":
+        aux = json.loads(b)
+        shares = [None if s is None else base64.b64decode(s) for s in aux["data_square"]]
+        return ImportExtendedDataSquare(shares, codecs[aux["codec"]], NewDefaultTree)
+
+    def deepCopy(self, codec: Codec) -> "ExtendedDataSquare":
+        return ImportExtendedDataSquare(self.Flattened(), codec, self._tree_fn)
+
+
+def _device_of(codec) -> int:
+    return getattr(codec, "device", 0)
+
+
+def ComputeExtendedDataSquare(data: Sequence[bytes], codec: Codec, treeCreatorFn=NewDefaultTree):
+    """extendeddatasquare.go:50-77 on the GPU."""
+    keep, ptrs, lens = _bufs(data)
+    h = ctypes.c_void_p()
+    _check(library().rsm_eds_compute(device_context(_device_of(codec)), ptrs, lens, len(data), ctypes.byref(h)))
+    return ExtendedDataSquare(h.value, codec, treeCreatorFn, _device_of(codec))
+
+
+def ImportExtendedDataSquare(data: Sequence[Optional[bytes]], codec: Codec, treeCreatorFn=NewDefaultTree):
+    """extendeddatasquare.go:95-124 (host-only; no GPU needed until Repair)."""
+    keep, ptrs, lens = _bufs(data)
+    h = ctypes.c_void_p()
+    _check(library().rsm_eds_import(None, ptrs, lens, len(data), ctypes.byref(h)))
+    return ExtendedDataSquare(h.value, codec, treeCreatorFn, _device_of(codec))
+
+
+def NewExtendedDataSquare(codec: Codec, treeCreatorFn, edsWidth: int, shareSize: int):
+    """extendeddatasquare.go:129-152 (host-only)."""
+    h = ctypes.c_void_p()
+    _check(library().rsm_eds_new(None, edsWidth, shareSize, ctypes.byref(h)))
+    return ExtendedDataSquare(h.value, codec, treeCreatorFn, _device_of(codec))

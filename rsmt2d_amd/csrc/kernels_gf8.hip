@@ -1,0 +1,430 @@
+// kernels_gf8.hip -- CDNA4 (gfx950) Leopard GF(2^8) Reed-Solomon kernels.
+//
+// Replaces the per-codeword klauspost leopard8 encode/reconstruct that rsmt2d's
+// LeoRSCodec calls (leopard.go:28-59) with batched launches over a
+// device-resident extended data square (datasquare.go's grid as one contiguous
+// [W][W][S] HBM buffer, W = 2k).
+//
+// Work decomposition ("wave task"): one wavefront owns one codeword (a row or a
+// column of the square) x one 256-byte chunk of the share width.  Lane l holds
+// byte positions [chunk*256 + 4l, +4) of EVERY symbol of the codeword in
+// registers (u32 = 4 independent GF(2^8) symbols), so all butterflies are
+// lane-local and every lane of the wave applies the same twiddle: the whole
+// additive FFT is unrolled at compile time (template on the power-of-two size
+// M) and each twiddle multiply is a fixed 3 x v_perm_b32 table lookup.  Global
+// loads/stores are one dword per lane per share = 256 contiguous bytes per wave
+// instruction.  No LDS, no cross-lane traffic in the FFT body.
+//
+// Algorithm restated from SURVEY.md Appendix A (klauspost/reedsolomon v1.14.1
+// leopard8.go ifftDITEncoder8/fftDIT8/reconstruct); the radix-4 loop nesting of
+// the reference is rewritten layer-by-layer, which performs the identical
+// butterflies (groups are disjoint), and truncated groups are computed on
+// zero-padding (exact: see DESIGN.md "Truncation").
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <utility>
+#include "gf_tables.hpp"
+#include "rsm_kernels.hpp"
+
+namespace rsm {
+
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    [&]<int... I>(std::integer_sequence<int, I...>) {
+        (f(std::integral_constant<int, I>{}), ...);
+    }(std::make_integer_sequence<int, N>{});
+}
+
+// ---------------------------------------------------------------------------
+// GF(2^8) multiply of 4 packed symbols by the constant exp(L).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // gfx950 v_bitop3_b32: a ^ b ^ c
+}
+
+// A table dword materialised in a VGPR right where it is used.  v_perm_b32 may
+// read only one SGPR (gfx9 constant-bus limit), so one half of each 8-entry
+// table must be a VGPR; left to itself the compiler hoists all ~250 distinct
+// constants to the kernel entry and runs out of registers.
+template <uint32_t C>
+__device__ __forceinline__ uint32_t vconst() {
+    uint32_t v;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "i"(C));
+    return v;
+}
+
+// x ^= y * exp(L)
+template <unsigned L>
+__device__ __forceinline__ void gf8_muladd_ct(uint32_t& x, uint32_t y) {
+    constexpr PermTab t = make_perm_tab(L);
+    const uint32_t sa = y & 0x07070707u;
+    const uint32_t sb = (y >> 3) & 0x07070707u;
+    const uint32_t sc = (y >> 6) & 0x03030303u;
+    x = xor3(x, __builtin_amdgcn_perm(t.a_hi, vconst<t.a_lo>(), sa),
+             __builtin_amdgcn_perm(t.b_hi, vconst<t.b_lo>(), sb)) ^
+        __builtin_amdgcn_perm(t.c, t.c, sc);
+}
+
+// Runtime (wave-uniform) log constant: tables for all 256 logs in constant memory.
+struct PermTabAll {
+    PermTab t[256];
+};
+constexpr PermTabAll make_perm_all() {
+    PermTabAll a{};
+    for (unsigned L = 0; L < 256; ++L) a.t[L] = make_perm_tab(L);
+    return a;
+}
+__constant__ PermTabAll d_perm8 = make_perm_all();
+__constant__ Gf8Tables d_gf8 = kGf8;
+
+// Pins a wave-uniform value to an SGPR at this point of the program; used so the
+// per-symbol constant-memory table loads below are issued where they are needed
+// instead of all being hoisted to the kernel entry (hundreds of SGPRs).
+__device__ __forceinline__ uint32_t pin_sgpr(uint32_t x) {
+    asm volatile("; pin %0" : "+s"(x));
+    return x;
+}
+
+__device__ __forceinline__ uint32_t gf8_mul_rt(uint32_t y, unsigned L) {
+    const PermTab t = d_perm8.t[pin_sgpr(L)];
+    const uint32_t sa = y & 0x07070707u;
+    const uint32_t sb = (y >> 3) & 0x07070707u;
+    const uint32_t sc = (y >> 6) & 0x03030303u;
+    return xor3(__builtin_amdgcn_perm(t.a_hi, t.a_lo, sa), __builtin_amdgcn_perm(t.b_hi, t.b_lo, sb),
+                __builtin_amdgcn_perm(t.c, t.c, sc));
+}
+
+// IFFT_DIT2 (y ^= x; x ^= y*L) and FFT_DIT2 (x ^= y*L; y ^= x); L == 255 means
+// a zero twiddle: XOR half only (klauspost ifftDIT4/fftDIT4 "log_m == modulus").
+template <unsigned L>
+__device__ __forceinline__ void ifft2(uint32_t& x, uint32_t& y) {
+    y ^= x;
+    if constexpr (L != 255u) gf8_muladd_ct<L>(x, y);
+}
+template <unsigned L>
+__device__ __forceinline__ void fft2(uint32_t& x, uint32_t& y) {
+    if constexpr (L != 255u) gf8_muladd_ct<L>(x, y);
+    y ^= x;
+}
+
+// Inverse transform over N points, layer d = 1, 2, ..., N/2; block b uses
+// SKEW[OFF + b + d]  (encoder: OFF = m - 1; decoder: OFF = -1).
+template <int N, int OFF>
+__device__ __forceinline__ void ifft_layers(uint32_t (&w)[N]) {
+    static_for<16>([&](auto LG) {
+        constexpr int lg = decltype(LG)::value;
+        if constexpr ((1 << lg) < N) {
+            constexpr int d = 1 << lg;
+            static_for<N / 2>([&](auto Q) {
+                constexpr int q = decltype(Q)::value;
+                constexpr int b = (q / d) * 2 * d;
+                constexpr int i = b + (q % d);
+                constexpr unsigned L = kGf8.skew[OFF + b + d];
+                ifft2<L>(w[i], w[i + d]);
+            });
+        }
+    });
+}
+
+// Forward transform, layer d = N/2, ..., 1; block b uses SKEW[OFF + b + d]
+// (full transforms: OFF = -1; upper half of a 2N-point decoder transform: OFF = N - 1).
+template <int N, int OFF = -1>
+__device__ __forceinline__ void fft_layers(uint32_t (&w)[N]) {
+    static_for<16>([&](auto LG) {
+        constexpr int lg = 15 - decltype(LG)::value;
+        if constexpr ((1 << lg) < N) {
+            constexpr int d = 1 << lg;
+            static_for<N / 2>([&](auto Q) {
+                constexpr int q = decltype(Q)::value;
+                constexpr int b = (q / d) * 2 * d;
+                constexpr int i = b + (q % d);
+                constexpr unsigned L = kGf8.skew[OFF + b + d];
+                fft2<L>(w[i], w[i + d]);
+            });
+        }
+    });
+}
+
+__device__ __forceinline__ uint64_t cw_rel(const CodewordSet& cs, uint32_t q) {
+    if (cs.indices != nullptr) return (uint64_t)cs.indices[q] * cs.cw_stride;
+    const uint32_t sq = q / cs.per_square;
+    const uint32_t t = q - sq * cs.per_square;
+    return (uint64_t)sq * cs.square_stride + (uint64_t)t * cs.cw_stride;
+}
+
+// Offsets at or beyond kOob are out of range for every buffer resource below:
+// loads there return 0 and stores are dropped, so inactive lanes / padded symbols
+// need no exec-mask branches.
+constexpr uint32_t kOob = 0x80000000u;
+
+// Buffer resource over a wave-uniform base: 32-bit per-lane voffset + SGPR soffset
+// per symbol keeps address arithmetic off the VGPR file (guide T8/T20).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p) {
+    const uint64_t a = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    void* u = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(u, (short)0, (int)kOob, 0x00020000);
+}
+
+// ---------------------------------------------------------------------------
+// Encode: k data symbols -> k parity symbols per byte position, for every
+// codeword of a CodewordSet.  M = ceilPow2(k).
+// ---------------------------------------------------------------------------
+template <int M>
+__global__ __launch_bounds__(256, (M >= 128 ? 2 : 3)) void encode_gf8_kernel(CodewordSet cs) {
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t chunks = cs.chunks;
+    if (wave >= cs.count * chunks) return;
+    const uint32_t q = wave / chunks;
+    const uint32_t chunk = wave - q * chunks;
+    const uint32_t off0 = chunk * 256u + lane * 4u;
+    const uint32_t off = off0 < cs.S ? off0 : kOob;
+    const uint64_t rel = cw_rel(cs, q);
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(cs.base + rel);
+    const __amdgpu_buffer_rsrc_t ro = make_rsrc(cs.out_base + rel);
+    const uint32_t k = cs.k;
+    const uint32_t es = (uint32_t)cs.elem_stride;
+
+    uint32_t w[M];
+    static_for<M>([&](auto E) {
+        constexpr int e = decltype(E)::value;
+        w[e] = __builtin_amdgcn_raw_buffer_load_b32(rs, off, e < (int)k ? e * es : kOob, 0);
+    });
+    if constexpr (M > 1) {
+        ifft_layers<M, M - 1>(w);
+        fft_layers<M>(w);
+    }
+    const uint32_t oo = (uint32_t)cs.out_offset;
+    static_for<M>([&](auto E) {
+        constexpr int e = decltype(E)::value;
+        __builtin_amdgcn_raw_buffer_store_b32(w[e], ro, off, e < (int)k ? oo + e * es : kOob, 0);
+    });
+}
+
+// ---------------------------------------------------------------------------
+// Decode (reconstruct, recoverAll): fills every missing symbol of the listed
+// codewords in place.  Element e of codeword q: e < k data, k <= e < 2k parity.
+// presence: byte per cell of the square ([W][W], non-zero = present).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t addmod8(uint32_t a, uint32_t b) {
+    uint32_t s = a + b;
+    return (s + (s >> 8)) & 255u;
+}
+__device__ __forceinline__ uint32_t submod8(uint32_t a, uint32_t b) {
+    uint32_t d = a - b;
+    return (d + (d >> 8)) & 255u;
+}
+
+// FWHT over 256 log-domain entries held 4 per lane (entry 4*lane + j in e[j]).
+__device__ __forceinline__ void fwht256(uint32_t (&e)[4], uint32_t lane) {
+    // dist 1, 2 inside the lane
+    {
+        uint32_t a0 = addmod8(e[0], e[1]), a1 = submod8(e[0], e[1]);
+        uint32_t a2 = addmod8(e[2], e[3]), a3 = submod8(e[2], e[3]);
+        e[0] = addmod8(a0, a2); e[2] = submod8(a0, a2);
+        e[1] = addmod8(a1, a3); e[3] = submod8(a1, a3);
+    }
+    // dist 4..128 across lanes (partner lane = lane ^ (dist/4))
+#pragma unroll
+    for (int ld = 0; ld < 6; ++ld) {
+        const uint32_t mask = 1u << ld;
+        const bool upper = (lane & mask) != 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t p = __shfl_xor(e[j], (int)mask, 64);
+            e[j] = upper ? submod8(p, e[j]) : addmod8(e[j], p);
+        }
+    }
+}
+
+// Formal derivative restricted to one half (size H) of the 2H-point decoder
+// transform: out[j] = in[j] ^ XOR_{t: bit t of j == 0, j + 2^t < H} in[j + 2^t].
+// (The sequential reference loop, extendeddatacrossword -> leopard reconstruct
+// "work <- FormalDerivative(work, n)", reads only not-yet-updated elements, so it
+// equals this closed form; the 2^log2(H) cross-half term is added separately.)
+template <int H>
+__device__ __forceinline__ void derivative_half(uint32_t (&w)[H]) {
+    static_for<H>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        static_for<16>([&](auto T) {
+            constexpr int t = decltype(T)::value;
+            if constexpr ((1 << t) < H && ((j >> t) & 1) == 0 && j + (1 << t) < H) w[j] ^= w[j + (1 << t)];
+        });
+    });
+}
+
+// One wavefront per (codeword, 256-byte chunk).  The n = 2m point decoder
+// transform is run as two m-point halves: layers below m stay inside a half, so
+// only one half lives in registers at a time and the other is parked in LDS
+// (m x 64 dwords, lane-major: conflict-free).
+template <int M>
+__global__ __launch_bounds__(64) void decode_gf8_kernel(DecodeSet ds) {
+    __shared__ uint32_t park[M][64];
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t chunks = ds.chunks;
+    if (wave >= ds.count * chunks) return;
+    const uint32_t qi = wave / chunks;
+    const uint32_t chunk = wave - qi * chunks;
+    const uint32_t k = ds.k;
+    const uint32_t W = 2u * k;
+    const uint32_t vec = ds.indices[qi];
+    // element e lives at cell (r, c): row vector -> (vec, e); col vector -> (e, vec)
+    const uint64_t cell0 = ds.axis == 0 ? (uint64_t)vec * W : (uint64_t)vec;
+    const uint64_t cell_step = ds.axis == 0 ? 1u : (uint64_t)W;
+
+    // --- presence of the 2k elements as 64-bit ballots (wave-uniform) ---
+    uint64_t pres[(2 * M + 63) / 64];
+#pragma unroll
+    for (int g = 0; g < (2 * M + 63) / 64; ++g) {
+        const uint32_t e = g * 64u + lane;
+        const bool p = e < W && ds.presence[cell0 + e * cell_step] != 0;
+        pres[g] = __ballot(p);
+    }
+    auto present = [&](uint32_t e) -> bool { return (pres[e >> 6] >> (e & 63u)) & 1u; };
+
+    // --- error locator (log domain), klauspost reconstruct: lane holds entries
+    //     4*lane .. 4*lane+3 of the 256-entry table ---
+    uint32_t er[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t i = lane * 4u + j;
+        uint32_t v = 0;
+        if (i < k) v = present(k + i) ? 0u : 1u;                     // parity i missing
+        else if (i < (uint32_t)M) v = 1u;                            // recovery padding
+        else if (i < (uint32_t)M + k) v = present(i - M) ? 0u : 1u;  // data i-M missing
+        er[j] = v;
+    }
+    fwht256(er, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) er[j] = (er[j] * d_gf8.logwalsh[lane * 4u + j]) % 255u;
+    fwht256(er, lane);
+    const uint32_t er_packed = er[0] | (er[1] << 8) | (er[2] << 16) | (er[3] << 24);
+    auto err_at = [&](int i) -> uint32_t {
+        const uint32_t v = __builtin_amdgcn_readlane(er_packed, i >> 2);
+        return (v >> (8 * (i & 3))) & 255u;
+    };
+
+    const uint32_t off0 = chunk * 256u + lane * 4u;
+    const uint32_t off = off0 < ds.S ? off0 : kOob;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(ds.base);
+    auto soff = [&](uint32_t e) -> uint32_t { return pin_sgpr((uint32_t)((cell0 + (uint64_t)e * cell_step) * ds.S)); };
+    auto st = [&](uint32_t e, uint32_t v) { __builtin_amdgcn_raw_buffer_store_b32(v, rs, off, soff(e), 0); };
+
+    constexpr unsigned LM = kGf8.skew[M - 1];  // twiddle of the layer joining the halves
+    uint32_t w[M];
+
+    // 1. upper half: original data, scaled by the error locator; IFFT layers < M
+    static_for<M>([&](auto E) {
+        constexpr int e = decltype(E)::value;
+        w[e] = __builtin_amdgcn_raw_buffer_load_b32(rs, off, ((uint32_t)e < k && present(e)) ? soff(e) : kOob, 0);
+    });
+    static_for<M>([&](auto E) {
+        constexpr int e = decltype(E)::value;
+        if ((uint32_t)e < k && present(e)) w[e] = gf8_mul_rt(w[e], err_at(M + e));
+    });
+    ifft_layers<M, M - 1>(w);
+    static_for<M>([&](auto E) { park[decltype(E)::value][lane] = w[decltype(E)::value]; });
+
+    // 2. lower half: recovery (parity) data; IFFT layers < M
+    static_for<M>([&](auto E) {
+        constexpr int e = decltype(E)::value;
+        w[e] = __builtin_amdgcn_raw_buffer_load_b32(rs, off, ((uint32_t)e < k && present(k + e)) ? soff(k + e) : kOob, 0);
+    });
+    static_for<M>([&](auto E) {
+        constexpr int e = decltype(E)::value;
+        if ((uint32_t)e < k && present(k + e)) w[e] = gf8_mul_rt(w[e], err_at(e));
+    });
+    ifft_layers<M, -1>(w);
+
+    // 3. IFFT layer M (pairs i, i+M), then derivative of the lower half plus the
+    //    cross-half term x[j + M].
+    static_for<M>([&](auto E) {
+        constexpr int i = decltype(E)::value;
+        uint32_t bv = park[i][lane];
+        ifft2<LM>(w[i], bv);
+        park[i][lane] = bv;
+    });
+    derivative_half<M>(w);
+    static_for<M>([&](auto E) {
+        constexpr int i = decltype(E)::value;
+        const uint32_t bv = park[i][lane];
+        w[i] ^= bv;
+        park[i][lane] = w[i];  // park the finished lower half ...
+        w[i] = bv;             // ... and bring the upper half into registers
+    });
+
+    // 4. derivative of the upper half; FFT layer M; FFT layers < M of the upper half
+    derivative_half<M>(w);
+    static_for<M>([&](auto E) {
+        constexpr int i = decltype(E)::value;
+        uint32_t av = park[i][lane];
+        fft2<LM>(av, w[i]);
+        park[i][lane] = av;
+    });
+    fft_layers<M, M - 1>(w);
+    static_for<M>([&](auto E) {
+        constexpr int e = decltype(E)::value;
+        if ((uint32_t)e < k && !present(e)) st(e, gf8_mul_rt(w[e], 255u - err_at(M + e)));
+    });
+
+    // 5. lower half: FFT layers < M, reveal missing parity
+    static_for<M>([&](auto E) { w[decltype(E)::value] = park[decltype(E)::value][lane]; });
+    fft_layers<M, -1>(w);
+    static_for<M>([&](auto E) {
+        constexpr int e = decltype(E)::value;
+        if ((uint32_t)e < k && !present(k + e)) st(k + e, gf8_mul_rt(w[e], 255u - err_at(e)));
+    });
+}
+
+// ---------------------------------------------------------------------------
+// Host launchers
+// ---------------------------------------------------------------------------
+template <int M>
+static hipError_t launch_enc(const CodewordSet& cs, hipStream_t st) {
+    const uint64_t tasks = (uint64_t)cs.count * cs.chunks;
+    const uint32_t blocks = (uint32_t)((tasks + 3) / 4);
+    if (blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(encode_gf8_kernel<M>, dim3(blocks), dim3(256), 0, st, cs);
+    return hipGetLastError();
+}
+
+hipError_t launch_encode_gf8(const CodewordSet& cs, hipStream_t st) {
+    switch (ceil_pow2(cs.k)) {
+        case 1: return launch_enc<1>(cs, st);
+        case 2: return launch_enc<2>(cs, st);
+        case 4: return launch_enc<4>(cs, st);
+        case 8: return launch_enc<8>(cs, st);
+        case 16: return launch_enc<16>(cs, st);
+        case 32: return launch_enc<32>(cs, st);
+        case 64: return launch_enc<64>(cs, st);
+        case 128: return launch_enc<128>(cs, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+template <int M>
+static hipError_t launch_dec(const DecodeSet& ds, hipStream_t st) {
+    const uint64_t tasks = (uint64_t)ds.count * ds.chunks;
+    if (tasks == 0) return hipSuccess;
+    hipLaunchKernelGGL(decode_gf8_kernel<M>, dim3((uint32_t)tasks), dim3(64), 0, st, ds);
+    return hipGetLastError();
+}
+
+hipError_t launch_decode_gf8(const DecodeSet& ds, hipStream_t st) {
+    switch (ceil_pow2(ds.k)) {
+        case 1: return launch_dec<1>(ds, st);
+        case 2: return launch_dec<2>(ds, st);
+        case 4: return launch_dec<4>(ds, st);
+        case 8: return launch_dec<8>(ds, st);
+        case 16: return launch_dec<16>(ds, st);
+        case 32: return launch_dec<32>(ds, st);
+        case 64: return launch_dec<64>(ds, st);
+        case 128: return launch_dec<128>(ds, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace rsm

@@ -1,0 +1,64 @@
+// kernels_util.hip -- small device helpers for the Repair fast path.
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include "rsm_kernels.hpp"
+
+namespace rsm {
+
+// *mismatch |= any(a[i] != b[i]) over n bytes (n multiple of 16): the on-device
+// form of verifyEncoding's bytes.Equal (extendeddatacrossword.go:496-500).
+__global__ __launch_bounds__(256) void compare_kernel(const uint4* a, const uint4* b, uint64_t n16,
+                                                      uint32_t* mismatch) {
+    uint32_t diff = 0;
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * 256ull) {
+        const uint4 x = a[i], y = b[i];
+        diff |= (x.x ^ y.x) | (x.y ^ y.y) | (x.z ^ y.z) | (x.w ^ y.w);
+    }
+    if (__any(diff != 0) && (threadIdx.x & 63u) == 0) atomicOr(mismatch, 1u);
+}
+
+hipError_t launch_compare(const uint8_t* a, const uint8_t* b, uint64_t n, uint32_t* mismatch,
+                          hipStream_t st) {
+    const uint64_t n16 = n / 16;
+    if (n16 == 0) return hipSuccess;
+    uint64_t blocks = (n16 + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(compare_kernel, dim3((uint32_t)blocks), dim3(256), 0, st,
+                       reinterpret_cast<const uint4*>(a), reinterpret_cast<const uint4*>(b), n16, mismatch);
+    return hipGetLastError();
+}
+
+// flags[q] = 1 iff the parity half (cells k..2k-1) of vector indices[q] differs
+// between squares a and b (both [W][W][S]); one block per listed vector.
+__global__ __launch_bounds__(256) void compare_parity_kernel(const uint8_t* a, const uint8_t* b, uint32_t k,
+                                                             uint32_t S, uint32_t axis, const uint32_t* indices,
+                                                             uint32_t* flags) {
+    const uint32_t q = blockIdx.x;
+    const uint64_t W = 2ull * k;
+    const uint64_t vec = indices[q];
+    const uint32_t per_cell = S / 16;
+    uint32_t diff = 0;
+    for (uint32_t t = threadIdx.x; t < k * per_cell; t += 256) {
+        const uint64_t e = k + t / per_cell;
+        const uint64_t cell = axis == 0 ? vec * W + e : e * W + vec;
+        const uint64_t off = cell * S + (uint64_t)(t % per_cell) * 16;
+        const uint4 x = *reinterpret_cast<const uint4*>(a + off);
+        const uint4 y = *reinterpret_cast<const uint4*>(b + off);
+        diff |= (x.x ^ y.x) | (x.y ^ y.y) | (x.z ^ y.z) | (x.w ^ y.w);
+    }
+    __shared__ uint32_t any;
+    if (threadIdx.x == 0) any = 0;
+    __syncthreads();
+    if (diff) atomicOr(&any, 1u);
+    __syncthreads();
+    if (threadIdx.x == 0) flags[q] = any;
+}
+
+hipError_t launch_compare_parity(const uint8_t* a, const uint8_t* b, uint32_t k, uint32_t S, uint32_t axis,
+                                 const uint32_t* indices, uint32_t count, uint32_t* flags, hipStream_t st) {
+    if (count == 0) return hipSuccess;
+    hipLaunchKernelGGL(compare_parity_kernel, dim3(count), dim3(256), 0, st, a, b, k, S, axis, indices, flags);
+    return hipGetLastError();
+}
+
+}  // namespace rsm

@@ -1,0 +1,57 @@
+// rsm_kernels.hpp -- descriptors shared by the HIP kernels and the host runtime.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace rsm {
+
+__host__ __device__ constexpr uint32_t ceil_pow2(uint32_t x) {
+    uint32_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+// A batch of codewords laid out affinely in device memory.  Codeword q lives in
+// square q / per_square at offset (q % per_square) * cw_stride; its input
+// symbol e (e < k) is the share at + e * elem_stride, its parity symbol e at
+// + out_offset + e * elem_stride.  Rows of a [W][W][S] square:
+//   cw_stride = W*S, elem_stride = S,   out_offset = k*S
+// Columns:
+//   cw_stride = S,   elem_stride = W*S, out_offset = k*W*S
+struct CodewordSet {
+    uint8_t* base;
+    uint8_t* out_base;          // parity written at the same relative offsets from here
+    const uint32_t* indices;    // optional: codeword q is vector indices[q] of square 0
+    uint64_t square_stride;
+    uint64_t cw_stride;
+    uint64_t elem_stride;
+    uint64_t out_offset;
+    uint32_t per_square;
+    uint32_t count;   // total codewords
+    uint32_t k;
+    uint32_t S;       // share size in bytes (multiple of 64)
+    uint32_t chunks;  // ceil(S / bytes-per-wave)
+};
+
+// A list of row (axis 0) or column (axis 1) vectors of ONE [W][W][S] square to
+// reconstruct in place; presence is one byte per cell (non-zero = present).
+struct DecodeSet {
+    uint8_t* base;
+    const uint8_t* presence;
+    const uint32_t* indices;
+    uint32_t count;
+    uint32_t axis;
+    uint32_t k;
+    uint32_t S;
+    uint32_t chunks;
+};
+
+hipError_t launch_encode_gf8(const CodewordSet& cs, hipStream_t st);
+hipError_t launch_decode_gf8(const DecodeSet& ds, hipStream_t st);
+hipError_t launch_encode_gf16(const CodewordSet& cs, hipStream_t st);
+hipError_t launch_decode_gf16(const DecodeSet& ds, hipStream_t st);
+hipError_t launch_compare(const uint8_t* a, const uint8_t* b, uint64_t n, uint32_t* mismatch, hipStream_t st);
+hipError_t launch_compare_parity(const uint8_t* a, const uint8_t* b, uint32_t k, uint32_t S, uint32_t axis,
+                                 const uint32_t* indices, uint32_t count, uint32_t* flags, hipStream_t st);
+
+}  // namespace rsm

@@ -1,0 +1,342 @@
+// rsm_runtime.cpp -- context, device memory and the Codec half of the C ABI.
+//
+// The HIP kernels are the only compute path: every entry point that needs
+// arithmetic fails with RSM_EDEVICE when no GPU/HIP runtime is usable; there is
+// no CPU fallback anywhere in the product.
+#include "rsm_internal.hpp"
+
+#include <cstdio>
+#include <cstring>
+#include <cstdarg>
+
+namespace rsm {
+
+static thread_local std::string g_last_error;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    return fail(RSM_EDEVICE, "%s: %s", what, hipGetErrorString(e));
+}
+
+const char* last_error() { return g_last_error.c_str(); }
+
+DevBuf::~DevBuf() {
+    if (ptr) (void)hipFree(ptr);
+}
+hipError_t DevBuf::ensure(size_t n) {
+    if (n <= cap) return hipSuccess;
+    if (ptr) {
+        (void)hipFree(ptr);
+        ptr = nullptr;
+        cap = 0;
+    }
+    hipError_t e = hipMalloc(&ptr, n);
+    if (e == hipSuccess) cap = n;
+    return e;
+}
+
+HostBuf::~HostBuf() {
+    if (ptr) (void)hipHostFree(ptr);
+}
+hipError_t HostBuf::ensure(size_t n) {
+    if (n <= cap) return hipSuccess;
+    if (ptr) {
+        (void)hipHostFree(ptr);
+        ptr = nullptr;
+        cap = 0;
+    }
+    hipError_t e = hipHostMalloc(&ptr, n, hipHostMallocDefault);
+    if (e == hipSuccess) cap = n;
+    return e;
+}
+
+int validate_chunk_size(int64_t share_size) {
+    if (share_size % 64 != 0)
+        return fail(RSM_ESHARESIZE, "shareSize %lld must be a multiple of 64 bytes", (long long)share_size);
+    return RSM_OK;
+}
+
+int field_bits(uint32_t k) { return 2ull * k > 256ull ? 16 : 8; }
+
+// ---------------------------------------------------------------------------
+// Launch helpers (device-resident, asynchronous on `st`)
+// ---------------------------------------------------------------------------
+static uint32_t bytes_per_wave(uint32_t k) { return field_bits(k) == 8 ? 256u : kGf16BytesPerWave; }
+
+int launch_encode(const CodewordSet& cs0, hipStream_t st) {
+    CodewordSet cs = cs0;
+    if (cs.out_base == nullptr) cs.out_base = cs.base;
+    cs.chunks = (cs.S + bytes_per_wave(cs.k) - 1) / bytes_per_wave(cs.k);
+    hipError_t e = field_bits(cs.k) == 8 ? launch_encode_gf8(cs, st) : launch_encode_gf16(cs, st);
+    if (e == hipErrorNotSupported) return fail(RSM_EUNSUPPORTED, "encode: k=%u (GF16) not supported in this build", cs.k);
+    if (e != hipSuccess) return hip_fail(e, "encode kernel launch");
+    return RSM_OK;
+}
+
+int launch_decode(const DecodeSet& ds0, hipStream_t st) {
+    DecodeSet ds = ds0;
+    ds.chunks = (ds.S + bytes_per_wave(ds.k) - 1) / bytes_per_wave(ds.k);
+    hipError_t e = field_bits(ds.k) == 8 ? launch_decode_gf8(ds, st) : launch_decode_gf16(ds, st);
+    if (e == hipErrorNotSupported) return fail(RSM_EUNSUPPORTED, "decode: k=%u (GF16) not supported in this build", ds.k);
+    if (e != hipSuccess) return hip_fail(e, "decode kernel launch");
+    return RSM_OK;
+}
+
+// Two-phase in-place extension of `count` squares (extendeddatasquare.go:154-227):
+//   phase 1: every row r < k: Q0 row -> Q1 row            (erasureExtendRow)
+//   phase 2: every column c < 2k: [Q0|Q1] column -> [Q2|Q3] column
+// Phase 2 computes Q2 exactly as erasureExtendCol and Q3 by column-encoding Q1,
+// which equals the reference's row-encoding of Q2 by linearity of the 2D code
+// (extendeddatasquare.go:204-207; asserted in tests against the oracle, which
+// runs the reference order).
+int extend_squares(uint8_t* d_eds, uint32_t k, uint32_t S, uint32_t count, hipStream_t st, int phases) {
+    const uint64_t W = 2ull * k;
+    CodewordSet rows{};
+    rows.base = d_eds;
+    rows.square_stride = W * W * S;
+    rows.cw_stride = W * S;
+    rows.elem_stride = S;
+    rows.out_offset = (uint64_t)k * S;
+    rows.per_square = k;
+    rows.count = k * count;
+    rows.k = k;
+    rows.S = S;
+    if (phases & 1) {
+        int rc = launch_encode(rows, st);
+        if (rc) return rc;
+    }
+    if (!(phases & 2)) return RSM_OK;
+    CodewordSet cols{};
+    cols.base = d_eds;
+    cols.square_stride = W * W * S;
+    cols.cw_stride = S;
+    cols.elem_stride = W * S;
+    cols.out_offset = (uint64_t)k * W * S;
+    cols.per_square = (uint32_t)W;
+    cols.count = (uint32_t)W * count;
+    cols.k = k;
+    cols.S = S;
+    return launch_encode(cols, st);
+}
+
+}  // namespace rsm
+
+using namespace rsm;
+
+// ---------------------------------------------------------------------------
+// C ABI: context
+// ---------------------------------------------------------------------------
+extern "C" {
+
+const char* rsm_last_error(void) { return last_error(); }
+const char* rsm_version(void) { return "rsmt2d-mi355x 0.1.0 (gfx950)"; }
+
+int rsm_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int rsm_ctx_create(int device, rsm_ctx** out) {
+    if (!out) return fail(RSM_EINVAL, "rsm_ctx_create: out is NULL");
+    *out = nullptr;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0)
+        return fail(RSM_EDEVICE, "no HIP device available (%s): the MI355X path has no CPU fallback",
+                    e == hipSuccess ? "0 devices" : hipGetErrorString(e));
+    if (device < 0 || device >= n) return fail(RSM_EINVAL, "device %d out of range [0,%d)", device, n);
+    e = hipSetDevice(device);
+    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    auto* c = new (std::nothrow) rsm_ctx();
+    if (!c) return fail(RSM_ENOMEM, "rsm_ctx_create: out of memory");
+    c->device = device;
+    e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete c;
+        return hip_fail(e, "hipStreamCreate");
+    }
+    *out = c;
+    return RSM_OK;
+}
+
+void rsm_ctx_destroy(rsm_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    ctx->bufs.clear();
+    (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+// ---------------------------------------------------------------------------
+// C ABI: Codec
+// ---------------------------------------------------------------------------
+const char* rsm_codec_name(void) { return "Leopard"; }
+int64_t rsm_codec_max_chunks(void) { return (int64_t)32768 * 32768; }
+int rsm_codec_validate_chunk_size(int64_t share_size) { return validate_chunk_size(share_size); }
+int rsm_codec_field_bits(uint32_t k) { return field_bits(k); }
+
+int rsm_encode(rsm_ctx* ctx, const uint8_t* const* data, uint32_t k, uint32_t share_size,
+               uint8_t* const* parity) {
+    if (!ctx || !data || !parity || k == 0) return fail(RSM_EINVAL, "rsm_encode: bad arguments");
+    if (int rc = validate_chunk_size(share_size)) return rc;
+    if (share_size == 0) return fail(RSM_ESHAPE, "rsm_encode: zero-length shares");
+    if (2ull * k > 65536ull) return fail(RSM_ESHAPE, "rsm_encode: %u shards exceed the Leopard limit", 2 * k);
+    for (uint32_t i = 0; i < k; ++i)
+        if (!data[i]) return fail(RSM_EINVAL, "rsm_encode: data[%u] is nil", i);
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    const size_t S = share_size;
+    const size_t bytes = 2ull * k * S;
+    HostBuf& hb = ctx->host_buf(0);
+    DevBuf& db = ctx->dev_buf(0);
+    if ((e = hb.ensure(bytes)) != hipSuccess) return hip_fail(e, "hipHostMalloc");
+    if ((e = db.ensure(bytes)) != hipSuccess) return hip_fail(e, "hipMalloc");
+    uint8_t* h = static_cast<uint8_t*>(hb.ptr);
+    for (uint32_t i = 0; i < k; ++i) memcpy(h + i * S, data[i], S);
+    uint8_t* d = static_cast<uint8_t*>(db.ptr);
+    if ((e = hipMemcpyAsync(d, h, k * S, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess)
+        return hip_fail(e, "hipMemcpyAsync H2D");
+    CodewordSet cs{};
+    cs.base = d;
+    cs.square_stride = 0;
+    cs.cw_stride = 0;
+    cs.elem_stride = S;
+    cs.out_offset = (uint64_t)k * S;
+    cs.per_square = 1;
+    cs.count = 1;
+    cs.k = k;
+    cs.S = share_size;
+    if (int rc = launch_encode(cs, ctx->stream)) return rc;
+    if ((e = hipMemcpyAsync(h + k * S, d + k * S, k * S, hipMemcpyDeviceToHost, ctx->stream)) != hipSuccess)
+        return hip_fail(e, "hipMemcpyAsync D2H");
+    if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return hip_fail(e, "encode");
+    for (uint32_t i = 0; i < k; ++i) memcpy(parity[i], h + (k + i) * S, S);
+    return RSM_OK;
+}
+
+int rsm_decode(rsm_ctx* ctx, uint8_t* const* shares, const uint8_t* present, uint32_t n,
+               uint32_t share_size) {
+    if (!ctx || !shares || !present || n == 0 || (n & 1u)) return fail(RSM_EINVAL, "rsm_decode: bad arguments");
+    if (int rc = validate_chunk_size(share_size)) return rc;
+    const uint32_t k = n / 2;
+    uint32_t np = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (!shares[i]) return fail(RSM_EINVAL, "rsm_decode: shares[%u] buffer is NULL", i);
+        np += present[i] ? 1u : 0u;
+    }
+    if (np == n) return RSM_OK;
+    if (np < k) return fail(RSM_ETOOFEW, "too few shards given (%u of %u, need %u)", np, n, k);
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    const size_t S = share_size;
+    const size_t bytes = (size_t)n * S;
+    HostBuf& hb = ctx->host_buf(0);
+    DevBuf& db = ctx->dev_buf(0);
+    DevBuf& dp = ctx->dev_buf(1);
+    if ((e = hb.ensure(bytes + n + 16)) != hipSuccess) return hip_fail(e, "hipHostMalloc");
+    if ((e = db.ensure(bytes)) != hipSuccess) return hip_fail(e, "hipMalloc");
+    if ((e = dp.ensure(n + 16)) != hipSuccess) return hip_fail(e, "hipMalloc");
+    uint8_t* h = static_cast<uint8_t*>(hb.ptr);
+    for (uint32_t i = 0; i < n; ++i) {
+        if (present[i]) memcpy(h + i * S, shares[i], S);
+        else memset(h + i * S, 0, S);
+    }
+    uint8_t* hp = h + bytes;
+    for (uint32_t i = 0; i < n; ++i) hp[i] = present[i] ? 1 : 0;
+    uint32_t* hidx = reinterpret_cast<uint32_t*>(hp + ((n + 3) & ~3u));
+    (void)hidx;
+    uint8_t* d = static_cast<uint8_t*>(db.ptr);
+    uint8_t* dpres = static_cast<uint8_t*>(dp.ptr);
+    if ((e = hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess)
+        return hip_fail(e, "hipMemcpyAsync H2D");
+    if ((e = hipMemcpyAsync(dpres, hp, n, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess)
+        return hip_fail(e, "hipMemcpyAsync H2D");
+    DecodeSet ds{};
+    ds.base = d;
+    ds.presence = dpres;
+    ds.indices = ctx->zero_index();
+    ds.count = 1;
+    ds.axis = 0;  // a single codeword is row 0 of a 1 x 2k "square"
+    ds.k = k;
+    ds.S = share_size;
+    if (!ds.indices) return fail(RSM_EDEVICE, "rsm_decode: index buffer allocation failed");
+    if (int rc = launch_decode(ds, ctx->stream)) return rc;
+    if ((e = hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, ctx->stream)) != hipSuccess)
+        return hip_fail(e, "hipMemcpyAsync D2H");
+    if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return hip_fail(e, "decode");
+    for (uint32_t i = 0; i < n; ++i)
+        if (!present[i]) memcpy(shares[i], h + i * S, S);
+    return RSM_OK;
+}
+
+int rsm_extend_square(rsm_ctx* ctx, const uint8_t* ods, uint32_t k, uint32_t share_size, uint8_t* eds) {
+    if (!ctx || !ods || !eds || k == 0) return fail(RSM_EINVAL, "rsm_extend_square: bad arguments");
+    if (int rc = validate_chunk_size(share_size)) return rc;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    const size_t S = share_size, W = 2ull * k;
+    DevBuf& db = ctx->dev_buf(0);
+    if ((e = db.ensure(W * W * S)) != hipSuccess) return hip_fail(e, "hipMalloc");
+    uint8_t* d = static_cast<uint8_t*>(db.ptr);
+    // Q0 straight into the top-left quadrant: the EDS aliases the ODS.
+    if ((e = hipMemcpy2DAsync(d, W * S, ods, k * S, k * S, k, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess)
+        return hip_fail(e, "hipMemcpy2DAsync H2D");
+    if (int rc = extend_squares(d, k, share_size, 1, ctx->stream)) return rc;
+    if ((e = hipMemcpyAsync(eds, d, W * W * S, hipMemcpyDeviceToHost, ctx->stream)) != hipSuccess)
+        return hip_fail(e, "hipMemcpyAsync D2H");
+    if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return hip_fail(e, "extend");
+    return RSM_OK;
+}
+
+int rsm_extend_squares_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size, uint32_t count,
+                           void* stream) {
+    if (!ctx || !d_eds || k == 0) return fail(RSM_EINVAL, "rsm_extend_squares_dev: bad arguments");
+    if (int rc = validate_chunk_size(share_size)) return rc;
+    if (count == 0) return RSM_OK;
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    return extend_squares(static_cast<uint8_t*>(d_eds), k, share_size, count, st);
+}
+
+int rsm_extend_squares_phase_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size, uint32_t count,
+                                 int phase, void* stream) {
+    if (!ctx || !d_eds || k == 0 || (phase != 1 && phase != 2))
+        return fail(RSM_EINVAL, "rsm_extend_squares_phase_dev: bad arguments");
+    if (int rc = validate_chunk_size(share_size)) return rc;
+    if (count == 0) return RSM_OK;
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    return extend_squares(static_cast<uint8_t*>(d_eds), k, share_size, count, st, phase);
+}
+
+int rsm_decode_vectors_dev(rsm_ctx* ctx, void* d_eds, const uint8_t* d_presence, uint32_t k,
+                           uint32_t share_size, int axis, const uint32_t* d_indices, uint32_t count,
+                           void* stream) {
+    if (!ctx || !d_eds || !d_presence || !d_indices || k == 0 || (axis != 0 && axis != 1))
+        return fail(RSM_EINVAL, "rsm_decode_vectors_dev: bad arguments");
+    if (int rc = validate_chunk_size(share_size)) return rc;
+    if (count == 0) return RSM_OK;
+    DecodeSet ds{};
+    ds.base = static_cast<uint8_t*>(d_eds);
+    ds.presence = d_presence;
+    ds.indices = d_indices;
+    ds.count = count;
+    ds.axis = (uint32_t)axis;
+    ds.k = k;
+    ds.S = share_size;
+    return launch_decode(ds, stream ? static_cast<hipStream_t>(stream) : ctx->stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,130 @@
+"""CPU: the C ABI library loads, exports every symbol include/rsmt2d_hip.h declares,
+and its host-only logic (shape/size validation, grid get/set, DefaultTree roots)
+matches the reference semantics.  No compute call runs without a GPU."""
+import os
+import re
+
+import pytest
+
+import rsmt2d_amd as R
+from oracle import crossword
+from conftest import const_share, rand_shares
+
+HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "rsmt2d_hip.h")
+
+
+def declared_symbols():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(rsm_[a-z0-9_]+)\s*\(", txt)) - {"rsm_tree_root_fn"})
+
+
+def test_every_declared_symbol_is_exported(lib):
+    syms = declared_symbols()
+    assert len(syms) >= 30
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert set(syms) == set(R.SIGNATURES), set(syms) ^ set(R.SIGNATURES)
+
+
+def test_codec_surface(lib):
+    codec = R.NewLeoRSCodec()
+    assert codec.Name() == "Leopard" == R.Leopard                 # codecs.go:11
+    assert codec.MaxChunks() == 32768 * 32768                      # leopard.go:76-84
+    assert codec.ValidateChunkSize(512) is None                    # leopard.go:92-99
+    assert codec.ValidateChunkSize(64) is None
+    assert codec.ValidateChunkSize(65).code == R.RSM_ESHARESIZE
+    assert lib.rsm_codec_field_bits(128) == 8 and lib.rsm_codec_field_bits(129) == 16
+
+
+def test_import_flattened_and_cells(lib, rng):
+    shares = rand_shares(rng, 16, 64)
+    shares[5] = None
+    eds = R.ImportExtendedDataSquare(shares, R.NewLeoRSCodec(), R.NewDefaultTree)
+    assert eds.Width() == 4 and eds.originalDataWidth == 2 and eds.shareSize == 64
+    assert eds.Flattened() == shares
+    assert eds.GetCell(1, 1) is None
+    assert eds.GetCell(0, 1) == shares[1]
+    with pytest.raises(R.RSMError) as e:                            # SetCell on non-nil
+        eds.SetCell(0, 1, shares[1])
+    assert e.value.code == R.RSM_ECELL
+    with pytest.raises(R.RSMError):                                 # wrong size
+        eds.SetCell(1, 1, b"\0" * 65)
+    eds.SetCell(1, 1, b"\7" * 64)
+    assert eds.GetCell(1, 1) == b"\7" * 64
+    assert eds.Row(1)[1] == b"\7" * 64 and eds.Col(1)[1] == b"\7" * 64
+
+
+def test_shape_errors(lib):
+    codec = R.NewLeoRSCodec()
+    with pytest.raises(R.RSMError) as e:                            # extendeddatasquare_test.go:84-88
+        R.ImportExtendedDataSquare([b"\1" * 65], codec, R.NewDefaultTree)
+    assert e.value.code == R.RSM_ESHARESIZE
+    with pytest.raises(R.RSMError) as e:                            # datasquare_test.go:48-65
+        R.ImportExtendedDataSquare([b"\1" * 64] * 3, codec, R.NewDefaultTree)
+    assert e.value.code == R.RSM_ESHAPE
+    with pytest.raises(R.RSMError) as e:                            # uneven shares
+        R.ImportExtendedDataSquare([b"\1" * 64] * 3 + [b"\1" * 128], codec, R.NewDefaultTree)
+    assert e.value.code == R.RSM_ESHAPE
+    with pytest.raises(R.RSMError) as e:                            # odd EDS width
+        R.ImportExtendedDataSquare([b"\1" * 64] * 9, codec, R.NewDefaultTree)
+    assert e.value.code == R.RSM_ESHAPE
+    with pytest.raises(R.RSMError):                                 # NewExtendedDataSquare odd width
+        R.NewExtendedDataSquare(codec, R.NewDefaultTree, 1, 512)
+    with pytest.raises(R.RSMError):                                 # ... and bad share size
+        R.NewExtendedDataSquare(codec, R.NewDefaultTree, 4, 65)
+    eds = R.NewExtendedDataSquare(codec, R.NewDefaultTree, 4, 512)  # extendeddatasquare_test.go:131-146
+    assert eds.Width() == 4 and eds.shareSize == 512
+    eds.SetCell(0, 0, const_share(1))
+    assert eds.GetCell(0, 0) == const_share(1)
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 5, 7, 8, 13, 16, 70])
+def test_default_tree_matches_restatement(lib, rng, n):
+    leaves = rand_shares(rng, n, 64)
+    assert R._default_root(leaves) == crossword.merkle_root(leaves)
+
+
+def test_roots_of_imported_square(lib, rng):
+    shares = rand_shares(rng, 64, 128)
+    eds = R.ImportExtendedDataSquare(shares, R.NewLeoRSCodec(), R.NewDefaultTree)
+    sq = crossword.Square(shares)
+    assert eds.RowRoots() == sq.roots(crossword.Row)
+    assert eds.ColRoots() == sq.roots(crossword.Col)
+    assert eds.Roots() == sq.roots(crossword.Row) + sq.roots(crossword.Col)
+    eds.setCell(0, 0, None)                                         # extendeddatasquare_test.go:250-262
+    with pytest.raises(R.RSMError) as e:
+        eds.RowRoots()
+    assert e.value.code == R.RSM_ETREE
+
+
+def test_custom_tree_plugin(lib, rng):
+    class XorTree(R.Tree):
+        def __init__(self):
+            self.acc = bytearray(8)
+
+        def Push(self, d):
+            for i, b in enumerate(d[:8]):
+                self.acc[i] ^= b
+
+        def Root(self):
+            return bytes(self.acc)
+
+    shares = rand_shares(rng, 16, 64)
+    eds = R.ImportExtendedDataSquare(shares, R.NewLeoRSCodec(), lambda axis, idx: XorTree())
+    roots = eds.RowRoots()
+    assert len(roots) == 4 and all(len(r) == 8 for r in roots)
+
+
+def test_json_roundtrip_host_only(lib, rng):
+    shares = rand_shares(rng, 16, 64)
+    eds = R.ImportExtendedDataSquare(shares, R.NewLeoRSCodec(), R.NewDefaultTree)
+    back = R.ExtendedDataSquare.UnmarshalJSON(eds.MarshalJSON())
+    assert back.Equals(eds)
+
+
+def test_no_gpu_fails_loudly(lib):
+    if lib.rsm_device_count() > 0:
+        pytest.skip("a GPU is present")
+    with pytest.raises(R.DeviceError):
+        R.NewLeoRSCodec().Encode([b"\1" * 64] * 2)
