@@ -71,17 +71,21 @@ def cpu_baseline(k, S, seconds):
 def main():
     a = parse()
     import numpy as np
-    import torch
-    import torch.distributed as dist
-    import rsmt2d_amd as R
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
     if world > 1:
+        # torch.distributed only for the timing barrier and the max-over-ranks of the
+        # elapsed time (the workload itself has no data-path exchange).  torch's own HIP
+        # runtime must initialise before librsmt2d_hip.so is loaded.
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
         dist.init_process_group(backend="nccl", init_method="env://")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        dev = torch.device("cuda", local)
+    import rsmt2d_amd as R
 
     wl = WORKLOADS[a.workload]
     k, S = wl["k"], wl["S"]
@@ -91,65 +95,59 @@ def main():
     L = R.library()
     ctx = R.device_context(local)
 
-    # synthetic ODS (seeded uniform bytes) placed in the top-left quadrant of each square
-    g = torch.Generator(device=dev)
-    g.manual_seed(0x52534D543244 + rank)
-    eds = torch.empty((B, W, W, S), dtype=torch.uint8, device=dev)
-    eds[:, :k, :k] = torch.randint(0, 256, (B, k, k, S), dtype=torch.uint8, device=dev, generator=g)
-    stream = torch.cuda.current_stream(dev)
-    sh = stream.cuda_stream
+    # synthetic ODS: seeded uniform bytes (SplitMix64) generated on the device; each
+    # square's top-left quadrant is its ODS (the other quadrants are overwritten).
+    buf = R.DeviceBuffer(B * sq_bytes, local)
+    buf.fill_random(0x52534D543244 + rank)
 
     def step():
-        R._check(L.rsm_extend_squares_dev(ctx, eds.data_ptr(), k, S, B, sh))
+        R._check(L.rsm_extend_squares_dev(ctx, buf.ptr, k, S, B, None))
 
     for _ in range(a.warmup):
         step()
-    torch.cuda.synchronize()
-    # correctness gate on one square before timing (oracle is test infra; bench only checks)
+    R._check(L.rsm_sync(ctx))
+    # correctness gate on one square before timing (the oracle is the checker only)
     if rank == 0:
         import oracle
-        got = eds[0].cpu().numpy()
+        got = buf.download(sq_bytes).reshape(W, W, S)
         want = oracle.extend_square(got[:k, :k].copy(), nthreads=min(16, os.cpu_count() or 1))
         if not np.array_equal(got, want):
             raise SystemExit("bench: GPU EDS differs from oracle -- refusing to report")
 
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    barrier()
+    R._check(L.rsm_sync(ctx))
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    R._check(L.rsm_sync(ctx))
+    barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # per-kernel durations on the launch stream (HIP events), separate short run
-    nrep = max(5, min(a.steps, 20))
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(nrep)]
-    for i in range(nrep):
-        ev[i][0].record(stream)
-        R._check(L.rsm_extend_squares_phase_dev(ctx, eds.data_ptr(), k, S, B, 1, sh))
-        ev[i][1].record(stream)
-        R._check(L.rsm_extend_squares_phase_dev(ctx, eds.data_ptr(), k, S, B, 2, sh))
-        ev[i][2].record(stream)
-    torch.cuda.synchronize()
-    t_row = sum(e[0].elapsed_time(e[1]) for e in ev) / nrep / 1e3
-    t_col = sum(e[1].elapsed_time(e[2]) for e in ev) / nrep / 1e3
+    # per-kernel durations: HIP events on the launch stream (the context stream)
+    import ctypes
+    row_ms, col_ms, step_ms = ctypes.c_float(), ctypes.c_float(), ctypes.c_float()
+    R._check(L.rsm_time_extend(ctx, buf.ptr, k, S, B, max(5, min(a.steps, 20)), ctypes.byref(row_ms),
+                               ctypes.byref(col_ms), ctypes.byref(step_ms)))
+    t_row, t_col = row_ms.value / 1e3, col_ms.value / 1e3
 
     ods_bytes = k * k * S
     total = world * B * a.steps * ods_bytes
     value = total / elapsed / 2**30
     ms_per_step = elapsed / a.steps * 1e3
     algo_step = 4 * ods_bytes * B  # read Q0 once, write Q1+Q2+Q3
-    col_bytes = 4 * ods_bytes * B  # column pass moves [Q0|Q1] in and [Q2|Q3] out
+    col_bytes = 4 * ods_bytes * B  # column pass: [Q0|Q1] in, [Q2|Q3] out
     row_bytes = 2 * ods_bytes * B  # row pass: Q0 in, Q1 out
-    dominant = ("encode_gf8_kernel<128> column pass" if k == 128 else f"encode kernel column pass (k={k})",
-                col_bytes, t_col) if t_col >= t_row else ("row pass", row_bytes, t_row)
+    kname = "encode_gf8_kernel<128>" if k <= 128 else "encode_gf16_kernel"
+    dominant = ((kname + " column pass", col_bytes, t_col) if t_col >= t_row else (kname + " row pass", row_bytes, t_row))
     ach = dominant[1] / dominant[2] / 1e9
     out = {
         "metric": "GiB/s device-resident 2D RS encode, k=128 square, 512 B shares; % HBM peak",
@@ -163,7 +161,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8" if k <= 128 else "u16",
-        "data": "synthetic (seeded uniform bytes, device-generated)",
+        "data": "synthetic (seeded SplitMix64 bytes, device-generated)",
         "config": {"workload": f"{a.workload}: {wl['desc']}", "k": k, "share_size": S,
                    "squares_per_step": B, "eds_bytes_per_step": B * sq_bytes,
                    "parallelism": f"independent squares per GPU x{world}"},
@@ -171,7 +169,8 @@ def main():
                      "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
                      "kernel": dominant[0], "avg_launch_us": round(dominant[2] * 1e6, 2),
                      "bytes_per_launch": dominant[1]},
-        "step_roofline": {"algorithmic_bytes": algo_step, "achieved": round(algo_step / (elapsed / a.steps) / 1e9, 1),
+        "step_roofline": {"algorithmic_bytes": algo_step,
+                          "achieved": round(algo_step / (elapsed / a.steps) / 1e9, 1),
                           "frac": round(algo_step / (elapsed / a.steps) / 1e9 / HBM_PEAK_GBS, 4),
                           "row_pass_us": round(t_row * 1e6, 2), "col_pass_us": round(t_col * 1e6, 2)},
     }
@@ -187,9 +186,10 @@ def main():
         out["host_path"] = {"value": round(n * ods_bytes / (time.perf_counter() - t1) / 2**30, 3), "unit": "GiB/s",
                             "note": "rsm_extend_square: pageable host ODS -> H2D -> extend -> D2H EDS, one square"}
         out["cpu_baseline"] = None if a.no_cpu_baseline else cpu_baseline(k, S, a.cpu_seconds)
+    buf.free()
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist is not None:
         dist.destroy_process_group()
 
 

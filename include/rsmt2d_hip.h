@@ -75,8 +75,8 @@ int rsm_extend_square(rsm_ctx* ctx, const uint8_t* ods, uint32_t k, uint32_t sha
                       uint8_t* eds);
 /* Device-resident, in place: d_eds holds `count` consecutive [2k][2k][S] squares
  * whose top-left quadrant already holds the ODS (the EDS aliases the ODS, as in
- * ComputeExtendedDataSquare).  Enqueued on `stream` (a hipStream_t, NULL =
- * the context stream); asynchronous. */
+ * ComputeExtendedDataSquare).  Enqueued on `stream` (a hipStream_t of this
+ * library's HIP runtime; NULL = the context stream); asynchronous. */
 int rsm_extend_squares_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size, uint32_t count,
                            void* stream);
 /* One phase of the above: phase 1 = row pass (Q0 -> Q1), phase 2 = column pass
@@ -89,6 +89,22 @@ int rsm_extend_squares_phase_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t
 int rsm_decode_vectors_dev(rsm_ctx* ctx, void* d_eds, const uint8_t* d_presence, uint32_t k,
                            uint32_t share_size, int axis, const uint32_t* d_indices, uint32_t count,
                            void* stream);
+
+/* ---- device memory / timing on the context's HIP runtime ---------------------- */
+/* The context's stream (hipStream_t); the *_dev calls above use it when their
+ * stream argument is NULL. */
+void* rsm_ctx_stream(rsm_ctx* ctx);
+int rsm_dev_alloc(rsm_ctx* ctx, uint64_t bytes, void** out);
+int rsm_dev_free(rsm_ctx* ctx, void* p);
+/* kind: 0 host->device, 1 device->host, 2 device->device; synchronous. */
+int rsm_memcpy(rsm_ctx* ctx, void* dst, const void* src, uint64_t bytes, int kind);
+/* SplitMix64 byte stream (seeded synthetic shares), asynchronous on the ctx stream. */
+int rsm_dev_fill_random(rsm_ctx* ctx, void* d, uint64_t bytes, uint64_t seed);
+int rsm_sync(rsm_ctx* ctx);
+/* Event-timed extension of `count` in-place squares on the ctx stream, averaged
+ * over `reps`: row pass, column pass and their sum, in milliseconds. */
+int rsm_time_extend(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size, uint32_t count,
+                    uint32_t reps, float* row_ms, float* col_ms, float* step_ms);
 
 /* ---- Tree plugin (tree.go:11-28) ------------------------------------------------ */
 /* Computes the root of one row/column: Push(leaves[0..n)) then Root().  Writes

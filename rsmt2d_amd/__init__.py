@@ -116,6 +116,14 @@ SIGNATURES = {
     "rsm_extend_squares_dev": (_I32, [_VP, _VP, _U32, _U32, _U32, _VP]),
     "rsm_extend_squares_phase_dev": (_I32, [_VP, _VP, _U32, _U32, _U32, _I32, _VP]),
     "rsm_decode_vectors_dev": (_I32, [_VP, _VP, _VP, _U32, _U32, _I32, _VP, _U32, _VP]),
+    "rsm_ctx_stream": (_VP, [_VP]),
+    "rsm_dev_alloc": (_I32, [_VP, _U64, ctypes.POINTER(_VP)]),
+    "rsm_dev_free": (_I32, [_VP, _VP]),
+    "rsm_memcpy": (_I32, [_VP, _VP, _VP, _U64, _I32]),
+    "rsm_dev_fill_random": (_I32, [_VP, _VP, _U64, _U64]),
+    "rsm_sync": (_I32, [_VP]),
+    "rsm_time_extend": (_I32, [_VP, _VP, _U32, _U32, _U32, _U32, ctypes.POINTER(ctypes.c_float),
+                               ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
     "rsm_default_tree_root": (_I32, [_VP, _I32, _U32, _VP, _U32, _U32, _VP, _VP]),
     "rsm_eds_compute": (_I32, [_VP, _VP, _VP, _U64, ctypes.POINTER(_VP)]),
     "rsm_eds_import": (_I32, [_VP, _VP, _VP, _U64, ctypes.POINTER(_VP)]),
@@ -182,6 +190,43 @@ def device_context(device: int = 0) -> int:
             _check(library().rsm_ctx_create(device, ctypes.byref(h)))
             _ctx[device] = h.value
         return _ctx[device]
+
+
+class DeviceBuffer:
+    """Device memory owned by this library's HIP runtime (bench / tests plumbing)."""
+
+    def __init__(self, nbytes: int, device: int = 0):
+        self.ctx = device_context(device)
+        self.nbytes = int(nbytes)
+        p = ctypes.c_void_p()
+        _check(library().rsm_dev_alloc(self.ctx, self.nbytes, ctypes.byref(p)))
+        self.ptr = p.value
+
+    def fill_random(self, seed: int):
+        _check(library().rsm_dev_fill_random(self.ctx, self.ptr, self.nbytes, seed))
+
+    def upload(self, arr, offset: int = 0):
+        import numpy as np
+        a = np.ascontiguousarray(arr)
+        _check(library().rsm_memcpy(self.ctx, self.ptr + offset, a.ctypes.data, a.nbytes, 0))
+
+    def download(self, nbytes: int = None, offset: int = 0):
+        import numpy as np
+        n = self.nbytes - offset if nbytes is None else nbytes
+        out = np.empty(n, np.uint8)
+        _check(library().rsm_memcpy(self.ctx, out.ctypes.data, self.ptr + offset, n, 1))
+        return out
+
+    def free(self):
+        if self.ptr:
+            library().rsm_dev_free(self.ctx, self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
 
 
 def _bufs(shares: Sequence[Optional[bytes]]):

@@ -1,9 +1,31 @@
-// kernels_util.hip -- small device helpers for the Repair fast path.
+// kernels_util.hip -- small device helpers: Repair fast-path comparisons and the
+// synthetic-input generator used by benchmarks.
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include "rsm_kernels.hpp"
 
 namespace rsm {
+
+// Fills n bytes with the SplitMix64 stream of `seed` (word i = splitmix(seed + (i+1)*golden)),
+// byte-identical to oracle.splitmix64_bytes.
+__global__ __launch_bounds__(256) void fill_random_kernel(uint64_t* p, uint64_t nwords, uint64_t seed) {
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < nwords; i += (uint64_t)gridDim.x * 256ull) {
+        uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        p[i] = z ^ (z >> 31);
+    }
+}
+
+hipError_t launch_fill_random(void* p, uint64_t bytes, uint64_t seed, hipStream_t st) {
+    const uint64_t nwords = bytes / 8;
+    if (nwords == 0) return hipSuccess;
+    uint64_t blocks = (nwords + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(fill_random_kernel, dim3((uint32_t)blocks), dim3(256), 0, st, static_cast<uint64_t*>(p),
+                       nwords, seed);
+    return hipGetLastError();
+}
 
 // *mismatch |= any(a[i] != b[i]) over n bytes (n multiple of 16): the on-device
 // form of verifyEncoding's bytes.Equal (extendeddatacrossword.go:496-500).

@@ -340,3 +340,83 @@ int rsm_decode_vectors_dev(rsm_ctx* ctx, void* d_eds, const uint8_t* d_presence,
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// C ABI: device memory, synthetic inputs and event timing on the context's own
+// HIP runtime/stream.  (A host process embedding a second HIP runtime -- e.g.
+// PyTorch's bundled one -- must not hand its stream objects to this library;
+// device pointers are shared fine.)
+// ---------------------------------------------------------------------------
+extern "C" {
+
+void* rsm_ctx_stream(rsm_ctx* ctx) { return ctx ? static_cast<void*>(ctx->stream) : nullptr; }
+
+int rsm_dev_alloc(rsm_ctx* ctx, uint64_t bytes, void** out) {
+    if (!ctx || !out) return fail(RSM_EINVAL, "rsm_dev_alloc: bad arguments");
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    if ((e = hipMalloc(out, bytes ? bytes : 1)) != hipSuccess) return hip_fail(e, "hipMalloc");
+    return RSM_OK;
+}
+
+int rsm_dev_free(rsm_ctx* ctx, void* p) {
+    if (!ctx) return fail(RSM_EINVAL, "rsm_dev_free: NULL ctx");
+    if (!p) return RSM_OK;
+    (void)hipSetDevice(ctx->device);
+    hipError_t e = hipFree(p);
+    return e == hipSuccess ? RSM_OK : hip_fail(e, "hipFree");
+}
+
+int rsm_memcpy(rsm_ctx* ctx, void* dst, const void* src, uint64_t bytes, int kind) {
+    if (!ctx || !dst || !src || kind < 0 || kind > 2) return fail(RSM_EINVAL, "rsm_memcpy: bad arguments");
+    const hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice : kind == 1 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    if ((e = hipMemcpyAsync(dst, src, bytes, k, ctx->stream)) != hipSuccess) return hip_fail(e, "hipMemcpyAsync");
+    if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+    return RSM_OK;
+}
+
+int rsm_dev_fill_random(rsm_ctx* ctx, void* d, uint64_t bytes, uint64_t seed) {
+    if (!ctx || !d) return fail(RSM_EINVAL, "rsm_dev_fill_random: bad arguments");
+    hipError_t e = launch_fill_random(d, bytes, seed, ctx->stream);
+    return e == hipSuccess ? RSM_OK : hip_fail(e, "fill_random");
+}
+
+int rsm_sync(rsm_ctx* ctx) {
+    if (!ctx) return fail(RSM_EINVAL, "rsm_sync: NULL ctx");
+    hipError_t e = hipStreamSynchronize(ctx->stream);
+    return e == hipSuccess ? RSM_OK : hip_fail(e, "hipStreamSynchronize");
+}
+
+int rsm_time_extend(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size, uint32_t count, uint32_t reps,
+                    float* row_ms, float* col_ms, float* step_ms) {
+    if (!ctx || !d_eds || reps == 0) return fail(RSM_EINVAL, "rsm_time_extend: bad arguments");
+    hipEvent_t ev[3];
+    for (auto& x : ev)
+        if (hipEventCreate(&x) != hipSuccess) return fail(RSM_EDEVICE, "hipEventCreate");
+    float acc[3] = {0, 0, 0};
+    int rc = RSM_OK;
+    for (uint32_t r = 0; r < reps && rc == RSM_OK; ++r) {
+        (void)hipEventRecord(ev[0], ctx->stream);
+        rc = extend_squares(static_cast<uint8_t*>(d_eds), k, share_size, count, ctx->stream, 1);
+        (void)hipEventRecord(ev[1], ctx->stream);
+        if (rc == RSM_OK) rc = extend_squares(static_cast<uint8_t*>(d_eds), k, share_size, count, ctx->stream, 2);
+        (void)hipEventRecord(ev[2], ctx->stream);
+        if (hipEventSynchronize(ev[2]) != hipSuccess) rc = fail(RSM_EDEVICE, "hipEventSynchronize");
+        float a = 0, b = 0;
+        (void)hipEventElapsedTime(&a, ev[0], ev[1]);
+        (void)hipEventElapsedTime(&b, ev[1], ev[2]);
+        acc[0] += a;
+        acc[1] += b;
+        acc[2] += a + b;
+    }
+    for (auto& x : ev) (void)hipEventDestroy(x);
+    if (rc) return rc;
+    if (row_ms) *row_ms = acc[0] / reps;
+    if (col_ms) *col_ms = acc[1] / reps;
+    if (step_ms) *step_ms = acc[2] / reps;
+    return RSM_OK;
+}
+
+}  // extern "C"

@@ -25,4 +25,11 @@ if [[ $STEPS == *prof* ]]; then
   run rocprof 600 rocprofv3 --kernel-trace --stats -d "$PWD/$OUT/prof" -o run --output-format csv -- \
       python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-}; ok $? || exit 6
 fi
+if [[ $STEPS == *pmc* ]]; then
+  export TMPDIR=/tmp
+  run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$PWD/$OUT/pmc_fetch" -o run --output-format csv -- \
+      python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-}; ok $? || exit 7
+  run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$PWD/$OUT/pmc_write" -o run --output-format csv -- \
+      python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-}; ok $? || exit 8
+fi
 exit 0

@@ -74,19 +74,21 @@ def test_extend_square_matches_oracle(lib, rng, k):
     assert (got == want).all()
 
 
-def test_extend_squares_dev_batched(lib, rng):
-    """Device-resident in-place batch (the bench path) on 3 squares, k=128, S=512."""
-    torch = pytest.importorskip("torch")
+def test_extend_squares_dev_batched(lib):
+    """Device-resident in-place batch (the bench path) on 3 squares, k=128, S=512; the
+    synthetic input generator must reproduce oracle.splitmix64_bytes."""
     k, S, n = 128, 512, 3
-    ods = rng.integers(0, 256, (n, k, k, S), dtype=np.uint8)
-    eds = torch.zeros((n, 2 * k, 2 * k, S), dtype=torch.uint8, device="cuda")
-    eds[:, :k, :k] = torch.from_numpy(ods).cuda()
-    st = torch.cuda.current_stream()
-    R._check(lib.rsm_extend_squares_dev(R.device_context(), eds.data_ptr(), k, S, n, st.cuda_stream))
-    torch.cuda.synchronize()
-    got = eds.cpu().numpy()
+    W = 2 * k
+    buf = R.DeviceBuffer(n * W * W * S)
+    buf.fill_random(1234)
+    ref = oracle.splitmix64_bytes(n * W * W * S, seed=1234).reshape(n, W, W, S)
+    assert (buf.download().reshape(n, W, W, S) == ref).all()
+    R._check(lib.rsm_extend_squares_dev(buf.ctx, buf.ptr, k, S, n, None))
+    R._check(lib.rsm_sync(buf.ctx))
+    got = buf.download().reshape(n, W, W, S)
     for i in range(n):
-        assert (got[i] == oracle.extend_square(ods[i], nthreads=8)).all(), i
+        assert (got[i] == oracle.extend_square(ref[i, :k, :k].copy(), nthreads=8)).all(), i
+    buf.free()
 
 
 def test_affine_digest_k128(lib):
