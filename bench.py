@@ -149,6 +149,18 @@ def main():
     kname = "encode_gf8_kernel<128>" if k <= 128 else "encode_gf16_kernel"
     dominant = ((kname + " column pass", col_bytes, t_col) if t_col >= t_row else (kname + " row pass", row_bytes, t_row))
     ach = dominant[1] / dominant[2] / 1e9
+    # HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC
+    # passes (scripts/pmc_summary.py; FETCH_SIZE x2 gfx950 correction), matched by
+    # kernel and grid size -- null when no matching profile exists.
+    traffic = None
+    chunks = (S + 255) // 256 if k <= 128 else (S + 127) // 128
+    ncw = (W if t_col >= t_row else k) * B
+    grid_threads = (ncw * chunks + 3) // 4 * 256
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    if os.path.exists(pmc_path):
+        for row in json.load(open(pmc_path)).get("launches", []):
+            if row["grid_threads"] == grid_threads and ("<%d>" % (1 << (k - 1).bit_length()) in row["kernel"]):
+                traffic = int(row["traffic_bytes"])
     out = {
         "metric": "GiB/s device-resident 2D RS encode, k=128 square, 512 B shares; % HBM peak",
         "value": round(value, 3),
@@ -166,7 +178,7 @@ def main():
                    "squares_per_step": B, "eds_bytes_per_step": B * sq_bytes,
                    "parallelism": f"independent squares per GPU x{world}"},
         "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel": dominant[0], "avg_launch_us": round(dominant[2] * 1e6, 2),
                      "bytes_per_launch": dominant[1]},
         "step_roofline": {"algorithmic_bytes": algo_step,
