@@ -226,7 +226,7 @@ struct DevSquare {
         ds.axis = (uint32_t)axis;
         ds.k = k;
         ds.S = S;
-        return launch_decode(ds, st);
+        return launch_decode(ctx, ds, st);
     }
     // verifyEncoding for many complete vectors at once: re-encode their first
     // half into the scratch square and compare parity halves.  bad[i] = 1 on mismatch.
@@ -246,7 +246,7 @@ struct DevSquare {
         cs.count = (uint32_t)idx.size();
         cs.k = k;
         cs.S = S;
-        if (int rc = launch_encode(cs, st)) return rc;
+        if (int rc = launch_encode(ctx, cs, st)) return rc;
         if ((r = launch_compare_parity(d_eds, d_scratch, k, S, (uint32_t)axis, d_idx, cs.count, d_flags, st)) != hipSuccess)
             return hip_fail(r, "compare parity");
         if ((r = hipMemcpyAsync(bad.data(), d_flags, idx.size() * 4, hipMemcpyDeviceToHost, st)) != hipSuccess)
@@ -479,7 +479,7 @@ int fast_repair(rsm_eds* e, DevSquare& dev, const uint8_t* row_roots, const uint
     hipError_t r = hipMemcpy2DAsync(dev.d_scratch, (size_t)W * S, dev.d_eds, (size_t)W * S, (size_t)k * S, k,
                                     hipMemcpyDeviceToDevice, dev.st);
     if (r != hipSuccess) return hip_fail(r, "D2D Q0");
-    if (int rc = extend_squares(dev.d_scratch, k, e->S, 1, dev.st)) return rc;
+    if (int rc = extend_squares(dev.ctx, dev.d_scratch, k, e->S, 1, dev.st)) return rc;
     if ((r = hipMemsetAsync(dev.d_flags, 0, 4, dev.st)) != hipSuccess) return hip_fail(r, "memset");
     if ((r = launch_compare(dev.d_eds, dev.d_scratch, (uint64_t)W * W * S, dev.d_flags, dev.st)) != hipSuccess)
         return hip_fail(r, "compare");

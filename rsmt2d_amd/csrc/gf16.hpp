@@ -1,0 +1,35 @@
+// gf16.hpp -- GF(2^16) tables and device resources shared by host and kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <vector>
+
+namespace rsm {
+
+// v_perm_b32 tables for y -> y * exp(L) on packed GF(2^16) symbols.  The 16-bit
+// symbol is cut into six chunks (lo byte bits [0,3) [3,6) [6,8), hi byte bits
+// [0,3) [3,6) [6,8)); chunk c has an output-lo and an output-hi byte table of up
+// to 8 entries held as two dwords each: w[4c+0..1] = lo table, w[4c+2..3] = hi.
+struct alignas(16) PermTab16 {
+    uint32_t w[24];
+};
+
+struct Gf16Host {
+    std::vector<uint16_t> exp, log, skew, logwalsh;
+    std::vector<PermTab16> perm;  // 65536 entries
+};
+const Gf16Host& gf16_host();
+
+// Device copies + scratch, owned by a context.
+struct Gf16Dev {
+    const PermTab16* perm = nullptr;  // [65536]
+    const uint16_t* skew = nullptr;   // [65535]
+    const uint16_t* logwalsh = nullptr;
+    uint8_t* scratch = nullptr;       // work arrays
+    uint64_t scratch_bytes = 0;
+    uint16_t* errs = nullptr;         // decoder error locators [count][n]
+    uint64_t errs_bytes = 0;
+};
+
+}  // namespace rsm

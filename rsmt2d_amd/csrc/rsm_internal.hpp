@@ -9,12 +9,10 @@
 #include <string>
 
 #include "../../include/rsmt2d_hip.h"
+#include "gf16.hpp"
 #include "rsm_kernels.hpp"
 
 namespace rsm {
-
-// Bytes of share width one GF(2^16) wave task covers (see kernels_gf16.hip).
-constexpr uint32_t kGf16BytesPerWave = 128;
 
 int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 int hip_fail(hipError_t e, const char* what);
@@ -42,20 +40,18 @@ struct HostBuf {
     hipError_t ensure(size_t n);
 };
 
-int launch_encode(const CodewordSet& cs, hipStream_t st);
-int launch_decode(const DecodeSet& ds, hipStream_t st);
-int extend_squares(uint8_t* d_eds, uint32_t k, uint32_t S, uint32_t count, hipStream_t st, int phases = 3);
-
 }  // namespace rsm
 
 struct rsm_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    std::recursive_mutex mu_storage;
-    std::mutex mu;
+    std::mutex mu;       // serialises API calls that use the context's staging buffers
+    std::mutex gf16_mu;  // guards gf16 table upload / scratch growth
     std::map<int, std::unique_ptr<rsm::DevBuf>> bufs;
     std::map<int, std::unique_ptr<rsm::HostBuf>> hbufs;
     uint32_t* d_zero_index = nullptr;
+    rsm::Gf16Dev gf16{};
+    bool gf16_ready = false;
 
     rsm::DevBuf& dev_buf(int slot) {
         auto& p = bufs[slot];
@@ -78,3 +74,16 @@ struct rsm_ctx {
         return d_zero_index;
     }
 };
+
+namespace rsm {
+
+// GF(2^16) tables on the context's device (uploaded once) + scratch sized for
+// `scratch_bytes` of work arrays.  Returns RSM_OK or an RSM_E* code.
+int ensure_gf16(rsm_ctx* ctx, uint64_t scratch_bytes, uint64_t errs_bytes);
+
+int launch_encode(rsm_ctx* ctx, const CodewordSet& cs, hipStream_t st);
+int launch_decode(rsm_ctx* ctx, const DecodeSet& ds, hipStream_t st);
+int extend_squares(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, uint32_t count, hipStream_t st,
+                   int phases = 3);
+
+}  // namespace rsm

@@ -48,8 +48,9 @@ struct DecodeSet {
 
 hipError_t launch_encode_gf8(const CodewordSet& cs, hipStream_t st);
 hipError_t launch_decode_gf8(const DecodeSet& ds, hipStream_t st);
-hipError_t launch_encode_gf16(const CodewordSet& cs, hipStream_t st);
-hipError_t launch_decode_gf16(const DecodeSet& ds, hipStream_t st);
+struct Gf16Dev;
+hipError_t launch_encode_gf16(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st);
+hipError_t launch_decode_gf16(const DecodeSet& ds, const Gf16Dev& g, hipStream_t st);
 hipError_t launch_fill_random(void* p, uint64_t bytes, uint64_t seed, hipStream_t st);
 hipError_t launch_compare(const uint8_t* a, const uint8_t* b, uint64_t n, uint32_t* mismatch, hipStream_t st);
 hipError_t launch_compare_parity(const uint8_t* a, const uint8_t* b, uint32_t k, uint32_t S, uint32_t axis,

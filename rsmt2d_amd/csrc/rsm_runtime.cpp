@@ -70,23 +70,88 @@ int field_bits(uint32_t k) { return 2ull * k > 256ull ? 16 : 8; }
 // ---------------------------------------------------------------------------
 // Launch helpers (device-resident, asynchronous on `st`)
 // ---------------------------------------------------------------------------
-static uint32_t bytes_per_wave(uint32_t k) { return field_bits(k) == 8 ? 256u : kGf16BytesPerWave; }
+// GF(2^16) kernels support m = ceilPow2(k) in {256, 512} (2k <= 1024 shards:
+// every configuration in BASELINE.json); larger k returns RSM_EUNSUPPORTED.
+static bool gf16_supported(uint32_t k) { return k > 128 && k <= 512; }
 
-int launch_encode(const CodewordSet& cs0, hipStream_t st) {
+int ensure_gf16(rsm_ctx* ctx, uint64_t scratch_bytes, uint64_t errs_bytes) {
+    std::lock_guard<std::mutex> lk(ctx->gf16_mu);
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    if (!ctx->gf16_ready) {
+        const Gf16Host& t = gf16_host();
+        DevBuf& perm = ctx->dev_buf(20);
+        DevBuf& skew = ctx->dev_buf(21);
+        DevBuf& lw = ctx->dev_buf(22);
+        const size_t pb = t.perm.size() * sizeof(PermTab16), sb = t.skew.size() * 2, lb = t.logwalsh.size() * 2;
+        if ((e = perm.ensure(pb)) != hipSuccess || (e = skew.ensure(sb)) != hipSuccess || (e = lw.ensure(lb)) != hipSuccess)
+            return hip_fail(e, "hipMalloc (GF16 tables)");
+        if ((e = hipMemcpy(perm.ptr, t.perm.data(), pb, hipMemcpyHostToDevice)) != hipSuccess ||
+            (e = hipMemcpy(skew.ptr, t.skew.data(), sb, hipMemcpyHostToDevice)) != hipSuccess ||
+            (e = hipMemcpy(lw.ptr, t.logwalsh.data(), lb, hipMemcpyHostToDevice)) != hipSuccess)
+            return hip_fail(e, "upload GF16 tables");
+        ctx->gf16.perm = static_cast<const PermTab16*>(perm.ptr);
+        ctx->gf16.skew = static_cast<const uint16_t*>(skew.ptr);
+        ctx->gf16.logwalsh = static_cast<const uint16_t*>(lw.ptr);
+        ctx->gf16_ready = true;
+    }
+    if (scratch_bytes > ctx->gf16.scratch_bytes) {
+        // a kernel may still read the old scratch: drain the device before freeing it
+        if ((e = hipDeviceSynchronize()) != hipSuccess) return hip_fail(e, "hipDeviceSynchronize");
+        DevBuf& s = ctx->dev_buf(23);
+        if ((e = s.ensure(scratch_bytes)) != hipSuccess) return hip_fail(e, "hipMalloc (GF16 scratch)");
+        ctx->gf16.scratch = static_cast<uint8_t*>(s.ptr);
+        ctx->gf16.scratch_bytes = scratch_bytes;
+    }
+    if (errs_bytes > ctx->gf16.errs_bytes) {
+        if ((e = hipDeviceSynchronize()) != hipSuccess) return hip_fail(e, "hipDeviceSynchronize");
+        DevBuf& s = ctx->dev_buf(24);
+        if ((e = s.ensure(errs_bytes)) != hipSuccess) return hip_fail(e, "hipMalloc (GF16 error locators)");
+        ctx->gf16.errs = static_cast<uint16_t*>(s.ptr);
+        ctx->gf16.errs_bytes = errs_bytes;
+    }
+    return RSM_OK;
+}
+
+// Scratch budget for GF16 work arrays: all codewords of a launch when that fits
+// in 1 GiB, else 1 GiB worth per batch (the launcher loops).
+static uint64_t gf16_budget(uint64_t per_cw, uint64_t count) {
+    const uint64_t cap = 1ull << 30;
+    const uint64_t want = per_cw * count;
+    return want < cap ? want : (cap / per_cw) * per_cw;
+}
+
+int launch_encode(rsm_ctx* ctx, const CodewordSet& cs0, hipStream_t st) {
     CodewordSet cs = cs0;
     if (cs.out_base == nullptr) cs.out_base = cs.base;
-    cs.chunks = (cs.S + bytes_per_wave(cs.k) - 1) / bytes_per_wave(cs.k);
-    hipError_t e = field_bits(cs.k) == 8 ? launch_encode_gf8(cs, st) : launch_encode_gf16(cs, st);
-    if (e == hipErrorNotSupported) return fail(RSM_EUNSUPPORTED, "encode: k=%u (GF16) not supported in this build", cs.k);
+    hipError_t e;
+    if (field_bits(cs.k) == 8) {
+        cs.chunks = (cs.S + 255) / 256;
+        e = launch_encode_gf8(cs, st);
+    } else {
+        if (!gf16_supported(cs.k)) return fail(RSM_EUNSUPPORTED, "encode: k=%u (m > 512) not supported in this build", cs.k);
+        const uint64_t per_cw = (uint64_t)ceil_pow2(cs.k) * cs.S;
+        if (int rc = ensure_gf16(ctx, gf16_budget(per_cw, cs.count), 0)) return rc;
+        e = launch_encode_gf16(cs, ctx->gf16, st);
+    }
     if (e != hipSuccess) return hip_fail(e, "encode kernel launch");
     return RSM_OK;
 }
 
-int launch_decode(const DecodeSet& ds0, hipStream_t st) {
+int launch_decode(rsm_ctx* ctx, const DecodeSet& ds0, hipStream_t st) {
     DecodeSet ds = ds0;
-    ds.chunks = (ds.S + bytes_per_wave(ds.k) - 1) / bytes_per_wave(ds.k);
-    hipError_t e = field_bits(ds.k) == 8 ? launch_decode_gf8(ds, st) : launch_decode_gf16(ds, st);
-    if (e == hipErrorNotSupported) return fail(RSM_EUNSUPPORTED, "decode: k=%u (GF16) not supported in this build", ds.k);
+    hipError_t e;
+    if (field_bits(ds.k) == 8) {
+        ds.chunks = (ds.S + 255) / 256;
+        e = launch_decode_gf8(ds, st);
+    } else {
+        if (!gf16_supported(ds.k)) return fail(RSM_EUNSUPPORTED, "decode: k=%u (m > 512) not supported in this build", ds.k);
+        const uint64_t n = 2ull * ceil_pow2(ds.k);
+        const uint64_t per_cw = 2ull * n * ds.S;
+        const uint64_t budget = gf16_budget(per_cw, ds.count);
+        if (int rc = ensure_gf16(ctx, budget, (budget / per_cw) * n * sizeof(uint16_t))) return rc;
+        e = launch_decode_gf16(ds, ctx->gf16, st);
+    }
     if (e != hipSuccess) return hip_fail(e, "decode kernel launch");
     return RSM_OK;
 }
@@ -98,7 +163,8 @@ int launch_decode(const DecodeSet& ds0, hipStream_t st) {
 // which equals the reference's row-encoding of Q2 by linearity of the 2D code
 // (extendeddatasquare.go:204-207; asserted in tests against the oracle, which
 // runs the reference order).
-int extend_squares(uint8_t* d_eds, uint32_t k, uint32_t S, uint32_t count, hipStream_t st, int phases) {
+int extend_squares(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, uint32_t count, hipStream_t st,
+                   int phases) {
     const uint64_t W = 2ull * k;
     CodewordSet rows{};
     rows.base = d_eds;
@@ -111,7 +177,7 @@ int extend_squares(uint8_t* d_eds, uint32_t k, uint32_t S, uint32_t count, hipSt
     rows.k = k;
     rows.S = S;
     if (phases & 1) {
-        int rc = launch_encode(rows, st);
+        int rc = launch_encode(ctx, rows, st);
         if (rc) return rc;
     }
     if (!(phases & 2)) return RSM_OK;
@@ -125,7 +191,7 @@ int extend_squares(uint8_t* d_eds, uint32_t k, uint32_t S, uint32_t count, hipSt
     cols.count = (uint32_t)W * count;
     cols.k = k;
     cols.S = S;
-    return launch_encode(cols, st);
+    return launch_encode(ctx, cols, st);
 }
 
 }  // namespace rsm
@@ -218,7 +284,7 @@ int rsm_encode(rsm_ctx* ctx, const uint8_t* const* data, uint32_t k, uint32_t sh
     cs.count = 1;
     cs.k = k;
     cs.S = share_size;
-    if (int rc = launch_encode(cs, ctx->stream)) return rc;
+    if (int rc = launch_encode(ctx, cs, ctx->stream)) return rc;
     if ((e = hipMemcpyAsync(h + k * S, d + k * S, k * S, hipMemcpyDeviceToHost, ctx->stream)) != hipSuccess)
         return hip_fail(e, "hipMemcpyAsync D2H");
     if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return hip_fail(e, "encode");
@@ -273,7 +339,7 @@ int rsm_decode(rsm_ctx* ctx, uint8_t* const* shares, const uint8_t* present, uin
     ds.k = k;
     ds.S = share_size;
     if (!ds.indices) return fail(RSM_EDEVICE, "rsm_decode: index buffer allocation failed");
-    if (int rc = launch_decode(ds, ctx->stream)) return rc;
+    if (int rc = launch_decode(ctx, ds, ctx->stream)) return rc;
     if ((e = hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, ctx->stream)) != hipSuccess)
         return hip_fail(e, "hipMemcpyAsync D2H");
     if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return hip_fail(e, "decode");
@@ -295,7 +361,7 @@ int rsm_extend_square(rsm_ctx* ctx, const uint8_t* ods, uint32_t k, uint32_t sha
     // Q0 straight into the top-left quadrant: the EDS aliases the ODS.
     if ((e = hipMemcpy2DAsync(d, W * S, ods, k * S, k * S, k, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess)
         return hip_fail(e, "hipMemcpy2DAsync H2D");
-    if (int rc = extend_squares(d, k, share_size, 1, ctx->stream)) return rc;
+    if (int rc = extend_squares(ctx, d, k, share_size, 1, ctx->stream)) return rc;
     if ((e = hipMemcpyAsync(eds, d, W * W * S, hipMemcpyDeviceToHost, ctx->stream)) != hipSuccess)
         return hip_fail(e, "hipMemcpyAsync D2H");
     if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return hip_fail(e, "extend");
@@ -308,7 +374,7 @@ int rsm_extend_squares_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share
     if (int rc = validate_chunk_size(share_size)) return rc;
     if (count == 0) return RSM_OK;
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-    return extend_squares(static_cast<uint8_t*>(d_eds), k, share_size, count, st);
+    return extend_squares(ctx, static_cast<uint8_t*>(d_eds), k, share_size, count, st);
 }
 
 int rsm_extend_squares_phase_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size, uint32_t count,
@@ -318,7 +384,7 @@ int rsm_extend_squares_phase_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t
     if (int rc = validate_chunk_size(share_size)) return rc;
     if (count == 0) return RSM_OK;
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-    return extend_squares(static_cast<uint8_t*>(d_eds), k, share_size, count, st, phase);
+    return extend_squares(ctx, static_cast<uint8_t*>(d_eds), k, share_size, count, st, phase);
 }
 
 int rsm_decode_vectors_dev(rsm_ctx* ctx, void* d_eds, const uint8_t* d_presence, uint32_t k,
@@ -336,7 +402,7 @@ int rsm_decode_vectors_dev(rsm_ctx* ctx, void* d_eds, const uint8_t* d_presence,
     ds.axis = (uint32_t)axis;
     ds.k = k;
     ds.S = share_size;
-    return launch_decode(ds, stream ? static_cast<hipStream_t>(stream) : ctx->stream);
+    return launch_decode(ctx, ds, stream ? static_cast<hipStream_t>(stream) : ctx->stream);
 }
 
 }  // extern "C"
@@ -399,9 +465,9 @@ int rsm_time_extend(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size, 
     int rc = RSM_OK;
     for (uint32_t r = 0; r < reps && rc == RSM_OK; ++r) {
         (void)hipEventRecord(ev[0], ctx->stream);
-        rc = extend_squares(static_cast<uint8_t*>(d_eds), k, share_size, count, ctx->stream, 1);
+        rc = extend_squares(ctx, static_cast<uint8_t*>(d_eds), k, share_size, count, ctx->stream, 1);
         (void)hipEventRecord(ev[1], ctx->stream);
-        if (rc == RSM_OK) rc = extend_squares(static_cast<uint8_t*>(d_eds), k, share_size, count, ctx->stream, 2);
+        if (rc == RSM_OK) rc = extend_squares(ctx, static_cast<uint8_t*>(d_eds), k, share_size, count, ctx->stream, 2);
         (void)hipEventRecord(ev[2], ctx->stream);
         if (hipEventSynchronize(ev[2]) != hipSuccess) rc = fail(RSM_EDEVICE, "hipEventSynchronize");
         float a = 0, b = 0;
