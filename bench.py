@@ -44,6 +44,7 @@ def parse():
     p.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     p.add_argument("--batch", type=int, default=0, help="squares per step (default: >= 512 MiB of EDS)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-c5", action="store_true", help="skip the config-5 (sharded 512x512 square) line")
     p.add_argument("--cpu-seconds", type=float, default=3.0)
     return p.parse_args()
 
@@ -66,6 +67,52 @@ def cpu_baseline(k, S, seconds):
             "kind": "port",
             "sample": f"{n} squares k={k} S={S} through oracle/leopard_oracle.c (scalar C restatement of "
                       f"klauspost leopard, {threads} threads over codewords); the Go reference cannot run here"}
+
+
+def bench_c5(world, rank, local, dist, steps, L, R):
+    """Config 5: one 512x512 -> 1024x1024 square (GF(2^16), 512 B shares).  N=1: the
+    whole square on one GPU; N>1: rows sharded over the N GPUs + RCCL all-gather of
+    the top half (rsmt2d_amd.distributed).  Strong scaling of a single square."""
+    k, S = 512, 512
+    W = 2 * k
+    steps = max(3, min(steps, 10))
+    if world == 1:
+        ctx = R.device_context(local)
+        buf = R.DeviceBuffer(W * W * S, local)
+        buf.fill_random(0xC5)
+        R._check(L.rsm_extend_squares_dev(ctx, buf.ptr, k, S, 1, None))
+        R._check(L.rsm_sync(ctx))
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            R._check(L.rsm_extend_squares_dev(ctx, buf.ptr, k, S, 1, None))
+        R._check(L.rsm_sync(ctx))
+        dt = (time.perf_counter() - t0) / steps
+        buf.free()
+    else:
+        import torch
+        from rsmt2d_amd.distributed import RowShardedExtender, hip_backend
+        eds = torch.zeros((W, W, S), dtype=torch.uint8, device=f"cuda:{local}")
+        ext = RowShardedExtender(k, S, *hip_backend(local))
+        r0, r1 = ext.rows
+        g = torch.Generator(device=f"cuda:{local}")
+        g.manual_seed(0xC5 + rank)
+        eds[r0:r1, :k] = torch.randint(0, 256, (r1 - r0, k, S), dtype=torch.uint8, device=eds.device, generator=g)
+        torch.cuda.synchronize()
+        ext.extend(eds)
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            ext.extend(eds)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=eds.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item()) / steps
+        del eds
+    return {"workload": "c5: 512x512->1024x1024 square, 512 B shares, GF(2^16)"
+                        + ("" if world == 1 else f", rows sharded over {world} GPUs + RCCL all-gather of [Q0|Q1]"),
+            "n_gpus": world, "ms_per_square": round(dt * 1e3, 4), "ods_GiB_s": round(k * k * S / dt / 2**30, 3),
+            "scaling": "strong (one square)"}
 
 
 def main():
@@ -199,6 +246,8 @@ def main():
                             "note": "rsm_extend_square: pageable host ODS -> H2D -> extend -> D2H EDS, one square"}
         out["cpu_baseline"] = None if a.no_cpu_baseline else cpu_baseline(k, S, a.cpu_seconds)
     buf.free()
+    if not a.no_c5:
+        out["c5"] = bench_c5(world, rank, local, dist, a.steps, L, R)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

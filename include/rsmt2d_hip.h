@@ -83,6 +83,14 @@ int rsm_extend_squares_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share
  * ([Q0|Q1] -> [Q2|Q3]); for per-kernel timing/profiling.  Asynchronous. */
 int rsm_extend_squares_phase_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size,
                                  uint32_t count, int phase, void* stream);
+/* Rows [row0, row0+nrows) / columns [col0, col0+ncols) of one in-place
+ * [2k][2k][S] square: the per-GPU units of the row-sharded multi-GPU schedule
+ * (rows of the top half on each GPU, an all-gather of [Q0|Q1], then each GPU's
+ * column slice).  Asynchronous on `stream` (NULL = context stream). */
+int rsm_extend_rows_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size, uint32_t row0,
+                        uint32_t nrows, void* stream);
+int rsm_extend_cols_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size, uint32_t col0,
+                        uint32_t ncols, void* stream);
 /* Device-resident batched reconstruct of whole rows (axis 0) or columns (axis 1)
  * of one [2k][2k][S] square: d_presence is one byte per cell, d_indices the
  * vectors to rebuild (each must have >= k cells present).  Asynchronous. */

@@ -387,6 +387,46 @@ int rsm_extend_squares_phase_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t
     return extend_squares(ctx, static_cast<uint8_t*>(d_eds), k, share_size, count, st, phase);
 }
 
+// Row / column slices of ONE in-place [2k][2k][S] square -- the per-GPU units of the
+// row-sharded multi-GPU schedule (erasureExtendRow / erasureExtendCol for a range).
+int rsm_extend_rows_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size, uint32_t row0, uint32_t nrows,
+                        void* stream) {
+    if (!ctx || !d_eds || k == 0 || row0 + nrows > 2 * k) return fail(RSM_EINVAL, "rsm_extend_rows_dev: bad arguments");
+    if (int rc = validate_chunk_size(share_size)) return rc;
+    if (nrows == 0) return RSM_OK;
+    const uint64_t W = 2ull * k, S = share_size;
+    CodewordSet cs{};
+    cs.base = static_cast<uint8_t*>(d_eds) + row0 * W * S;
+    cs.square_stride = 0;
+    cs.cw_stride = W * S;
+    cs.elem_stride = S;
+    cs.out_offset = k * S;
+    cs.per_square = nrows;
+    cs.count = nrows;
+    cs.k = k;
+    cs.S = share_size;
+    return launch_encode(ctx, cs, stream ? static_cast<hipStream_t>(stream) : ctx->stream);
+}
+
+int rsm_extend_cols_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size, uint32_t col0, uint32_t ncols,
+                        void* stream) {
+    if (!ctx || !d_eds || k == 0 || col0 + ncols > 2 * k) return fail(RSM_EINVAL, "rsm_extend_cols_dev: bad arguments");
+    if (int rc = validate_chunk_size(share_size)) return rc;
+    if (ncols == 0) return RSM_OK;
+    const uint64_t W = 2ull * k, S = share_size;
+    CodewordSet cs{};
+    cs.base = static_cast<uint8_t*>(d_eds) + col0 * S;
+    cs.square_stride = 0;
+    cs.cw_stride = S;
+    cs.elem_stride = W * S;
+    cs.out_offset = k * W * S;
+    cs.per_square = ncols;
+    cs.count = ncols;
+    cs.k = k;
+    cs.S = share_size;
+    return launch_encode(ctx, cs, stream ? static_cast<hipStream_t>(stream) : ctx->stream);
+}
+
 int rsm_decode_vectors_dev(rsm_ctx* ctx, void* d_eds, const uint8_t* d_presence, uint32_t k,
                            uint32_t share_size, int axis, const uint32_t* d_indices, uint32_t count,
                            void* stream) {

@@ -1,0 +1,61 @@
+"""GPU: the per-GPU units of the row-sharded schedule (config 5) and the
+RowShardedExtender on RCCL (world_size 1 on the one-GPU test box; N>1 runs in the
+driver's multi-GPU bench, the exchange logic is covered by test_distributed_cpu)."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import oracle
+import rsmt2d_amd as R
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("k,S,parts", [(64, 512, 4), (512, 512, 8)])
+def test_row_and_column_slices(lib, k, S, parts):
+    """Rows then columns in `parts` slices each == the full extension (what 8 ranks do)."""
+    W = 2 * k
+    ods = oracle.splitmix64_bytes(k * k * S, seed=99).reshape(k, k, S)
+    buf = R.DeviceBuffer(W * W * S)
+    full = np.zeros((W, W, S), np.uint8)
+    full[:k, :k] = ods
+    buf.upload(full)
+    for g in range(parts):
+        R._check(lib.rsm_extend_rows_dev(buf.ctx, buf.ptr, k, S, g * k // parts, k // parts, None))
+    for g in range(parts):
+        R._check(lib.rsm_extend_cols_dev(buf.ctx, buf.ptr, k, S, g * W // parts, W // parts, None))
+    R._check(lib.rsm_sync(buf.ctx))
+    got = buf.download().reshape(W, W, S)
+    assert (got == oracle.extend_square(ods, nthreads=min(16, os.cpu_count() or 1))).all()
+
+
+SCRIPT = r"""
+import os, sys
+sys.path.insert(0, {root!r})
+import numpy as np, torch, torch.distributed as dist
+os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT="29533", RANK="0", WORLD_SIZE="1")
+torch.cuda.set_device(0)
+dist.init_process_group("nccl")
+from rsmt2d_amd.distributed import RowShardedExtender, hip_backend
+import oracle
+k, S = 64, 512
+ods = np.random.default_rng(3).integers(0, 256, (k, k, S), dtype=np.uint8)
+eds = torch.zeros((2 * k, 2 * k, S), dtype=torch.uint8, device="cuda")
+eds[:k, :k] = torch.from_numpy(ods).cuda()
+torch.cuda.synchronize()
+ext = RowShardedExtender(k, S, *hip_backend(0))
+ext.extend(eds)
+ok = bool((eds.cpu().numpy() == oracle.extend_square(ods)).all())
+dist.destroy_process_group()
+print("SHARDED_OK" if ok else "SHARDED_MISMATCH")
+"""
+
+
+def test_row_sharded_extender_rccl_world1():
+    pytest.importorskip("torch")
+    r = subprocess.run([sys.executable, "-c", SCRIPT.format(root=ROOT)], capture_output=True, text=True, timeout=300)
+    assert "SHARDED_OK" in r.stdout, r.stdout + r.stderr

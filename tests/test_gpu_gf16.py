@@ -53,8 +53,8 @@ def test_survey_digest_k256(lib):
     gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "restatement.json")))
     want = [r for r in gold["affine_digests_survey"] if r["k"] == 256][0]["sha256"]
     got = np.empty((512, 512, 128), np.uint8)
-    R._check(lib.rsm_extend_square(R.device_context(), oracle.affine_pattern(256, 128).ctypes.data, 256, 128,
-                                   got.ctypes.data))
+    ods = oracle.affine_pattern(256, 128)  # keep the array alive across the C call
+    R._check(lib.rsm_extend_square(R.device_context(), ods.ctypes.data, 256, 128, got.ctypes.data))
     assert hashlib.sha256(got.tobytes()).hexdigest() == want
 
 
