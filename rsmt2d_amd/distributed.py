@@ -37,8 +37,8 @@ class RowShardedExtender:
     """Extends one [2k][2k][S] square (uint8 tensor, Q0 rows of this rank filled) in place."""
 
     def __init__(self, k: int, share_size: int, encode_rows: Callable, encode_cols: Callable,
-                 group: Optional[dist.ProcessGroup] = None, after_local: Optional[Callable] = None,
-                 before_local: Optional[Callable] = None):
+                 after_local: Optional[Callable] = None, before_local: Optional[Callable] = None, *,
+                 group: Optional[dist.ProcessGroup] = None):
         self.k, self.S = k, share_size
         self.group = group
         self.world = dist.get_world_size(group)
