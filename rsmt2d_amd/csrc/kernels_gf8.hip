@@ -53,16 +53,35 @@ __device__ __forceinline__ uint32_t vconst() {
     return v;
 }
 
-// x ^= y * exp(L)
+// x ^= y * exp(L), as ONE scheduling unit: the compiler, left to schedule the
+// twelve instructions freely, computes the partial products of many butterflies
+// ahead of their use and needs ~70 extra VGPRs; as a unit the temporaries die
+// inside it.  Pure register ops (no memory, no special hazards: VALU->VALU and
+// SALU->VALU dependencies are interlocked), so it is not volatile.
+// The two VGPR table halves (ta = a_lo, tb = b_lo) are materialised once per FFT
+// block by the caller and shared by the block's d butterflies.
+template <unsigned L>
+__device__ __forceinline__ void gf8_muladd_ct(uint32_t& x, uint32_t y, uint32_t ta, uint32_t tb) {
+    constexpr PermTab t = make_perm_tab(L);
+    uint32_t sa, sb, sc;
+    asm("v_lshrrev_b32 %[sb], 3, %[y]\n\t"
+        "v_lshrrev_b32 %[sc], 6, %[y]\n\t"
+        "v_and_b32 %[sa], %[m7], %[y]\n\t"
+        "v_and_b32 %[sb], %[m7], %[sb]\n\t"
+        "v_and_b32 %[sc], %[m3], %[sc]\n\t"
+        "v_perm_b32 %[sa], %[ahi], %[ta], %[sa]\n\t"
+        "v_perm_b32 %[sb], %[bhi], %[tb], %[sb]\n\t"
+        "v_perm_b32 %[sc], %[cc], %[cc], %[sc]\n\t"
+        "v_bitop3_b32 %[x], %[x], %[sa], %[sb] bitop3:0x96\n\t"
+        "v_xor_b32 %[x], %[x], %[sc]"
+        : [x] "+v"(x), [sa] "=&v"(sa), [sb] "=&v"(sb), [sc] "=&v"(sc)
+        : [y] "v"(y), [ta] "v"(ta), [tb] "v"(tb), [m7] "i"(0x07070707), [m3] "i"(0x03030303),
+          [ahi] "s"(t.a_hi), [bhi] "s"(t.b_hi), [cc] "s"(t.c));
+}
 template <unsigned L>
 __device__ __forceinline__ void gf8_muladd_ct(uint32_t& x, uint32_t y) {
     constexpr PermTab t = make_perm_tab(L);
-    const uint32_t sa = y & 0x07070707u;
-    const uint32_t sb = (y >> 3) & 0x07070707u;
-    const uint32_t sc = (y >> 6) & 0x03030303u;
-    x = xor3(x, __builtin_amdgcn_perm(t.a_hi, vconst<t.a_lo>(), sa),
-             __builtin_amdgcn_perm(t.b_hi, vconst<t.b_lo>(), sb)) ^
-        __builtin_amdgcn_perm(t.c, t.c, sc);
+    gf8_muladd_ct<L>(x, y, vconst<t.a_lo>(), vconst<t.b_lo>());
 }
 
 // Runtime (wave-uniform) log constant: tables for all 256 logs in constant memory.
@@ -115,12 +134,20 @@ __device__ __forceinline__ void ifft_layers(uint32_t (&w)[N]) {
         constexpr int lg = decltype(LG)::value;
         if constexpr ((1 << lg) < N) {
             constexpr int d = 1 << lg;
-            static_for<N / 2>([&](auto Q) {
-                constexpr int q = decltype(Q)::value;
-                constexpr int b = (q / d) * 2 * d;
-                constexpr int i = b + (q % d);
+            static_for<N / (2 * d)>([&](auto B) {
+                constexpr int b = decltype(B)::value * 2 * d;
                 constexpr unsigned L = kGf8.skew[OFF + b + d];
-                ifft2<L>(w[i], w[i + d]);
+                if constexpr (L == 255u) {
+                    static_for<d>([&](auto Q) { w[b + decltype(Q)::value + d] ^= w[b + decltype(Q)::value]; });
+                } else {
+                    constexpr PermTab t = make_perm_tab(L);
+                    const uint32_t ta = vconst<t.a_lo>(), tb = vconst<t.b_lo>();
+                    static_for<d>([&](auto Q) {
+                        constexpr int i = b + decltype(Q)::value;
+                        w[i + d] ^= w[i];
+                        gf8_muladd_ct<L>(w[i], w[i + d], ta, tb);
+                    });
+                }
             });
         }
     });
@@ -134,12 +161,20 @@ __device__ __forceinline__ void fft_layers(uint32_t (&w)[N]) {
         constexpr int lg = 15 - decltype(LG)::value;
         if constexpr ((1 << lg) < N) {
             constexpr int d = 1 << lg;
-            static_for<N / 2>([&](auto Q) {
-                constexpr int q = decltype(Q)::value;
-                constexpr int b = (q / d) * 2 * d;
-                constexpr int i = b + (q % d);
+            static_for<N / (2 * d)>([&](auto B) {
+                constexpr int b = decltype(B)::value * 2 * d;
                 constexpr unsigned L = kGf8.skew[OFF + b + d];
-                fft2<L>(w[i], w[i + d]);
+                if constexpr (L == 255u) {
+                    static_for<d>([&](auto Q) { w[b + decltype(Q)::value + d] ^= w[b + decltype(Q)::value]; });
+                } else {
+                    constexpr PermTab t = make_perm_tab(L);
+                    const uint32_t ta = vconst<t.a_lo>(), tb = vconst<t.b_lo>();
+                    static_for<d>([&](auto Q) {
+                        constexpr int i = b + decltype(Q)::value;
+                        gf8_muladd_ct<L>(w[i], w[i + d], ta, tb);
+                        w[i + d] ^= w[i];
+                    });
+                }
             });
         }
     });
@@ -172,7 +207,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p) {
 // codeword of a CodewordSet.  M = ceilPow2(k).
 // ---------------------------------------------------------------------------
 template <int M>
-__global__ __launch_bounds__(256, (M >= 128 ? 2 : 3)) void encode_gf8_kernel(CodewordSet cs) {
+__global__ __launch_bounds__(256, 3) void encode_gf8_kernel(CodewordSet cs) {
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t chunks = cs.chunks;
