@@ -45,6 +45,7 @@ def parse():
     p.add_argument("--batch", type=int, default=0, help="squares per step (default: >= 512 MiB of EDS)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-c5", action="store_true", help="skip the config-5 (sharded 512x512 square) line")
+    p.add_argument("--no-c3", action="store_true", help="skip the config-3 (Repair) timings")
     p.add_argument("--cpu-seconds", type=float, default=3.0)
     return p.parse_args()
 
@@ -113,6 +114,99 @@ def bench_c5(world, rank, local, dist, steps, L, R):
                         + ("" if world == 1 else f", rows sharded over {world} GPUs + RCCL all-gather of [Q0|Q1]"),
             "n_gpus": world, "ms_per_square": round(dt * 1e3, 4), "ods_GiB_s": round(k * k * S / dt / 2**30, 3),
             "scaling": "strong (one square)"}
+
+
+def bench_c3(local, L, R, repeats=5):
+    """Config 3: k=128, S=512, exactly k of the 2k cells of every
+    row erased (BenchmarkRepair's scheme, extendeddatacrossword_test.go:443-453),
+    honest DefaultTree roots.  Two timings:
+      decode_sweep -- the device decode of all 2k rows alone (rsm_decode_vectors_dev
+                      over a device-resident EDS + presence mask, HIP-synchronised);
+      repair       -- (*ExtendedDataSquare).Repair end to end as BenchmarkRepair
+                      times it (import untimed): upload, device sweeps, full
+                      re-extension check, host SHA-256 roots of every row/col.
+    Replicas only: Repair is not sharded."""
+    import ctypes
+    import numpy as np
+    k, S = 128, 512
+    W = 2 * k
+    ctx = R.device_context(local)
+    rng = np.random.default_rng(0xC3)
+    # original EDS from the device extension of a seeded ODS
+    buf = R.DeviceBuffer(W * W * S, local)
+    buf.fill_random(0xC3)
+    R._check(L.rsm_extend_squares_dev(ctx, buf.ptr, k, S, 1, None))
+    R._check(L.rsm_sync(ctx))
+    full = buf.download(W * W * S).reshape(W, W, S)
+    present = np.ones((W, W), np.uint8)
+    for r in range(W):
+        present[r, rng.choice(W, size=k, replace=False)] = 0
+
+    # honest roots
+    base = full.ctypes.data
+    ptrs = (ctypes.c_void_p * (W * W))(*[base + i * S for i in range(W * W)])
+    lens = (ctypes.c_uint32 * (W * W))(*([S] * (W * W)))
+    h = ctypes.c_void_p()
+    R._check(L.rsm_eds_import(None, ptrs, lens, W * W, ctypes.byref(h)))
+    roots = {}
+    for axis in (0, 1):
+        out = ctypes.create_string_buffer(W * 32)
+        rl = ctypes.c_uint32()
+        R._check(L.rsm_eds_roots(h, axis, None, None, out, 32, ctypes.byref(rl)))  # NULL = DefaultTree
+        roots[axis] = out.raw
+    L.rsm_eds_free(h)
+
+    # (1) device decode sweep alone
+    damaged = full * present[:, :, None]
+    buf.upload(damaged)
+    pres_d = R.DeviceBuffer(W * W, local)
+    pres_d.upload(present)
+    idx_d = R.DeviceBuffer(4 * W, local)
+    idx_d.upload(np.arange(W, dtype=np.uint32))
+    sweep = lambda: R._check(L.rsm_decode_vectors_dev(ctx, buf.ptr, pres_d.ptr, k, S, 0, idx_d.ptr, W, None))
+    sweep()
+    R._check(L.rsm_sync(ctx))
+    if not np.array_equal(buf.download(W * W * S).reshape(W, W, S), full):
+        raise SystemExit("bench c3: device decode sweep differs from the original EDS")
+    n_sw = 50
+    t0 = time.perf_counter()
+    for _ in range(n_sw):
+        sweep()
+    R._check(L.rsm_sync(ctx))
+    t_sweep = (time.perf_counter() - t0) / n_sw
+    for b in (buf, pres_d, idx_d):
+        b.free()
+
+    # (2) end-to-end Repair (import untimed, as BenchmarkRepair)
+    flat_ptrs = (ctypes.c_void_p * (W * W))(*[base + i * S if present.flat[i] else None for i in range(W * W)])
+    flat_lens = (ctypes.c_uint32 * (W * W))(*[S if present.flat[i] else 0 for i in range(W * W)])
+    times, stats = [], R.RepairStats()
+    for _ in range(repeats):
+        h = ctypes.c_void_p()
+        R._check(L.rsm_eds_import(None, flat_ptrs, flat_lens, W * W, ctypes.byref(h)))
+        R._check(L.rsm_eds_set_context(h, ctx))
+        byz = R._Byz()
+        t0 = time.perf_counter()
+        R._check(L.rsm_eds_repair(h, roots[0], roots[1], 32, None, None, ctypes.byref(byz)))
+        times.append(time.perf_counter() - t0)
+        R._check(L.rsm_eds_repair_stats(h, ctypes.byref(stats)))
+        if repeats and len(times) == 1:
+            got = np.empty((W, W, S), np.uint8)
+            pr = np.empty((W, W), np.uint8)
+            R._check(L.rsm_eds_flattened(h, got.ctypes.data, pr.ctypes.data))
+            if not (pr.all() and np.array_equal(got, full)):
+                raise SystemExit("bench c3: repaired EDS differs from the original")
+        L.rsm_eds_free(h)
+    t_rep = sorted(times)[len(times) // 2]
+    algo = W * W * S  # SURVEY §8(d): present shares read + missing shares written
+    return {"workload": "c3: k=128, S=512, 128 of 256 cells erased in every row (BenchmarkRepair scheme)",
+            "decode_sweep_us": round(t_sweep * 1e6, 2),
+            "decode_sweep_GB_s": round(algo / t_sweep / 1e9, 1),
+            "decode_sweep_frac": round(algo / t_sweep / 1e9 / HBM_PEAK_GBS, 4),
+            "repair_ms": round(t_rep * 1e3, 3), "repair_samples": repeats,
+            "repair_fast_path": int(stats.fast_path), "repair_sweeps": int(stats.sweeps),
+            "note": "repair = rsm_eds_repair end to end (H2D, device sweeps, re-extension check, "
+                    "host SHA-256 roots of all 512 vectors, D2H); median of samples"}
 
 
 def main():
@@ -246,6 +340,8 @@ def main():
                             "note": "rsm_extend_square: pageable host ODS -> H2D -> extend -> D2H EDS, one square"}
         out["cpu_baseline"] = None if a.no_cpu_baseline else cpu_baseline(k, S, a.cpu_seconds)
     buf.free()
+    if rank == 0 and world == 1 and not a.no_c3:
+        out["c3"] = bench_c3(local, L, R)
     if not a.no_c5:
         out["c5"] = bench_c5(world, rank, local, dist, a.steps, L, R)
     if rank == 0:

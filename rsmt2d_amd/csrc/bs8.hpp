@@ -1,0 +1,191 @@
+// bs8.hpp -- bit-sliced GF(2^8) Leopard encode arithmetic (host + device).
+//
+// Representation: 32 bytes of one symbol position range are held as 8 u32
+// bit-planes (plane i = bit i of each of the 32 bytes).  Multiplication by a
+// compile-time constant exp(L) is then a fixed GF(2)-linear map of the planes:
+//   out_i = XOR_{j : bit i of (2^j * exp(L)) = 1} y_j
+// i.e. ~4 plane XORs per output plane, 2 per v_bitop3_b32 (3-input XOR) -- about
+// 16 VALU per 32 bytes, against 80 for the byte-table (v_perm) multiply.
+//
+// The additive-FFT schedule is the one of kernels_gf8.hip (IFFT_DIT layers
+// d = 1..M/2 with skew offset M-1, then FFT_DIT layers M/2..1 with offset -1;
+// SURVEY.md Appendix A.4, klauspost leopard8.go ifftDITEncoder8/fftDIT8), split
+// for M = 128 into
+//   small layers d = 1, 2, 4   on 16 consecutive symbols e = 16a + j  (fixed a)
+//   large layers d = 8 .. 64   on 16 strided symbols   e = 8h + g    (fixed g)
+// so that a thread never needs more than 16 symbols x 8 planes = 128 registers,
+// and every twiddle is a compile-time constant within a (small: a / large: all)
+// specialisation.  This header holds the arithmetic only; the data movement
+// (global loads, the LDS exchange between the two layouts) is in
+// kernels_gf8_bs.hip, and tests/native/bs8_host.cpp runs the same templates on
+// the CPU against the oracle.
+#pragma once
+#include <cstdint>
+#include <utility>
+#include "gf_tables.hpp"
+
+#if defined(__HIPCC__)
+#define RSM_HD __host__ __device__ __forceinline__
+#else
+#define RSM_HD inline __attribute__((always_inline))
+#endif
+
+namespace rsm::bs8 {
+
+template <int N, typename F>
+RSM_HD void sfor(F&& f) {
+    [&]<int... I>(std::integer_sequence<int, I...>) {
+        (f(std::integral_constant<int, I>{}), ...);
+    }(std::make_integer_sequence<int, N>{});
+}
+
+// acc ^= b ^ c  /  acc ^= b.  On the device each is one volatile instruction, so
+// the network runs in program order and updates its planes in place: left to
+// schedule compiler-generated XORs freely, LLVM hoists and shares terms across
+// butterflies and across the 8 per-wave variants of the small layers and spills
+// hundreds of VGPRs (measured: 355 spills, -25% throughput).  Plain 32-bit VALU
+// ops interlock on each other; the boundary to compiler-generated code (which
+// may copy these registers with 64-bit moves) is padded in kernels_gf8_bs.hip.
+RSM_HD void xor3_into(uint32_t& acc, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(acc) : "v"(b), "v"(c));
+#else
+    acc ^= b ^ c;
+#endif
+}
+RSM_HD void xor_into(uint32_t& acc, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("v_xor_b32 %0, %0, %1" : "+v"(acc) : "v"(b));
+#else
+    acc ^= b;
+#endif
+}
+
+// rows[i] has bit j set iff bit i of (2^j * exp(L)) is set.
+struct Rows {
+    uint8_t r[8];
+};
+constexpr Rows mul_rows(unsigned L) {
+    Rows m{};
+    for (unsigned j = 0; j < 8; ++j) {
+        const unsigned p = gf8_mul_log(1u << j, L);
+        for (unsigned i = 0; i < 8; ++i)
+            if ((p >> i) & 1u) m.r[i] = static_cast<uint8_t>(m.r[i] | (1u << j));
+    }
+    return m;
+}
+
+constexpr int ctz8(unsigned m) {
+    int i = 0;
+    while (!((m >> i) & 1u)) ++i;
+    return i;
+}
+
+// acc ^= XOR of y[j] for the bits j of MASK, two planes per 3-input XOR.
+template <unsigned MASK>
+RSM_HD void acc_terms(uint32_t& acc, const uint32_t (&y)[8]) {
+    if constexpr (MASK != 0) {
+        constexpr int j1 = ctz8(MASK);
+        constexpr unsigned rest = MASK & (MASK - 1);
+        if constexpr (rest == 0) {
+            xor_into(acc, y[j1]);
+        } else {
+            constexpr int j2 = ctz8(rest);
+            xor3_into(acc, y[j1], y[j2]);
+            acc_terms<rest & (rest - 1)>(acc, y);
+        }
+    }
+}
+
+// x ^= y * exp(L)
+template <unsigned L>
+RSM_HD void muladd(uint32_t (&x)[8], const uint32_t (&y)[8]) {
+    constexpr Rows R = mul_rows(L);
+    sfor<8>([&](auto I) { acc_terms<R.r[decltype(I)::value]>(x[decltype(I)::value], y); });
+}
+
+// IFFT_DIT2: y ^= x; x ^= y*L.   FFT_DIT2: x ^= y*L; y ^= x.   L == 255: XOR only.
+template <unsigned L>
+RSM_HD void ifft2(uint32_t (&x)[8], uint32_t (&y)[8]) {
+    sfor<8>([&](auto I) { xor_into(y[decltype(I)::value], x[decltype(I)::value]); });
+    if constexpr (L != 255u) muladd<L>(x, y);
+}
+template <unsigned L>
+RSM_HD void fft2(uint32_t (&x)[8], uint32_t (&y)[8]) {
+    if constexpr (L != 255u) muladd<L>(x, y);
+    sfor<8>([&](auto I) { xor_into(y[decltype(I)::value], x[decltype(I)::value]); });
+}
+
+// 8x8 bit-matrix transpose applied to each of the 4 byte lanes of 8 words:
+// afterwards bit q of byte b of w[p] = bit p of byte b of the original w[q].
+// An involution: the same network converts bytes -> planes and planes -> bytes.
+RSM_HD void swapbits(uint32_t& a, uint32_t& b, int s, uint32_t m) {
+    const uint32_t t = ((a >> s) ^ b) & m;
+    b ^= t;
+    a ^= t << s;
+}
+RSM_HD void transpose8(uint32_t (&w)[8]) {
+    swapbits(w[0], w[4], 4, 0x0F0F0F0Fu);
+    swapbits(w[1], w[5], 4, 0x0F0F0F0Fu);
+    swapbits(w[2], w[6], 4, 0x0F0F0F0Fu);
+    swapbits(w[3], w[7], 4, 0x0F0F0F0Fu);
+    swapbits(w[0], w[2], 2, 0x33333333u);
+    swapbits(w[1], w[3], 2, 0x33333333u);
+    swapbits(w[4], w[6], 2, 0x33333333u);
+    swapbits(w[5], w[7], 2, 0x33333333u);
+    swapbits(w[0], w[1], 1, 0x55555555u);
+    swapbits(w[2], w[3], 1, 0x55555555u);
+    swapbits(w[4], w[5], 1, 0x55555555u);
+    swapbits(w[6], w[7], 1, 0x55555555u);
+}
+
+constexpr int kM = 128;        // transform size handled here (65 <= k <= 128)
+constexpr int kOffEnc = kM - 1;  // encoder IFFT skew offset
+
+// Small layers: registers j = 0..15 hold symbols e = 16A + j.
+template <int A>
+RSM_HD void small_ifft(uint32_t (&X)[16][8]) {
+    sfor<3>([&](auto LG) {
+        constexpr int d = 1 << decltype(LG)::value;
+        sfor<16 / (2 * d)>([&](auto B) {
+            constexpr int b = decltype(B)::value * 2 * d;
+            constexpr unsigned L = kGf8.skew[kOffEnc + 16 * A + b + d];
+            sfor<d>([&](auto Q) { ifft2<L>(X[b + decltype(Q)::value], X[b + decltype(Q)::value + d]); });
+        });
+    });
+}
+template <int A>
+RSM_HD void small_fft(uint32_t (&X)[16][8]) {
+    sfor<3>([&](auto LG) {
+        constexpr int d = 4 >> decltype(LG)::value;
+        sfor<16 / (2 * d)>([&](auto B) {
+            constexpr int b = decltype(B)::value * 2 * d;
+            constexpr unsigned L = kGf8.skew[-1 + 16 * A + b + d];
+            sfor<d>([&](auto Q) { fft2<L>(X[b + decltype(Q)::value], X[b + decltype(Q)::value + d]); });
+        });
+    });
+}
+
+// Large layers: registers h = 0..15 hold symbols e = 8h + g (any g < 8): the
+// pairing bit is a bit of h and the block start 8*(h & ~(2dh-1)) does not
+// depend on g, so one code path serves every g.
+RSM_HD void large_ifft_fft(uint32_t (&X)[16][8]) {
+    sfor<4>([&](auto LG) {  // IFFT d = 8, 16, 32, 64
+        constexpr int dh = 1 << decltype(LG)::value;
+        sfor<16 / (2 * dh)>([&](auto B) {
+            constexpr int hb = decltype(B)::value * 2 * dh;
+            constexpr unsigned L = kGf8.skew[kOffEnc + 8 * hb + 8 * dh];
+            sfor<dh>([&](auto Q) { ifft2<L>(X[hb + decltype(Q)::value], X[hb + decltype(Q)::value + dh]); });
+        });
+    });
+    sfor<4>([&](auto LG) {  // FFT d = 64, 32, 16, 8
+        constexpr int dh = 8 >> decltype(LG)::value;
+        sfor<16 / (2 * dh)>([&](auto B) {
+            constexpr int hb = decltype(B)::value * 2 * dh;
+            constexpr unsigned L = kGf8.skew[-1 + 8 * hb + 8 * dh];
+            sfor<dh>([&](auto Q) { fft2<L>(X[hb + decltype(Q)::value], X[hb + decltype(Q)::value + dh]); });
+        });
+    });
+}
+
+}  // namespace rsm::bs8

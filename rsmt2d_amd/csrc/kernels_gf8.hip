@@ -22,6 +22,8 @@
 // zero-padding (exact: see DESIGN.md "Truncation").
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <cstdlib>
+#include <cstring>
 #include <utility>
 #include "gf_tables.hpp"
 #include "rsm_kernels.hpp"
@@ -426,7 +428,17 @@ static hipError_t launch_enc(const CodewordSet& cs, hipStream_t st) {
     return hipGetLastError();
 }
 
+// RSM_GF8_KERNEL=table forces the byte-table kernel for M = 128 (A/B measurements).
+static bool bs128_enabled() {
+    static const bool on = [] {
+        const char* v = getenv("RSM_GF8_KERNEL");
+        return !(v && strcmp(v, "table") == 0);
+    }();
+    return on;
+}
+
 hipError_t launch_encode_gf8(const CodewordSet& cs, hipStream_t st) {
+    if (bs128_enabled() && bs128_applicable(cs)) return launch_encode_gf8_bs128(cs, st);
     switch (ceil_pow2(cs.k)) {
         case 1: return launch_enc<1>(cs, st);
         case 2: return launch_enc<2>(cs, st);

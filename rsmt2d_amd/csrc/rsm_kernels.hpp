@@ -47,6 +47,9 @@ struct DecodeSet {
 };
 
 hipError_t launch_encode_gf8(const CodewordSet& cs, hipStream_t st);
+// bit-sliced M = 128 encode (kernels_gf8_bs.hip); launch_encode_gf8 picks it when applicable
+bool bs128_applicable(const CodewordSet& cs);
+hipError_t launch_encode_gf8_bs128(const CodewordSet& cs, hipStream_t st);
 hipError_t launch_decode_gf8(const DecodeSet& ds, hipStream_t st);
 struct Gf16Dev;
 hipError_t launch_encode_gf16(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st);

@@ -20,7 +20,7 @@ def test_encode_matches_oracle(lib, rng, k, S):
     assert R.NewLeoRSCodec().Encode(data) == oracle.encode(data)
 
 
-@pytest.mark.parametrize("S", [64, 192, 320, 1024])
+@pytest.mark.parametrize("S", [64, 192, 320, 1024, 2112, 4096])
 def test_encode_partial_chunks(lib, rng, S):
     data = rand_shares(rng, 128, S)
     assert R.NewLeoRSCodec().Encode(data) == oracle.encode(data)
@@ -89,6 +89,16 @@ def test_extend_squares_dev_batched(lib):
     for i in range(n):
         assert (got[i] == oracle.extend_square(ref[i, :k, :k].copy(), nthreads=8)).all(), i
     buf.free()
+
+
+@pytest.mark.parametrize("k,S", [(65, 64), (100, 2112), (128, 3072)])
+def test_extend_square_bitsliced_shapes(lib, rng, k, S):
+    """M = 128 squares whose 2 KiB bit-sliced sets straddle codewords / shares."""
+    ods = rng.integers(0, 256, (k, k, S), dtype=np.uint8)
+    want = oracle.extend_square(ods, nthreads=8)
+    got = np.empty_like(want)
+    R._check(lib.rsm_extend_square(R.device_context(), ods.ctypes.data, k, S, got.ctypes.data))
+    assert (got == want).all()
 
 
 def test_affine_digest_k128(lib):

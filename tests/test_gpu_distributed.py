@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize("k,S,parts", [(64, 512, 4), (512, 512, 8)])
+@pytest.mark.parametrize("k,S,parts", [(64, 512, 4), (128, 512, 4), (128, 1088, 2), (512, 512, 8)])
 def test_row_and_column_slices(lib, k, S, parts):
     """Rows then columns in `parts` slices each == the full extension (what 8 ranks do)."""
     W = 2 * k
