@@ -46,6 +46,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-c5", action="store_true", help="skip the config-5 (sharded 512x512 square) line")
     p.add_argument("--no-c3", action="store_true", help="skip the config-3 (Repair) timings")
+    p.add_argument("--dist", action="store_true",
+                   help="initialise torch.distributed even at N=1 (rehearses the sharded c5 path on one GPU)")
     p.add_argument("--cpu-seconds", type=float, default=3.0)
     return p.parse_args()
 
@@ -72,12 +74,14 @@ def cpu_baseline(k, S, seconds):
 
 def bench_c5(world, rank, local, dist, steps, L, R):
     """Config 5: one 512x512 -> 1024x1024 square (GF(2^16), 512 B shares).  N=1: the
-    whole square on one GPU; N>1: rows sharded over the N GPUs + RCCL all-gather of
-    the top half (rsmt2d_amd.distributed).  Strong scaling of a single square."""
+    whole square on one GPU; N>1: rows sharded over the N GPUs, then an RCCL
+    all-to-all hands every GPU its column slice of the top half (SURVEY §8(e) Option B,
+    rsmt2d_amd.distributed.TransposeShardedExtender); the all-gather schedule (Option
+    A) is timed beside it.  Strong scaling of a single square."""
     k, S = 512, 512
     W = 2 * k
     steps = max(3, min(steps, 10))
-    if world == 1:
+    if dist is None:
         ctx = R.device_context(local)
         buf = R.DeviceBuffer(W * W * S, local)
         buf.fill_random(0xC5)
@@ -91,29 +95,52 @@ def bench_c5(world, rank, local, dist, steps, L, R):
         buf.free()
     else:
         import torch
-        from rsmt2d_amd.distributed import RowShardedExtender, hip_backend
-        eds = torch.zeros((W, W, S), dtype=torch.uint8, device=f"cuda:{local}")
+        from rsmt2d_amd.distributed import (RowShardedExtender, TransposeShardedExtender, hip_backend,
+                                            hip_transpose_backend)
+        dev = torch.device("cuda", local)
+        g = torch.Generator(device=dev)
+        g.manual_seed(0xC5 + rank)
+
+        def timed(fn):
+            fn()
+            torch.cuda.synchronize()
+            dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                fn()
+            torch.cuda.synchronize()
+            dist.barrier()
+            t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            return float(t.item()) / steps
+
+        # Option B (primary): all-to-all of column slices
+        tx = TransposeShardedExtender(k, S, *hip_transpose_backend(local))
+        n, w = k // world, W // world
+        rows = torch.zeros((n, W, S), dtype=torch.uint8, device=dev)
+        rows[:, :k] = torch.randint(0, 256, (n, k, S), dtype=torch.uint8, device=dev, generator=g)
+        top = torch.empty((k, w, S), dtype=torch.uint8, device=dev)
+        bottom = torch.empty_like(top)
+        torch.cuda.synchronize()
+        dt = timed(lambda: tx.extend(rows, top, bottom))
+        del rows, top, bottom
+        # Option A (north_star's all-gather of the top half), for comparison
+        eds = torch.zeros((W, W, S), dtype=torch.uint8, device=dev)
         ext = RowShardedExtender(k, S, *hip_backend(local))
         r0, r1 = ext.rows
-        g = torch.Generator(device=f"cuda:{local}")
-        g.manual_seed(0xC5 + rank)
-        eds[r0:r1, :k] = torch.randint(0, 256, (r1 - r0, k, S), dtype=torch.uint8, device=eds.device, generator=g)
+        eds[r0:r1, :k] = torch.randint(0, 256, (r1 - r0, k, S), dtype=torch.uint8, device=dev, generator=g)
         torch.cuda.synchronize()
-        ext.extend(eds)
-        dist.barrier()
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            ext.extend(eds)
-        torch.cuda.synchronize()
-        dist.barrier()
-        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=eds.device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item()) / steps
+        dt_ag = timed(lambda: ext.extend(eds))
         del eds
-    return {"workload": "c5: 512x512->1024x1024 square, 512 B shares, GF(2^16)"
-                        + ("" if world == 1 else f", rows sharded over {world} GPUs + RCCL all-gather of [Q0|Q1]"),
-            "n_gpus": world, "ms_per_square": round(dt * 1e3, 4), "ods_GiB_s": round(k * k * S / dt / 2**30, 3),
-            "scaling": "strong (one square)"}
+    out = {"workload": "c5: 512x512->1024x1024 square, 512 B shares, GF(2^16)"
+                       + ("" if world == 1 else f", rows sharded over {world} GPUs + RCCL all-to-all of column slices"),
+           "n_gpus": world, "ms_per_square": round(dt * 1e3, 4), "ods_GiB_s": round(k * k * S / dt / 2**30, 3),
+           "scaling": "strong (one square)"}
+    if dist is not None:
+        out["received_bytes_per_gpu"] = (world - 1) * (k // world) * (W // world) * S
+        out["allgather_ms_per_square"] = round(dt_ag * 1e3, 4)
+        out["allgather_received_bytes_per_gpu"] = (world - 1) * (k // world) * W * S
+    return out
 
 
 def bench_c3(local, L, R, repeats=5):
@@ -217,7 +244,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world > 1:
+    if world > 1 or a.dist:
         # torch.distributed only for the timing barrier and the max-over-ranks of the
         # elapsed time (the workload itself has no data-path exchange).  torch's own HIP
         # runtime must initialise before librsmt2d_hip.so is loaded.

@@ -91,6 +91,13 @@ int rsm_extend_rows_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_si
                         uint32_t nrows, void* stream);
 int rsm_extend_cols_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size, uint32_t col0,
                         uint32_t ncols, void* stream);
+/* Generic device batch of `count` codewords (k data shares -> k parity shares each,
+ * the Encode of leopard.go:28-45 for every codeword): data share e of codeword q is
+ * at d_in + q*cw_stride + e*share_stride, its parity share e is written at
+ * d_out + q*cw_stride + e*share_stride (byte strides).  Used for the compact
+ * column slices of the all-to-all multi-GPU schedule.  Asynchronous. */
+int rsm_encode_batch_dev(rsm_ctx* ctx, const void* d_in, void* d_out, uint32_t k, uint32_t share_size,
+                         uint32_t count, uint64_t cw_stride, uint64_t share_stride, void* stream);
 /* Device-resident batched reconstruct of whole rows (axis 0) or columns (axis 1)
  * of one [2k][2k][S] square: d_presence is one byte per cell, d_indices the
  * vectors to rebuild (each must have >= k cells present).  Asynchronous. */

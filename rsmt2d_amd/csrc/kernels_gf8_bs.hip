@@ -111,60 +111,112 @@ __device__ __forceinline__ void exchange(uint32_t (&X)[16][8], v4u* lds, uint32_
 
 }  // namespace
 
-__global__ __launch_bounds__(512, 1) void encode_gf8_bs128_kernel(CodewordSet cs) {
-    __shared__ v4u lds[128 * 64];
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t lane = threadIdx.x & 63u;
+// Per-set addressing: a set is virtual bytes [2048 t, 2048 t + 2048) of the
+// concatenated shares of the CodewordSet; lane l's two 16-byte pieces are at
+// set bytes 16l and 1024 + 16l.  off[] are relative to the set's first codeword.
+struct SetAddr {
+    __amdgpu_buffer_rsrc_t rs, ro;
+    uint32_t off[2];
+};
+
+__device__ __forceinline__ SetAddr set_addr(const CodewordSet& cs, uint32_t t, uint32_t lane) {
+    SetAddr a;
     const uint32_t S = cs.S;
-    // set = virtual bytes [2048 b, 2048 b + 2048) of the concatenated shares
-    const uint64_t v0 = (uint64_t)blockIdx.x * kSetBytes;
+    const uint64_t v0 = (uint64_t)t * kSetBytes;
     const uint32_t q0 = __builtin_amdgcn_readfirstlane((uint32_t)(v0 / S));
     const uint32_t r0 = __builtin_amdgcn_readfirstlane((uint32_t)(v0 - (uint64_t)q0 * S));
     const uint64_t rel0 = cw_rel_bs(cs, q0);
-    uint32_t off[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         const uint32_t v = r0 + 1024u * h + 16u * lane;  // < S + 2048
         const uint32_t dq = v / S;
         const uint32_t q = q0 + dq;
         const uint32_t o = v - dq * S;
-        off[h] = q < cs.count ? (uint32_t)(cw_rel_bs(cs, q) - rel0) + o : kOobBs;
+        a.off[h] = q < cs.count ? (uint32_t)(cw_rel_bs(cs, q) - rel0) + o : kOobBs;
     }
-    const __amdgpu_buffer_rsrc_t rs = make_rsrc_bs(cs.base + rel0);
-    const __amdgpu_buffer_rsrc_t ro = make_rsrc_bs(cs.out_base + rel0);
+    a.rs = make_rsrc_bs(cs.base + rel0);
+    a.ro = make_rsrc_bs(cs.out_base + rel0);
+    return a;
+}
+
+__device__ __forceinline__ uint32_t sym_off(uint32_t e, uint32_t k, uint32_t base, uint32_t es) {
+    return __builtin_amdgcn_readfirstlane(e < k ? base + e * es : kOobBs);
+}
+
+// Symbols j < kPre of every wave's small-layout group are prefetched into LDS
+// (LDS-DMA, no VGPRs) while the previous set finishes; the rest load to VGPRs.
+// P layout: [wave][j][half][lane] x 16 B = 128 KiB, time-shared with the
+// exchange buffer (P is consumed before the first exchange and refilled after
+// the second).
+constexpr int kPre = 8;
+
+__device__ __forceinline__ void prefetch_set(const CodewordSet& cs, uint32_t t, uint32_t wv, uint32_t lane,
+                                             v4u* lds) {
+    const SetAddr a = set_addr(cs, t, lane);
+    const uint32_t k = cs.k, es = (uint32_t)cs.elem_stride;
+    bs8::sfor<kPre>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        const uint32_t so = sym_off(16u * wv + j, k, 0, es);
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                a.rs, (__attribute__((address_space(3))) void*)&lds[((wv * kPre + j) * 2 + h) * 64], 16, a.off[h],
+                so, 0, 0);
+    });
+}
+
+// Persistent: one workgroup per CU walks sets t = blockIdx.x, += gridDim.x.
+__global__ __launch_bounds__(512, 1) void encode_gf8_bs128_kernel(CodewordSet cs, uint32_t sets) {
+    __shared__ v4u lds[128 * 64];
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
     const uint32_t k = cs.k;
     const uint32_t es = (uint32_t)cs.elem_stride;
-
-    uint32_t X[16][8];
-    bs8::sfor<16>([&](auto J) {
-        constexpr int j = decltype(J)::value;
-        const uint32_t e = 16u * wv + j;
-        const uint32_t so = __builtin_amdgcn_readfirstlane(e < k ? e * es : kOobBs);
-        const v4u a = __builtin_amdgcn_raw_buffer_load_b128(rs, off[0], so, 0);
-        const v4u b = __builtin_amdgcn_raw_buffer_load_b128(rs, off[1], so, 0);
-        X[j][0] = a.x; X[j][1] = a.y; X[j][2] = a.z; X[j][3] = a.w;
-        X[j][4] = b.x; X[j][5] = b.y; X[j][6] = b.z; X[j][7] = b.w;
-    });
-    bs8::sfor<16>([&](auto J) { bs8::transpose8(X[decltype(J)::value]); });
-
-    small_layers<true>(wv, X);
-    exchange<true>(X, lds, wv, lane);
-    bs8::large_ifft_fft(X);
-    exchange<false>(X, lds, wv, lane);
-    small_layers<false>(wv, X);
-
     const uint32_t oo = (uint32_t)cs.out_offset;
-    bs8::sfor<16>([&](auto J) {
-        constexpr int j = decltype(J)::value;
-        bs8::transpose8(X[j]);
-        const uint32_t e = 16u * wv + j;
-        const uint32_t so = __builtin_amdgcn_readfirstlane(e < k ? oo + e * es : kOobBs);
-        v4u a, b;
-        a.x = X[j][0]; a.y = X[j][1]; a.z = X[j][2]; a.w = X[j][3];
-        b.x = X[j][4]; b.y = X[j][5]; b.z = X[j][6]; b.w = X[j][7];
-        __builtin_amdgcn_raw_buffer_store_b128(a, ro, off[0], so, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(b, ro, off[1], so, 0);
-    });
+    uint32_t t = blockIdx.x;
+    if (t >= sets) return;
+    prefetch_set(cs, t, wv, lane, lds);
+
+    for (; t < sets; t += gridDim.x) {
+        const SetAddr a = set_addr(cs, t, lane);
+        uint32_t X[16][8];
+        bs8::sfor<16 - kPre>([&](auto J) {
+            constexpr int j = kPre + decltype(J)::value;
+            const uint32_t so = sym_off(16u * wv + j, k, 0, es);
+            const v4u x = __builtin_amdgcn_raw_buffer_load_b128(a.rs, a.off[0], so, 0);
+            const v4u y = __builtin_amdgcn_raw_buffer_load_b128(a.rs, a.off[1], so, 0);
+            X[j][0] = x.x; X[j][1] = x.y; X[j][2] = x.z; X[j][3] = x.w;
+            X[j][4] = y.x; X[j][5] = y.y; X[j][6] = y.z; X[j][7] = y.w;
+        });
+        __syncthreads();  // prefetched symbols landed (waits on the LDS-DMA)
+        bs8::sfor<kPre>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            const v4u x = lds[((wv * kPre + j) * 2 + 0) * 64 + lane];
+            const v4u y = lds[((wv * kPre + j) * 2 + 1) * 64 + lane];
+            X[j][0] = x.x; X[j][1] = x.y; X[j][2] = x.z; X[j][3] = x.w;
+            X[j][4] = y.x; X[j][5] = y.y; X[j][6] = y.z; X[j][7] = y.w;
+        });
+        __syncthreads();  // P consumed before the exchange reuses it
+        bs8::sfor<16>([&](auto J) { bs8::transpose8(X[decltype(J)::value]); });
+
+        small_layers<true>(wv, X);
+        exchange<true>(X, lds, wv, lane);
+        bs8::large_ifft_fft(X);
+        exchange<false>(X, lds, wv, lane);
+        if (t + gridDim.x < sets) prefetch_set(cs, t + gridDim.x, wv, lane, lds);
+        small_layers<false>(wv, X);
+
+        bs8::sfor<16>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            bs8::transpose8(X[j]);
+            const uint32_t so = sym_off(16u * wv + j, k, oo, es);
+            v4u x, y;
+            x.x = X[j][0]; x.y = X[j][1]; x.z = X[j][2]; x.w = X[j][3];
+            y.x = X[j][4]; y.y = X[j][5]; y.z = X[j][6]; y.w = X[j][7];
+            __builtin_amdgcn_raw_buffer_store_b128(x, a.ro, a.off[0], so, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(y, a.ro, a.off[1], so, 0);
+        });
+    }
 }
 
 // True when every offset the kernel forms stays below the buffer-resource limit
@@ -177,10 +229,22 @@ bool bs128_applicable(const CodewordSet& cs) {
     return span + sym < kOobBs;
 }
 
+static uint32_t device_cus() {
+    static const uint32_t n = [] {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        return (uint32_t)cus;
+    }();
+    return n;
+}
+
 hipError_t launch_encode_gf8_bs128(const CodewordSet& cs, hipStream_t st) {
     const uint64_t sets = ((uint64_t)cs.count * cs.S + kSetBytes - 1) / kSetBytes;
     if (sets == 0) return hipSuccess;
-    hipLaunchKernelGGL(encode_gf8_bs128_kernel, dim3((uint32_t)sets), dim3(512), 0, st, cs);
+    const uint32_t grid = (uint32_t)(sets < device_cus() ? sets : device_cus());
+    hipLaunchKernelGGL(encode_gf8_bs128_kernel, dim3(grid), dim3(512), 0, st, cs, (uint32_t)sets);
     return hipGetLastError();
 }
 

@@ -427,6 +427,26 @@ int rsm_extend_cols_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_si
     return launch_encode(ctx, cs, stream ? static_cast<hipStream_t>(stream) : ctx->stream);
 }
 
+int rsm_encode_batch_dev(rsm_ctx* ctx, const void* d_in, void* d_out, uint32_t k, uint32_t share_size,
+                         uint32_t count, uint64_t cw_stride, uint64_t share_stride, void* stream) {
+    if (!ctx || !d_in || !d_out || k == 0 || share_stride < share_size)
+        return fail(RSM_EINVAL, "rsm_encode_batch_dev: bad arguments");
+    if (int rc = validate_chunk_size(share_size)) return rc;
+    if (count == 0) return RSM_OK;
+    CodewordSet cs{};
+    cs.base = static_cast<uint8_t*>(const_cast<void*>(d_in));
+    cs.out_base = static_cast<uint8_t*>(d_out);
+    cs.square_stride = 0;
+    cs.cw_stride = cw_stride;
+    cs.elem_stride = share_stride;
+    cs.out_offset = 0;
+    cs.per_square = count;
+    cs.count = count;
+    cs.k = k;
+    cs.S = share_size;
+    return launch_encode(ctx, cs, stream ? static_cast<hipStream_t>(stream) : ctx->stream);
+}
+
 int rsm_decode_vectors_dev(rsm_ctx* ctx, void* d_eds, const uint8_t* d_presence, uint32_t k,
                            uint32_t share_size, int axis, const uint32_t* d_indices, uint32_t count,
                            void* stream) {

@@ -67,6 +67,45 @@ class RowShardedExtender:
         self._after_local()
 
 
+class TransposeShardedExtender:
+    """SURVEY.md §8(e) Option B: the all-gather of the top half replaced by an
+    all-to-all transpose, so each rank receives only its own column slice.
+
+    Rank g of G (n = k/G rows, w = 2k/G columns):
+      rows   [n][2k][S]  its ODS rows (Q0 part filled); the row pass writes Q1 in place
+      top    [k][w][S]   receives columns [g*w, (g+1)*w) of the whole top half [Q0|Q1]
+      bottom [k][w][S]   the column pass writes the same columns of [Q2|Q3]
+    Bytes received per rank: (G-1)/G * k*w*S  (config 5, G = 8: 28 MiB) instead of the
+    all-gather's (G-1)/G * k*2k*S (224 MiB).  The send buffer packs, for every
+    destination d, this rank's rows restricted to d's columns (one strided copy)."""
+
+    def __init__(self, k: int, share_size: int, encode_rows: Callable, encode_batch: Callable,
+                 after_local: Optional[Callable] = None, before_local: Optional[Callable] = None, *,
+                 group: Optional[dist.ProcessGroup] = None):
+        self.k, self.S = k, share_size
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.rows = shard(k, self.world, self.rank)
+        self.cols = shard(2 * k, self.world, self.rank)
+        self._enc_rows, self._enc_batch = encode_rows, encode_batch
+        self._after_local = after_local or (lambda: None)
+        self._before_local = before_local or (lambda: None)
+
+    def extend(self, rows: torch.Tensor, top: torch.Tensor, bottom: torch.Tensor) -> None:
+        k, S, G = self.k, self.S, self.world
+        n, w = k // G, 2 * k // G
+        assert rows.shape == (n, 2 * k, S) and top.shape == (k, w, S) and bottom.shape == (k, w, S)
+        assert rows.is_contiguous() and top.is_contiguous() and bottom.is_contiguous()
+        self._enc_rows(rows)                                     # Q0 rows -> Q1 rows (in place)
+        self._after_local()
+        send = rows.view(n, G, w, S).transpose(0, 1).contiguous()  # [G][n][w][S]: block d -> rank d
+        dist.all_to_all_single(top.view(-1), send.view(-1), group=self.group)
+        self._before_local()
+        self._enc_batch(top, bottom)                             # my w columns: [Q0|Q1] -> [Q2|Q3]
+        self._after_local()
+
+
 def hip_backend(device: int = 0):
     """(encode_rows, encode_cols, after_local, before_local) bound to the HIP C ABI."""
     from . import _check, device_context, library
@@ -89,3 +128,27 @@ def hip_backend(device: int = 0):
         torch.cuda.current_stream().synchronize()
 
     return rows, cols, after, before
+
+
+def hip_transpose_backend(device: int = 0):
+    """(encode_rows, encode_batch, after_local, before_local) for TransposeShardedExtender."""
+    from . import _check, device_context, library
+
+    L = library()
+    ctx = device_context(device)
+
+    def rows(r):
+        n, W, S = r.shape
+        _check(L.rsm_extend_rows_dev(ctx, r.data_ptr(), W // 2, S, 0, n, None))
+
+    def batch(top, bottom):
+        k, w, S = top.shape
+        _check(L.rsm_encode_batch_dev(ctx, top.data_ptr(), bottom.data_ptr(), k, S, w, S, w * S, None))
+
+    def after():
+        _check(L.rsm_sync(ctx))
+
+    def before():
+        torch.cuda.current_stream().synchronize()
+
+    return rows, batch, after, before

@@ -88,3 +88,68 @@ def test_shard_math():
     assert shard(1024, 8, 3) == (384, 512)
     with pytest.raises(ValueError):
         shard(10, 4, 0)
+
+
+def _oracle_row_block(rows):
+    import oracle
+    n, W, S = rows.shape
+    k = W // 2
+    a = rows.numpy()
+    for r in range(n):
+        par = oracle.encode([a[r, c].tobytes() for c in range(k)])
+        for i, p in enumerate(par):
+            a[r, k + i] = np.frombuffer(p, np.uint8)
+
+
+def _oracle_batch(top, bottom):
+    import oracle
+    k, w, S = top.shape
+    t, b = top.numpy(), bottom.numpy()
+    for c in range(w):
+        par = oracle.encode([t[r, c].tobytes() for r in range(k)])
+        for i, p in enumerate(par):
+            b[i, c] = np.frombuffer(p, np.uint8)
+
+
+def _worker_transpose(rank, world, port, k, S, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from rsmt2d_amd.distributed import TransposeShardedExtender
+        ods = np.random.default_rng(11).integers(0, 256, (k, k, S), dtype=np.uint8)
+        ext = TransposeShardedExtender(k, S, _oracle_row_block, _oracle_batch)
+        r0, r1 = ext.rows
+        c0, c1 = ext.cols
+        rows = torch.zeros((r1 - r0, 2 * k, S), dtype=torch.uint8)
+        rows[:, :k] = torch.from_numpy(ods[r0:r1])
+        top = torch.zeros((k, c1 - c0, S), dtype=torch.uint8)
+        bottom = torch.zeros_like(top)
+        ext.extend(rows, top, bottom)
+        import oracle
+        want = oracle.extend_square(ods)
+        ok = bool((top.numpy() == want[:k, c0:c1]).all() and (bottom.numpy() == want[k:, c0:c1]).all()
+                  and (rows.numpy() == want[r0:r1]).all())
+        flags = [None] * world
+        dist.all_gather_object(flags, ok)
+        if rank == 0:
+            q.put(all(flags))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover - surfaced through the queue
+        q.put(repr(e))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_transpose_sharded_matches_reference(world):
+    """Option B (all-to-all of column slices): every rank ends with its exact column
+    slice of the reference EDS (top and bottom) and its extended rows."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_transpose, args=(r, world, port, 8, 64, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+    assert res is True, res
