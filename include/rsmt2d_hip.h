@@ -98,6 +98,12 @@ int rsm_extend_cols_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_si
  * column slices of the all-to-all multi-GPU schedule.  Asynchronous. */
 int rsm_encode_batch_dev(rsm_ctx* ctx, const void* d_in, void* d_out, uint32_t k, uint32_t share_size,
                          uint32_t count, uint64_t cw_stride, uint64_t share_stride, void* stream);
+/* RowRoots()/ColRoots() with DefaultTree (datasquare.go:218-327, tree.go:32-59) of a
+ * complete device-resident [width][width][share_size] square, on the GPU:
+ * d_roots (device) receives 2*width*32 bytes, the row roots then the column roots.
+ * width <= 2048.  Asynchronous on `stream`. */
+int rsm_roots_dev(rsm_ctx* ctx, const void* d_eds, uint32_t width, uint32_t share_size, void* d_roots,
+                  void* stream);
 /* Device-resident batched reconstruct of whole rows (axis 0) or columns (axis 1)
  * of one [2k][2k][S] square: d_presence is one byte per cell, d_indices the
  * vectors to rebuild (each must have >= k cells present).  Asynchronous. */

@@ -494,7 +494,26 @@ int fast_repair(rsm_eds* e, DevSquare& dev, const uint8_t* row_roots, const uint
         e->stats.fallback_reason = kFallbackEncoding;
         return 1;
     }
-    // ... and match every committed row and column root.
+    // ... and match every committed row and column root: on the device for the
+    // DefaultTree (kernels_sha.hip), through the host Tree plugin otherwise.
+    if (tree.is_default() && root_len == 32 && roots_dev_supported(W)) {
+        DevBuf& rb = dev.ctx->dev_buf(31);
+        if ((r = rb.ensure((size_t)2 * W * 32)) != hipSuccess) return hip_fail(r, "hipMalloc (roots)");
+        if (int rc = device_roots(dev.ctx, dev.d_eds, W, e->S, static_cast<uint8_t*>(rb.ptr), dev.st)) return rc;
+        std::vector<uint8_t> got((size_t)2 * W * 32);
+        if ((r = hipMemcpyAsync(got.data(), rb.ptr, got.size(), hipMemcpyDeviceToHost, dev.st)) != hipSuccess)
+            return hip_fail(r, "D2H roots");
+        if (int rc = dev.sync()) return rc;
+        if (memcmp(got.data(), row_roots, (size_t)W * 32) != 0 ||
+            memcmp(got.data() + (size_t)W * 32, col_roots, (size_t)W * 32) != 0) {
+            e->stats.fallback_reason = kFallbackRoots;
+            return 1;
+        }
+        e->data.swap(repaired);
+        std::fill(e->present.begin(), e->present.end(), 1);
+        e->stats.fast_path = 1;
+        return RSM_OK;
+    }
     std::vector<int> axes;
     std::vector<uint32_t> idxs;
     std::vector<std::vector<const uint8_t*>> leaves;
@@ -640,6 +659,27 @@ int rsm_eds_roots(rsm_eds* e, int axis, rsm_tree_root_fn tree_fn, void* user, ui
     if (!e || !roots_out || !root_len || (axis != RSM_AXIS_ROW && axis != RSM_AXIS_COL))
         return fail(RSM_EINVAL, "roots: bad arguments");
     Tree tree{tree_fn, user};
+    if (tree.is_default() && e->ctx && root_cap >= 32 && roots_dev_supported(e->width) &&
+        std::all_of(e->present.begin(), e->present.end(), [](uint8_t p) { return p != 0; })) {
+        // complete square + DefaultTree: every leaf and node hash on the GPU
+        const uint32_t W = e->width;
+        std::lock_guard<std::mutex> lk(e->ctx->mu);
+        DevSquare dev{};
+        if (int rc = dev.init(e->ctx, W, e->S)) return rc;
+        hipError_t r = hipMemcpyAsync(dev.d_eds, e->data.data(), e->data.size(), hipMemcpyHostToDevice, dev.st);
+        if (r != hipSuccess) return hip_fail(r, "H2D square");
+        DevBuf& rb = e->ctx->dev_buf(31);
+        if ((r = rb.ensure((size_t)2 * W * 32)) != hipSuccess) return hip_fail(r, "hipMalloc (roots)");
+        if (int rc = device_roots(e->ctx, dev.d_eds, W, e->S, static_cast<uint8_t*>(rb.ptr), dev.st)) return rc;
+        std::vector<uint8_t> got((size_t)W * 32);
+        if ((r = hipMemcpyAsync(got.data(), static_cast<uint8_t*>(rb.ptr) + (size_t)(axis == RSM_AXIS_COL) * W * 32,
+                                got.size(), hipMemcpyDeviceToHost, dev.st)) != hipSuccess)
+            return hip_fail(r, "D2H roots");
+        if (int rc = dev.sync()) return rc;
+        for (uint32_t i = 0; i < W; ++i) memcpy(roots_out + (size_t)i * root_cap, got.data() + (size_t)i * 32, 32);
+        *root_len = 32;
+        return RSM_OK;
+    }
     std::vector<int> axes;
     std::vector<uint32_t> idxs;
     std::vector<std::vector<const uint8_t*>> leaves;

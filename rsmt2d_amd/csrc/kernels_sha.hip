@@ -1,0 +1,206 @@
+// kernels_sha.hip -- row and column Merkle roots of a device-resident EDS.
+//
+// computeRoots / getRowRoot / getColRoot (datasquare.go:218-327)
+// with rsmt2d's DefaultTree (tree.go:32-59): celestiaorg/merkletree over SHA-256,
+//   leaf = SHA256(0x00 || share),  node = SHA256(0x01 || left || right),
+// and for a leaf count that is not a power of two the NebulousLabs stack order:
+// perfect subtrees for the set bits of n (largest first), folded from the right
+//   root = node(sub_hi, node(sub_mid, ... sub_lo)).
+// Host restatement: merkle.cpp (rsm_default_tree_root); tests compare both with
+// Python hashlib.
+//
+// Two kernels:
+//   leaf_hash_kernel : one thread per cell, streams its share through SHA-256
+//                      (S/64 + 1 blocks); the digest of a cell serves both its row
+//                      tree and its column tree.
+//   tree_root_kernel : one workgroup per tree (2W trees), level by level in LDS.
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace rsm {
+
+namespace {
+
+__constant__ uint32_t kK[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+
+constexpr uint32_t kH0[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                             0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+
+__device__ __forceinline__ uint32_t rotr(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, n); }
+// Big-endian message word whose first byte is the last byte of `prev` and whose
+// other three are the first three bytes of `cur` (both big-endian words): the
+// 1-byte domain prefix shifts every share word by one byte.
+__device__ __forceinline__ uint32_t shift8(uint32_t prev, uint32_t cur) {
+    return __builtin_amdgcn_alignbit(prev, cur, 8);
+}
+
+__device__ __forceinline__ void sha_block(uint32_t (&h)[8], uint32_t (&w)[16]) {
+    uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+        if (i >= 16) {
+            const uint32_t x = w[(i + 1) & 15], y = w[(i + 14) & 15];
+            const uint32_t s0 = rotr(x, 7) ^ rotr(x, 18) ^ (x >> 3);
+            const uint32_t s1 = rotr(y, 17) ^ rotr(y, 19) ^ (y >> 10);
+            w[i & 15] += s0 + w[(i + 9) & 15] + s1;
+        }
+        const uint32_t S1 = rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25);
+        const uint32_t ch = (e & f) ^ (~e & g);
+        const uint32_t t1 = hh + S1 + ch + kK[i] + w[i & 15];
+        const uint32_t S0 = rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22);
+        const uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+        hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
+    }
+    h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+}
+
+// SHA256(0x01 || L || R) for digests held as 8 big-endian words each.
+__device__ __forceinline__ void node_hash(const uint32_t (&L)[8], const uint32_t (&R)[8], uint32_t (&out)[8]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) out[i] = kH0[i];
+    uint32_t w[16];
+    w[0] = shift8(0x01u, L[0]);
+#pragma unroll
+    for (int i = 1; i < 8; ++i) w[i] = shift8(L[i - 1], L[i]);
+    w[8] = shift8(L[7], R[0]);
+#pragma unroll
+    for (int i = 1; i < 8; ++i) w[8 + i] = shift8(R[i - 1], R[i]);
+    sha_block(out, w);
+    w[0] = (R[7] << 24) | 0x00800000u;
+#pragma unroll
+    for (int i = 1; i < 15; ++i) w[i] = 0;
+    w[15] = 65u * 8u;
+    sha_block(out, w);
+}
+
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+
+// leaf[cell][8] = SHA256(0x00 || share(cell)), cell = row * W + col.
+__global__ __launch_bounds__(256) void leaf_hash_kernel(const uint8_t* __restrict__ eds, uint32_t cells,
+                                                        uint32_t S, uint32_t* __restrict__ leaf) {
+    const uint32_t cell = blockIdx.x * 256u + threadIdx.x;
+    if (cell >= cells) return;
+    const v4u* p = reinterpret_cast<const v4u*>(eds + (uint64_t)cell * S);
+    uint32_t h[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) h[i] = kH0[i];
+    uint32_t prev = 0;  // the 0x00 leaf prefix
+    for (uint32_t blk = 0; blk < S / 64u; ++blk) {
+        uint32_t w[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const v4u v = __builtin_nontemporal_load(p + blk * 4u + q);
+            const uint32_t b0 = __builtin_bswap32(v.x), b1 = __builtin_bswap32(v.y);
+            const uint32_t b2 = __builtin_bswap32(v.z), b3 = __builtin_bswap32(v.w);
+            w[4 * q + 0] = shift8(prev, b0);
+            w[4 * q + 1] = shift8(b0, b1);
+            w[4 * q + 2] = shift8(b1, b2);
+            w[4 * q + 3] = shift8(b2, b3);
+            prev = b3;
+        }
+        sha_block(h, w);
+    }
+    uint32_t w[16];
+    w[0] = (prev << 24) | 0x00800000u;  // last share byte, then the 0x80 pad byte
+#pragma unroll
+    for (int i = 1; i < 15; ++i) w[i] = 0;
+    w[15] = (S + 1u) * 8u;
+    sha_block(h, w);
+    v4u* o = reinterpret_cast<v4u*>(leaf + (uint64_t)cell * 8u);
+    o[0] = v4u{h[0], h[1], h[2], h[3]};
+    o[1] = v4u{h[4], h[5], h[6], h[7]};
+}
+
+constexpr uint32_t kMaxLevel1 = 1024;  // W <= 2048
+
+// One workgroup per tree: blockIdx.x < W -> row tree blockIdx.x, else column tree.
+// roots: [2][W][32] bytes (big-endian digest bytes, as Tree.Root() returns them).
+__global__ __launch_bounds__(256) void tree_root_kernel(const uint32_t* __restrict__ leaf, uint32_t W,
+                                                        uint8_t* __restrict__ roots) {
+    __shared__ uint32_t lvl[2][kMaxLevel1][8];
+    __shared__ uint32_t sub[16][8];
+    const uint32_t axis = blockIdx.x >= W ? 1u : 0u;
+    const uint32_t idx = blockIdx.x - axis * W;
+    const uint32_t n = W;
+    auto leaf_at = [&](uint32_t pos, uint32_t (&d)[8]) {
+        const uint64_t cell = axis == 0 ? (uint64_t)idx * W + pos : (uint64_t)pos * W + idx;
+        const v4u* s = reinterpret_cast<const v4u*>(leaf + cell * 8u);
+        const v4u a = s[0], b = s[1];
+        d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w; d[4] = b.x; d[5] = b.y; d[6] = b.z; d[7] = b.w;
+    };
+    if ((n & 1u) && threadIdx.x == 0) {  // height-0 subtree: the last leaf
+        uint32_t d[8];
+        leaf_at(n - 1, d);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) sub[0][i] = d[i];
+    }
+    uint32_t cur = 0;
+    for (uint32_t hgt = 1; (n >> hgt) > 0; ++hgt) {
+        const uint32_t cnt = n >> hgt;
+        for (uint32_t j = threadIdx.x; j < cnt; j += 256u) {
+            uint32_t L[8], R[8], o[8];
+            if (hgt == 1) {
+                leaf_at(2 * j, L);
+                leaf_at(2 * j + 1, R);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    L[i] = lvl[cur ^ 1u][2 * j][i];
+                    R[i] = lvl[cur ^ 1u][2 * j + 1][i];
+                }
+            }
+            node_hash(L, R, o);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) lvl[cur][j][i] = o[i];
+            if (((n >> hgt) & 1u) && j == cnt - 1) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) sub[hgt][i] = o[i];
+            }
+        }
+        __syncthreads();
+        cur ^= 1u;
+    }
+    if (threadIdx.x == 0) {
+        uint32_t acc[8];
+        int lo = __builtin_ctz(n);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i] = sub[lo][i];
+        for (int hgt = lo + 1; hgt < 16; ++hgt) {
+            if (!((n >> hgt) & 1u)) continue;
+            uint32_t L[8], o[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) L[i] = sub[hgt][i];
+            node_hash(L, acc, o);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) acc[i] = o[i];
+        }
+        uint32_t* r = reinterpret_cast<uint32_t*>(roots + ((uint64_t)axis * W + idx) * 32u);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) r[i] = __builtin_bswap32(acc[i]);
+    }
+}
+
+}  // namespace
+
+bool roots_dev_supported(uint32_t W) { return W >= 2 && W <= 2 * kMaxLevel1 && W < (1u << 16); }
+
+// d_leaf: scratch of W*W*32 bytes.
+hipError_t launch_roots(const uint8_t* d_eds, uint32_t W, uint32_t S, uint32_t* d_leaf, uint8_t* d_roots,
+                        hipStream_t st) {
+    const uint32_t cells = W * W;
+    hipLaunchKernelGGL(leaf_hash_kernel, dim3((cells + 255) / 256), dim3(256), 0, st, d_eds, cells, S, d_leaf);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(tree_root_kernel, dim3(2 * W), dim3(256), 0, st, d_leaf, W, d_roots);
+    return hipGetLastError();
+}
+
+}  // namespace rsm
