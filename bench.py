@@ -46,6 +46,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-c5", action="store_true", help="skip the config-5 (sharded 512x512 square) line")
     p.add_argument("--no-c3", action="store_true", help="skip the config-3 (Repair) timings")
+    p.add_argument("--no-roots", action="store_true", help="skip the extension + Merkle roots timing")
     p.add_argument("--dist", action="store_true",
                    help="initialise torch.distributed even at N=1 (rehearses the sharded c5 path on one GPU)")
     p.add_argument("--cpu-seconds", type=float, default=3.0)
@@ -236,6 +237,41 @@ def bench_c3(local, L, R, repeats=5):
                     "host SHA-256 roots of all 512 vectors, D2H); median of samples"}
 
 
+def bench_roots(local, L, R, buf, k, S, B, steps):
+    """BenchmarkExtensionWithRoots (extendeddatasquare_test.go:309-334): the 2D
+    extension plus RowRoots + ColRoots (DefaultTree) of every square, all on the
+    device (rsm_extend_squares_dev + rsm_roots_dev per square)."""
+    ctx = R.device_context(local)
+    W = 2 * k
+    sq = W * W * S
+    roots = R.DeviceBuffer(2 * W * 32 * B, local)
+
+    def run():
+        R._check(L.rsm_extend_squares_dev(ctx, buf.ptr, k, S, B, None))
+        for i in range(B):
+            R._check(L.rsm_roots_dev(ctx, buf.ptr + i * sq, W, S, roots.ptr + i * 2 * W * 32, None))
+
+    run()
+    R._check(L.rsm_sync(ctx))
+    n = max(3, min(steps, 10))
+    t0 = time.perf_counter()
+    for _ in range(n):
+        run()
+    R._check(L.rsm_sync(ctx))
+    dt = (time.perf_counter() - t0) / n
+    t0 = time.perf_counter()
+    for _ in range(n):
+        for i in range(B):
+            R._check(L.rsm_roots_dev(ctx, buf.ptr + i * sq, W, S, roots.ptr + i * 2 * W * 32, None))
+    R._check(L.rsm_sync(ctx))
+    dr = (time.perf_counter() - t0) / n
+    roots.free()
+    return {"workload": f"extension + DefaultTree row/col roots, k={k}, S={S}, {B} squares per step",
+            "ms_per_square": round(dt / B * 1e3, 4), "ods_GiB_s": round(B * k * k * S / dt / 2**30, 3),
+            "roots_only_ms_per_square": round(dr / B * 1e3, 4),
+            "note": "leaf SHA-256 per cell (shared by its row and column tree) + per-tree node hashes on the GPU"}
+
+
 def main():
     a = parse()
     import numpy as np
@@ -366,6 +402,8 @@ def main():
         out["host_path"] = {"value": round(n * ods_bytes / (time.perf_counter() - t1) / 2**30, 3), "unit": "GiB/s",
                             "note": "rsm_extend_square: pageable host ODS -> H2D -> extend -> D2H EDS, one square"}
         out["cpu_baseline"] = None if a.no_cpu_baseline else cpu_baseline(k, S, a.cpu_seconds)
+    if rank == 0 and world == 1 and not a.no_roots:
+        out["with_roots"] = bench_roots(local, L, R, buf, k, S, B, a.steps)
     buf.free()
     if rank == 0 and world == 1 and not a.no_c3:
         out["c3"] = bench_c3(local, L, R)

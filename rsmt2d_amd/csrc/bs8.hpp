@@ -104,16 +104,37 @@ RSM_HD void muladd(uint32_t (&x)[8], const uint32_t (&y)[8]) {
     sfor<8>([&](auto I) { acc_terms<R.r[decltype(I)::value]>(x[decltype(I)::value], y); });
 }
 
+#if defined(__HIPCC__)
+// Device butterflies: one generated asm block each (bs8_asm.inc, from
+// gen/gen_bs8_asm.cpp; the same networks as muladd below).  One block per
+// butterfly instead of one statement per instruction: the compiler pads every
+// asm boundary with an s_nop (a 4-cycle issue slot).
+#define RSM_BS8_DEV __device__ __forceinline__
+template <unsigned L>
+RSM_BS8_DEV void ifft2_asm(uint32_t (&x)[8], uint32_t (&y)[8]);
+template <unsigned L>
+RSM_BS8_DEV void fft2_asm(uint32_t (&x)[8], uint32_t (&y)[8]);
+#include "bs8_asm.inc"
+#endif
+
 // IFFT_DIT2: y ^= x; x ^= y*L.   FFT_DIT2: x ^= y*L; y ^= x.   L == 255: XOR only.
 template <unsigned L>
 RSM_HD void ifft2(uint32_t (&x)[8], uint32_t (&y)[8]) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    ifft2_asm<L>(x, y);
+#else
     sfor<8>([&](auto I) { xor_into(y[decltype(I)::value], x[decltype(I)::value]); });
     if constexpr (L != 255u) muladd<L>(x, y);
+#endif
 }
 template <unsigned L>
 RSM_HD void fft2(uint32_t (&x)[8], uint32_t (&y)[8]) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    fft2_asm<L>(x, y);
+#else
     if constexpr (L != 255u) muladd<L>(x, y);
     sfor<8>([&](auto I) { xor_into(y[decltype(I)::value], x[decltype(I)::value]); });
+#endif
 }
 
 // 8x8 bit-matrix transpose applied to each of the 4 byte lanes of 8 words:
