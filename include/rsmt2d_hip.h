@@ -80,7 +80,7 @@ int rsm_extend_square(rsm_ctx* ctx, const uint8_t* ods, uint32_t k, uint32_t sha
 int rsm_extend_squares_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size, uint32_t count,
                            void* stream);
 /* One phase of the above: phase 1 = row pass (Q0 -> Q1), phase 2 = column pass
- * ([Q0|Q1] -> [Q2|Q3]); for per-kernel timing/profiling.  Asynchronous. */
+ * ([Q0|Q1] -> [Q2|Q3]), 3 = both; for per-kernel timing/profiling.  Asynchronous. */
 int rsm_extend_squares_phase_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size,
                                  uint32_t count, int phase, void* stream);
 /* Rows [row0, row0+nrows) / columns [col0, col0+ncols) of one in-place

@@ -115,6 +115,8 @@ RSM_BS8_DEV void ifft2_asm(uint32_t (&x)[8], uint32_t (&y)[8]);
 template <unsigned L>
 RSM_BS8_DEV void fft2_asm(uint32_t (&x)[8], uint32_t (&y)[8]);
 #include "bs8_asm.inc"
+// small-layout layers of all eight waves, one asm statement each (branch on A inside)
+#include "bs8_small.inc"
 #endif
 
 // IFFT_DIT2: y ^= x; x ^= y*L.   FFT_DIT2: x ^= y*L; y ^= x.   L == 255: XOR only.
@@ -159,6 +161,46 @@ RSM_HD void transpose8(uint32_t (&w)[8]) {
     swapbits(w[4], w[5], 1, 0x55555555u);
     swapbits(w[6], w[7], 1, 0x55555555u);
 }
+
+#if defined(__HIPCC__)
+// Device 8x8 transpose as one asm block: per swap t1 = b << s, t2 = a >> s,
+// a = bfi(m << s, t1, a), b = bfi(m, t2, b) -- 4 VALU (the xor form above is 5 on
+// gfx9, which has no v_lshl_xor), two swaps interleaved so consecutive
+// instructions are independent.  Same permutation as transpose8.
+#define RSM_T8_PAIR(a, b, s, m, mh)                    \
+    "v_lshlrev_b32 %8, " #s ", %" #b "\n\t"             \
+    "v_lshrrev_b32 %9, " #s ", %" #a "\n\t"
+#define RSM_T8_PAIR2(a, b, s, m, mh)                   \
+    "v_lshlrev_b32 %10, " #s ", %" #b "\n\t"            \
+    "v_lshrrev_b32 %11, " #s ", %" #a "\n\t"
+#define RSM_T8_FIN(a, b, m, mh)                        \
+    "v_bfi_b32 %" #a ", %" #mh ", %8, %" #a "\n\t"        \
+    "v_bfi_b32 %" #b ", %" #m ", %9, %" #b "\n\t"
+#define RSM_T8_FIN2(a, b, m, mh)                       \
+    "v_bfi_b32 %" #a ", %" #mh ", %10, %" #a "\n\t"       \
+    "v_bfi_b32 %" #b ", %" #m ", %11, %" #b "\n\t"
+#define RSM_T8_2SWAPS(a0, b0, a1, b1, s, m, mh) \
+    RSM_T8_PAIR(a0, b0, s, m, mh) RSM_T8_PAIR2(a1, b1, s, m, mh) RSM_T8_FIN(a0, b0, m, mh) RSM_T8_FIN2(a1, b1, m, mh)
+__device__ __forceinline__ void transpose8_dev(uint32_t (&w)[8]) {
+    uint32_t t0, t1, t2, t3;
+    asm volatile(
+        RSM_T8_2SWAPS(0, 4, 1, 5, 4, 12, 13)
+        RSM_T8_2SWAPS(2, 6, 3, 7, 4, 12, 13)
+        RSM_T8_2SWAPS(0, 2, 1, 3, 2, 14, 15)
+        RSM_T8_2SWAPS(4, 6, 5, 7, 2, 14, 15)
+        RSM_T8_2SWAPS(0, 1, 2, 3, 1, 16, 17)
+        RSM_T8_2SWAPS(4, 5, 6, 7, 1, 16, 17)
+        : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]), "+v"(w[4]), "+v"(w[5]), "+v"(w[6]), "+v"(w[7]),
+          "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3)
+        : "s"(0x0F0F0F0Fu), "s"(0xF0F0F0F0u), "s"(0x33333333u), "s"(0xCCCCCCCCu), "s"(0x55555555u),
+          "s"(0xAAAAAAAAu));
+}
+#undef RSM_T8_PAIR
+#undef RSM_T8_PAIR2
+#undef RSM_T8_FIN
+#undef RSM_T8_FIN2
+#undef RSM_T8_2SWAPS
+#endif
 
 constexpr int kM = 128;        // transform size handled here (65 <= k <= 128)
 constexpr int kOffEnc = kM - 1;  // encoder IFFT skew offset

@@ -34,6 +34,7 @@
 // column pass, slices); callers with an index list use the byte-table kernel.
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <cstdlib>
 #include "bs8.hpp"
 #include "rsm_kernels.hpp"
 
@@ -112,7 +113,7 @@ __device__ __forceinline__ void dma16(uint32_t lds_byte, uint32_t voff, v4u srd,
     asm volatile(
         "s_mov_b32 %0, m0\n\t"
         "s_mov_b32 m0, %1\n\t"
-        "s_nop 0\n\t"
+        "s_nop 4\n\t"
         "buffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
         "s_mov_b32 m0, %0"
         : "=&s"(keep)
@@ -203,18 +204,18 @@ __device__ __forceinline__ void exchange(uint32_t (&X)[16][8], uint32_t base0) {
             else ds_w16<Lx::large_off(j)>(j < 8 ? base0 : base1, v);
         });
         lds_barrier();
-        v4u g[2][8];
-        if constexpr (TO_LARGE) {
-            ds_r16x8<Lx::large_off(0), 8192>(base0, g[0]);
-            ds_r16x8<Lx::large_off(8), 8192>(base1, g[1]);
-        } else {
-            ds_r16x8<Lx::small_off(0), 1024>(bsmall, g[0]);
-            ds_r16x8<Lx::small_off(8), 1024>(bsmall, g[1]);
-        }
-        bs8::sfor<16>([&](auto J) {
-            constexpr int j = decltype(J)::value;
-            const v4u v = g[j >> 3][j & 7];
-            X[j][4 * r + 0] = v.x; X[j][4 * r + 1] = v.y; X[j][4 * r + 2] = v.z; X[j][4 * r + 3] = v.w;
+        // read back in two groups of 8 (32 VGPRs of temporaries, not 64: the next
+        // set's direct loads may be in flight in P)
+        bs8::sfor<2>([&](auto Hh) {
+            constexpr int hh = decltype(Hh)::value;
+            v4u g[8];
+            if constexpr (TO_LARGE) ds_r16x8<Lx::large_off(8 * hh), 8192>(hh ? base1 : base0, g);
+            else ds_r16x8<Lx::small_off(8 * hh), 1024>(bsmall, g);
+            bs8::sfor<8>([&](auto J) {
+                constexpr int j = 8 * hh + decltype(J)::value;
+                const v4u v = g[j & 7];
+                X[j][4 * r + 0] = v.x; X[j][4 * r + 1] = v.y; X[j][4 * r + 2] = v.z; X[j][4 * r + 3] = v.w;
+            });
         });
         lds_barrier();
     });
@@ -228,13 +229,17 @@ __device__ __forceinline__ void exchange(uint32_t (&X)[16][8], uint32_t base0) {
 //               | wait vmcnt(32): DMA + direct loads of t+G landed
 //               | first half of t+G: read DMA, transpose, small IFFT, exchange,
 //                 large layers, exchange back, DMA of t+2G.
-template <int A>
+// MODE bits (diagnostics; 0 = production): 1 = direct loads one iteration earlier,
+// 2 = no arithmetic (memory + LDS only), 4 = no global memory (compute + LDS only)
+template <int A, int MODE>
 __device__ __forceinline__ void bs_wave(const CodewordSet& cs, uint32_t sets, v4u* lds) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t lds_base = (uint32_t)(uintptr_t)lds;
     const uint32_t xbase = lds_base + lane * 16u;
     const uint32_t k = cs.k, es = (uint32_t)cs.elem_stride, oo = (uint32_t)cs.out_offset;
     const uint32_t G = gridDim.x;
+    constexpr bool EARLY = MODE & 1, ARITH = !(MODE & 2);
+    const bool MEM = !(MODE & 4) || cs.S == 1;  // runtime-false in mode 4 (keeps the code alive)
     uint32_t X[16][8];
     uint32_t P[16 - kPre][8];
 
@@ -259,39 +264,47 @@ __device__ __forceinline__ void bs_wave(const CodewordSet& cs, uint32_t sets, v4
             bs8::sfor<8>([&](auto I) { X[kPre + j][decltype(I)::value] = P[j][decltype(I)::value]; });
         });
         lds_barrier();  // DMA buffer consumed by every wave
-        bs8::sfor<16>([&](auto J) { bs8::transpose8(X[decltype(J)::value]); });
-        bs8::small_ifft<A>(X);
+        // EARLY: the next set's direct loads go out now, a whole iteration ahead
+        if (EARLY && MEM && t + G < sets) issue_direct<A>(cs, set_addr(cs, t + G, lane), P);
+        if constexpr (ARITH) {
+            bs8::sfor<16>([&](auto J) { bs8::transpose8(X[decltype(J)::value]); });
+            bs8::small_ifft<A>(X);
+        }
         exchange<true, A>(X, xbase);
-        bs8::large_ifft_fft(X);
+        if constexpr (ARITH) bs8::large_ifft_fft(X);
         exchange<false, A>(X, xbase);
-        if (t + G < sets) issue_dma<A>(cs, set_addr(cs, t + G, lane), lds_base);
+        if (MEM && t + G < sets) issue_dma<A>(cs, set_addr(cs, t + G, lane), lds_base);
     };
 
     uint32_t t = blockIdx.x;
     {
         const SetAddr a = set_addr(cs, t, lane);
-        issue_direct<A>(cs, a, P);
-        issue_dma<A>(cs, a, lds_base);
+        if (MEM) {
+            issue_direct<A>(cs, a, P);
+            issue_dma<A>(cs, a, lds_base);
+        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     first_half(t);
     for (;;) {
         const uint32_t tn = t + G;
         const bool more = tn < sets;
-        if (more) issue_direct<A>(cs, set_addr(cs, tn, lane), P);
-        bs8::small_fft<A>(X);
+        if (!EARLY && MEM && more) issue_direct<A>(cs, set_addr(cs, tn, lane), P);
+        if constexpr (ARITH) bs8::small_fft<A>(X);
         {
             const SetAddr a = set_addr(cs, t, lane);
             const __amdgpu_buffer_rsrc_t ro = as_rsrc(a.ro);
             bs8::sfor<16>([&](auto J) {
                 constexpr int j = decltype(J)::value;
-                bs8::transpose8(X[j]);
+                if constexpr (ARITH) bs8::transpose8(X[j]);
                 const uint32_t so = sym_off(16u * A + j, k, oo, es);
                 v4u x, y;
                 x.x = X[j][0]; x.y = X[j][1]; x.z = X[j][2]; x.w = X[j][3];
                 y.x = X[j][4]; y.y = X[j][5]; y.z = X[j][6]; y.w = X[j][7];
-                __builtin_amdgcn_raw_buffer_store_b128(x, ro, a.off[0], so, 0);
-                __builtin_amdgcn_raw_buffer_store_b128(y, ro, a.off[1], so, 0);
+                if (MEM) {
+                    __builtin_amdgcn_raw_buffer_store_b128(x, ro, a.off[0], so, 0);
+                    __builtin_amdgcn_raw_buffer_store_b128(y, ro, a.off[1], so, 0);
+                }
             });
         }
         if (!more) break;
@@ -304,19 +317,294 @@ __device__ __forceinline__ void bs_wave(const CodewordSet& cs, uint32_t sets, v4
 
 }  // namespace
 
+template <int MODE>
 __global__ __launch_bounds__(512, 1) void encode_gf8_bs128_kernel(CodewordSet cs, uint32_t sets) {
     __shared__ v4u lds[128 * 64];
     if (blockIdx.x >= sets) return;
     switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
-        case 0: bs_wave<0>(cs, sets, lds); break;
-        case 1: bs_wave<1>(cs, sets, lds); break;
-        case 2: bs_wave<2>(cs, sets, lds); break;
-        case 3: bs_wave<3>(cs, sets, lds); break;
-        case 4: bs_wave<4>(cs, sets, lds); break;
-        case 5: bs_wave<5>(cs, sets, lds); break;
-        case 6: bs_wave<6>(cs, sets, lds); break;
-        default: bs_wave<7>(cs, sets, lds); break;
+        case 0: bs_wave<0, MODE>(cs, sets, lds); break;
+        case 1: bs_wave<1, MODE>(cs, sets, lds); break;
+        case 2: bs_wave<2, MODE>(cs, sets, lds); break;
+        case 3: bs_wave<3, MODE>(cs, sets, lds); break;
+        case 4: bs_wave<4, MODE>(cs, sets, lds); break;
+        case 5: bs_wave<5, MODE>(cs, sets, lds); break;
+        case 6: bs_wave<6, MODE>(cs, sets, lds); break;
+        default: bs_wave<7, MODE>(cs, sets, lds); break;
     }
+}
+
+// ---------------------------------------------------------------------------
+// Streaming form (bs128s): every load of set t+G is issued at the START of set
+// t, so HBM traffic runs under the whole transform instead of its tail.
+//   LDS  D [wave 8][j 8][half 2][lane 64] x 16 B = 128 KiB: symbols j < 8 of each
+//        wave by LDS-DMA; each wave reads and re-fills only its own 16 KiB, so
+//        the DMA needs no barrier, only the wave's own vmcnt.
+//   LDS  E [symbol 128][lane 64] x 4 B = 32 KiB: the layout exchange, one bit
+//        plane per round (16 ds_write_b32, barrier, 16 ds_read_b32 in place,
+//        barrier), 8 rounds each way.
+//   VGPR P: symbols j >= 8 of the next set (64 registers).
+// Iteration t: read D -> X[0..7], X[8..15] = P; issue DMA + direct loads of
+// t+G; transform; store t; wait vmcnt(32) (the 32 stores may stay in flight).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kDmaBytes = 128u * 1024u;
+constexpr uint32_t kXchBytes = 32u * 1024u;
+
+#define RSM_XW(j, o) "ds_write_b32 %16, %" #j " offset:" #o "\n\t"
+#define RSM_XR(j, o) "ds_read_b32 %" #j ", %17 offset:" #o "\n\t"
+#define RSM_XOPS(p)                                                                                             \
+    : "+v"(X[0][p]), "+v"(X[1][p]), "+v"(X[2][p]), "+v"(X[3][p]), "+v"(X[4][p]), "+v"(X[5][p]), "+v"(X[6][p]), \
+      "+v"(X[7][p]), "+v"(X[8][p]), "+v"(X[9][p]), "+v"(X[10][p]), "+v"(X[11][p]), "+v"(X[12][p]),           \
+      "+v"(X[13][p]), "+v"(X[14][p]), "+v"(X[15][p])                                                          \
+    : "v"(wb), "v"(rb)                                                                                        \
+    : "memory"
+// small layout (e = 16A + j): byte offset 256 j from e_small;  large (e = 8h + A): 2048 h from e_large
+template <int p>
+__device__ __forceinline__ void xch_to_large(uint32_t (&X)[16][8], uint32_t wb, uint32_t rb) {
+    asm volatile(RSM_XW(0, 0) RSM_XW(1, 256) RSM_XW(2, 512) RSM_XW(3, 768) RSM_XW(4, 1024) RSM_XW(5, 1280)
+                     RSM_XW(6, 1536) RSM_XW(7, 1792) RSM_XW(8, 2048) RSM_XW(9, 2304) RSM_XW(10, 2560)
+                         RSM_XW(11, 2816) RSM_XW(12, 3072) RSM_XW(13, 3328) RSM_XW(14, 3584) RSM_XW(15, 3840)
+                 "s_waitcnt lgkmcnt(0)\n\ts_barrier\n\t"
+                 RSM_XR(0, 0) RSM_XR(1, 2048) RSM_XR(2, 4096) RSM_XR(3, 6144) RSM_XR(4, 8192) RSM_XR(5, 10240)
+                     RSM_XR(6, 12288) RSM_XR(7, 14336) RSM_XR(8, 16384) RSM_XR(9, 18432) RSM_XR(10, 20480)
+                         RSM_XR(11, 22528) RSM_XR(12, 24576) RSM_XR(13, 26624) RSM_XR(14, 28672) RSM_XR(15, 30720)
+                 "s_waitcnt lgkmcnt(0)\n\ts_barrier" RSM_XOPS(p));
+}
+template <int p>
+__device__ __forceinline__ void xch_to_small(uint32_t (&X)[16][8], uint32_t wb, uint32_t rb) {
+    asm volatile(RSM_XW(0, 0) RSM_XW(1, 2048) RSM_XW(2, 4096) RSM_XW(3, 6144) RSM_XW(4, 8192) RSM_XW(5, 10240)
+                     RSM_XW(6, 12288) RSM_XW(7, 14336) RSM_XW(8, 16384) RSM_XW(9, 18432) RSM_XW(10, 20480)
+                         RSM_XW(11, 22528) RSM_XW(12, 24576) RSM_XW(13, 26624) RSM_XW(14, 28672) RSM_XW(15, 30720)
+                 "s_waitcnt lgkmcnt(0)\n\ts_barrier\n\t"
+                 RSM_XR(0, 0) RSM_XR(1, 256) RSM_XR(2, 512) RSM_XR(3, 768) RSM_XR(4, 1024) RSM_XR(5, 1280)
+                     RSM_XR(6, 1536) RSM_XR(7, 1792) RSM_XR(8, 2048) RSM_XR(9, 2304) RSM_XR(10, 2560)
+                         RSM_XR(11, 2816) RSM_XR(12, 3072) RSM_XR(13, 3328) RSM_XR(14, 3584) RSM_XR(15, 3840)
+                 "s_waitcnt lgkmcnt(0)\n\ts_barrier" RSM_XOPS(p));
+}
+#undef RSM_XW
+#undef RSM_XR
+#undef RSM_XOPS
+
+// MODE bits (diagnostics; 0 = production): 2 = no arithmetic, 4 = no global memory
+template <int A, int MODE>
+__device__ __forceinline__ void bs_stream_wave(const CodewordSet& cs, uint32_t sets, uint32_t lds_base) {
+    constexpr bool ARITH = !(MODE & 2);
+    const bool MEM = !(MODE & 4) || cs.S == 1;  // runtime-false in mode 4 (keeps the code alive)
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t G = gridDim.x;
+    const uint32_t k = cs.k, es = (uint32_t)cs.elem_stride, oo = (uint32_t)cs.out_offset;
+    const uint32_t dread = lds_base + A * 16384u + lane * 16u;
+    const uint32_t ebase = lds_base + kDmaBytes + lane * 4u;
+    const uint32_t e_small = ebase + 4096u * A, e_large = ebase + 256u * A;
+    uint32_t X[16][8];
+    uint32_t P[16 - kPre][8];
+
+    uint32_t t = blockIdx.x;
+    SetAddr a = set_addr(cs, t, lane);
+    if (MEM) {
+        issue_dma<A>(cs, a, lds_base);
+        issue_direct<A>(cs, a, P);
+    }
+    // vmcnt(0) through the builtin (gfx9 encoding: vmcnt 0, expcnt 7, lgkmcnt 15):
+    // the compiler sees it, so its own wait for P at the loop head stays vmcnt(32)
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    for (;;) {
+        {
+            v4u g[8];
+            bs8::sfor<2>([&](auto Hh) {
+                constexpr int hh = decltype(Hh)::value;
+                ds_r16x8<8192 * hh, 1024>(dread, g);
+                bs8::sfor<4>([&](auto J) {
+                    constexpr int j = 4 * hh + decltype(J)::value;
+                    const v4u x = g[2 * (j & 3)], y = g[2 * (j & 3) + 1];
+                    X[j][0] = x.x; X[j][1] = x.y; X[j][2] = x.z; X[j][3] = x.w;
+                    X[j][4] = y.x; X[j][5] = y.y; X[j][6] = y.z; X[j][7] = y.w;
+                });
+            });
+        }
+        bs8::sfor<16 - kPre>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            bs8::sfor<8>([&](auto I) { X[kPre + j][decltype(I)::value] = P[j][decltype(I)::value]; });
+        });
+        const uint32_t tn = t + G;
+        const bool more = tn < sets;
+        SetAddr an = a;
+        if (more) {
+            an = set_addr(cs, tn, lane);
+            if (MEM) {
+                issue_dma<A>(cs, an, lds_base);
+                issue_direct<A>(cs, an, P);
+            }
+        }
+        if constexpr (ARITH) {
+            bs8::sfor<16>([&](auto J) { bs8::transpose8_dev(X[decltype(J)::value]); });
+            bs8::small_ifft<A>(X);
+        }
+        bs8::sfor<8>([&](auto Pp) { xch_to_large<decltype(Pp)::value>(X, e_small, e_large); });
+        if constexpr (ARITH) bs8::large_ifft_fft(X);
+        bs8::sfor<8>([&](auto Pp) { xch_to_small<decltype(Pp)::value>(X, e_large, e_small); });
+        if constexpr (ARITH) bs8::small_fft<A>(X);
+        {
+            const __amdgpu_buffer_rsrc_t ro = as_rsrc(a.ro);
+            bs8::sfor<16>([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                if constexpr (ARITH) bs8::transpose8_dev(X[j]);
+                const uint32_t so = sym_off(16u * A + j, k, oo, es);
+                v4u x, y;
+                x.x = X[j][0]; x.y = X[j][1]; x.z = X[j][2]; x.w = X[j][3];
+                y.x = X[j][4]; y.y = X[j][5]; y.z = X[j][6]; y.w = X[j][7];
+                if (MEM) {
+                    __builtin_amdgcn_raw_buffer_store_b128(x, ro, a.off[0], so, 0);
+                    __builtin_amdgcn_raw_buffer_store_b128(y, ro, a.off[1], so, 0);
+                }
+            });
+        }
+        if (!more) break;
+        t = tn;
+        a = an;
+        // issue order: DMA(t) [16], direct(t) [16], stores(t - G) [32]
+        asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+    }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(512, 1) void encode_gf8_bs128s_kernel(CodewordSet cs, uint32_t sets) {
+    __shared__ uint32_t lds[(kDmaBytes + kXchBytes) / 4];
+    if (blockIdx.x >= sets) return;
+    const uint32_t base = (uint32_t)(uintptr_t)lds;
+    if constexpr ((MODE & 8) != 0) {  // diagnostic: every wave runs wave 0's program (wrong output)
+        bs_stream_wave<0, MODE>(cs, sets, base);
+        return;
+    }
+    switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
+        case 0: bs_stream_wave<0, MODE>(cs, sets, base); break;
+        case 1: bs_stream_wave<1, MODE>(cs, sets, base); break;
+        case 2: bs_stream_wave<2, MODE>(cs, sets, base); break;
+        case 3: bs_stream_wave<3, MODE>(cs, sets, base); break;
+        case 4: bs_stream_wave<4, MODE>(cs, sets, base); break;
+        case 5: bs_stream_wave<5, MODE>(cs, sets, base); break;
+        case 6: bs_stream_wave<6, MODE>(cs, sets, base); break;
+        default: bs_stream_wave<7, MODE>(cs, sets, base); break;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Unified streaming form (bs128u): the bs128s pipeline with the wave index A a
+// runtime (wave-uniform) value, so all eight waves run ONE instruction stream;
+// only the small-layout layers branch on A, inside one asm statement each
+// (bs8_small.inc).  Eight template copies of the whole per-wave program do not
+// fit the instruction cache (bs128s: 1.8x slower than the same code run by all
+// waves).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void issue_dma_rt(const CodewordSet& cs, const SetAddr& a, uint32_t lds_base, uint32_t A) {
+    const uint32_t k = cs.k, es = (uint32_t)cs.elem_stride;
+    bs8::sfor<kPre>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        const uint32_t so = sym_off(16u * A + j, k, 0, es);
+        const uint32_t l = lds_base + A * (kPre * 2048u) + j * 2048u;
+        dma16(l, a.off[0], a.rs, so);
+        dma16(l + 1024u, a.off[1], a.rs, so);
+    });
+}
+
+__device__ __forceinline__ void issue_direct_rt(const CodewordSet& cs, const SetAddr& a, uint32_t A,
+                                                uint32_t (&P)[16 - kPre][8]) {
+    const uint32_t k = cs.k, es = (uint32_t)cs.elem_stride;
+    const __amdgpu_buffer_rsrc_t rs = as_rsrc(a.rs);
+    bs8::sfor<16 - kPre>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        const uint32_t so = sym_off(16u * A + kPre + j, k, 0, es);
+        const v4u x = __builtin_amdgcn_raw_buffer_load_b128(rs, a.off[0], so, 0);
+        const v4u y = __builtin_amdgcn_raw_buffer_load_b128(rs, a.off[1], so, 0);
+        P[j][0] = x.x; P[j][1] = x.y; P[j][2] = x.z; P[j][3] = x.w;
+        P[j][4] = y.x; P[j][5] = y.y; P[j][6] = y.z; P[j][7] = y.w;
+    });
+}
+
+// MODE bits (diagnostics; 0 = production): 2 = no arithmetic, 4 = no global memory
+template <int MODE>
+__device__ __forceinline__ void bs_uni_wave(const CodewordSet& cs, uint32_t sets, uint32_t lds_base, uint32_t A) {
+    constexpr bool ARITH = !(MODE & 2);
+    const bool MEM = !(MODE & 4) || cs.S == 1;  // runtime-false in mode 4 (keeps the code alive)
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t G = gridDim.x;
+    const uint32_t k = cs.k, es = (uint32_t)cs.elem_stride, oo = (uint32_t)cs.out_offset;
+    const uint32_t dread = lds_base + A * 16384u + lane * 16u;
+    const uint32_t ebase = lds_base + kDmaBytes + lane * 4u;
+    const uint32_t e_small = ebase + 4096u * A, e_large = ebase + 256u * A;
+    uint32_t X[16][8];
+    uint32_t P[16 - kPre][8];
+
+    uint32_t t = blockIdx.x;
+    SetAddr a = set_addr(cs, t, lane);
+    if (MEM) {
+        issue_dma_rt(cs, a, lds_base, A);
+        issue_direct_rt(cs, a, A, P);
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), visible to the compiler (see bs_stream_wave)
+    for (;;) {
+        {
+            v4u g[8];
+            bs8::sfor<2>([&](auto Hh) {
+                constexpr int hh = decltype(Hh)::value;
+                ds_r16x8<8192 * hh, 1024>(dread, g);
+                bs8::sfor<4>([&](auto J) {
+                    constexpr int j = 4 * hh + decltype(J)::value;
+                    const v4u x = g[2 * (j & 3)], y = g[2 * (j & 3) + 1];
+                    X[j][0] = x.x; X[j][1] = x.y; X[j][2] = x.z; X[j][3] = x.w;
+                    X[j][4] = y.x; X[j][5] = y.y; X[j][6] = y.z; X[j][7] = y.w;
+                });
+            });
+        }
+        bs8::sfor<16 - kPre>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            bs8::sfor<8>([&](auto I) { X[kPre + j][decltype(I)::value] = P[j][decltype(I)::value]; });
+        });
+        const uint32_t tn = t + G;
+        const bool more = tn < sets;
+        SetAddr an = a;
+        if (more) {
+            an = set_addr(cs, tn, lane);
+            if (MEM) {
+                issue_dma_rt(cs, an, lds_base, A);
+                issue_direct_rt(cs, an, A, P);
+            }
+        }
+        if constexpr (ARITH) {
+            bs8::sfor<16>([&](auto J) { bs8::transpose8_dev(X[decltype(J)::value]); });
+            bs8::small_ifft_all(X, A);
+        }
+        bs8::sfor<8>([&](auto Pp) { xch_to_large<decltype(Pp)::value>(X, e_small, e_large); });
+        if constexpr (ARITH) bs8::large_ifft_fft(X);
+        bs8::sfor<8>([&](auto Pp) { xch_to_small<decltype(Pp)::value>(X, e_large, e_small); });
+        if constexpr (ARITH) bs8::small_fft_all(X, A);
+        {
+            const __amdgpu_buffer_rsrc_t ro = as_rsrc(a.ro);
+            bs8::sfor<16>([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                if constexpr (ARITH) bs8::transpose8_dev(X[j]);
+                const uint32_t so = sym_off(16u * A + j, k, oo, es);
+                v4u x, y;
+                x.x = X[j][0]; x.y = X[j][1]; x.z = X[j][2]; x.w = X[j][3];
+                y.x = X[j][4]; y.y = X[j][5]; y.z = X[j][6]; y.w = X[j][7];
+                if (MEM) {
+                    __builtin_amdgcn_raw_buffer_store_b128(x, ro, a.off[0], so, 0);
+                    __builtin_amdgcn_raw_buffer_store_b128(y, ro, a.off[1], so, 0);
+                }
+            });
+        }
+        if (!more) break;
+        t = tn;
+        a = an;
+        // issue order: DMA(t) [16], direct(t) [16], stores(t - G) [32]
+        asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+    }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(512, 1) void encode_gf8_bs128u_kernel(CodewordSet cs, uint32_t sets) {
+    __shared__ uint32_t lds[(kDmaBytes + kXchBytes) / 4];
+    if (blockIdx.x >= sets) return;
+    bs_uni_wave<MODE>(cs, sets, (uint32_t)(uintptr_t)lds, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
 }
 
 // True when every offset the kernel forms stays below the buffer-resource limit
@@ -345,7 +633,25 @@ hipError_t launch_encode_gf8_bs128(const CodewordSet& cs, hipStream_t st) {
     const uint64_t sets = ((uint64_t)cs.count * cs.S + kSetBytes - 1) / kSetBytes;
     if (sets == 0) return hipSuccess;
     const uint32_t grid = (uint32_t)(sets < device_cus() ? sets : device_cus());
-    hipLaunchKernelGGL(encode_gf8_bs128_kernel, dim3(grid), dim3(512), 0, st, cs, (uint32_t)sets);
+    static const int variant = [] {
+        const char* v = getenv("RSM_BS_VARIANT");
+        return v ? atoi(v) : 0;
+    }();
+    switch (variant) {
+#define RSM_BS_CASE(m) \
+    case m: hipLaunchKernelGGL(encode_gf8_bs128_kernel<m>, dim3(grid), dim3(512), 0, st, cs, (uint32_t)sets); break;
+        RSM_BS_CASE(1) RSM_BS_CASE(2) RSM_BS_CASE(3) RSM_BS_CASE(4) RSM_BS_CASE(5)
+#undef RSM_BS_CASE
+#define RSM_BS_CASE(m) \
+    case 10 + m: hipLaunchKernelGGL(encode_gf8_bs128s_kernel<m>, dim3(grid), dim3(512), 0, st, cs, (uint32_t)sets); break;
+        RSM_BS_CASE(0) RSM_BS_CASE(2) RSM_BS_CASE(4) RSM_BS_CASE(8) RSM_BS_CASE(12)
+#undef RSM_BS_CASE
+#define RSM_BS_CASE(m) \
+    case 30 + m: hipLaunchKernelGGL(encode_gf8_bs128u_kernel<m>, dim3(grid), dim3(512), 0, st, cs, (uint32_t)sets); break;
+        RSM_BS_CASE(0) RSM_BS_CASE(2) RSM_BS_CASE(4)
+#undef RSM_BS_CASE
+        default: hipLaunchKernelGGL(encode_gf8_bs128u_kernel<0>, dim3(grid), dim3(512), 0, st, cs, (uint32_t)sets);
+    }
     return hipGetLastError();
 }
 

@@ -389,7 +389,7 @@ int rsm_extend_squares_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share
 
 int rsm_extend_squares_phase_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size, uint32_t count,
                                  int phase, void* stream) {
-    if (!ctx || !d_eds || k == 0 || (phase != 1 && phase != 2))
+    if (!ctx || !d_eds || k == 0 || phase < 1 || phase > 3)
         return fail(RSM_EINVAL, "rsm_extend_squares_phase_dev: bad arguments");
     if (int rc = validate_chunk_size(share_size)) return rc;
     if (count == 0) return RSM_OK;
