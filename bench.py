@@ -49,7 +49,7 @@ def parse():
     p.add_argument("--no-roots", action="store_true", help="skip the extension + Merkle roots timing")
     p.add_argument("--dist", action="store_true",
                    help="initialise torch.distributed even at N=1 (rehearses the sharded c5 path on one GPU)")
-    p.add_argument("--cpu-seconds", type=float, default=3.0)
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
     return p.parse_args()
 
 
@@ -301,11 +301,18 @@ def main():
 
     # synthetic ODS: seeded uniform bytes (SplitMix64) generated on the device; each
     # square's top-left quadrant is its ODS (the other quadrants are overwritten).
-    buf = R.DeviceBuffer(B * sq_bytes, local)
-    buf.fill_random(0x52534D543244 + rank)
+    # Two batches are used alternately, so a step never finds the previous step's
+    # squares in the 256 MiB Infinity Cache (rotate > 512 MiB).
+    bufs = [R.DeviceBuffer(B * sq_bytes, local) for _ in range(2)]
+    for i, b in enumerate(bufs):
+        b.fill_random(0x52534D543244 + 2 * rank + i)
+    buf = bufs[0]
+    nstep = [0]
 
     def step():
-        R._check(L.rsm_extend_squares_dev(ctx, buf.ptr, k, S, B, None))
+        b = bufs[nstep[0] & 1]
+        nstep[0] += 1
+        R._check(L.rsm_extend_squares_dev(ctx, b.ptr, k, S, B, None))
 
     for _ in range(a.warmup):
         step()
@@ -339,9 +346,13 @@ def main():
     # per-kernel durations: HIP events on the launch stream (the context stream)
     import ctypes
     row_ms, col_ms, step_ms = ctypes.c_float(), ctypes.c_float(), ctypes.c_float()
-    R._check(L.rsm_time_extend(ctx, buf.ptr, k, S, B, max(5, min(a.steps, 20)), ctypes.byref(row_ms),
-                               ctypes.byref(col_ms), ctypes.byref(step_ms)))
-    t_row, t_col = row_ms.value / 1e3, col_ms.value / 1e3
+    rms, cms = [], []
+    for r in range(max(6, min(a.steps, 20))):  # one row + one column launch per call, batches alternating
+        R._check(L.rsm_time_extend(ctx, bufs[r & 1].ptr, k, S, B, 1, ctypes.byref(row_ms), ctypes.byref(col_ms),
+                                   ctypes.byref(step_ms)))
+        rms.append(row_ms.value)
+        cms.append(col_ms.value)
+    t_row, t_col = sum(rms) / len(rms) / 1e3, sum(cms) / len(cms) / 1e3
 
     ods_bytes = k * k * S
     total = world * B * a.steps * ods_bytes
@@ -350,20 +361,22 @@ def main():
     algo_step = 4 * ods_bytes * B  # read Q0 once, write Q1+Q2+Q3
     col_bytes = 4 * ods_bytes * B  # column pass: [Q0|Q1] in, [Q2|Q3] out
     row_bytes = 2 * ods_bytes * B  # row pass: Q0 in, Q1 out
-    kname = "encode_gf8_kernel<128>" if k <= 128 else "encode_gf16_kernel"
-    dominant = ((kname + " column pass", col_bytes, t_col) if t_col >= t_row else (kname + " row pass", row_bytes, t_row))
+    bitsliced = 64 < k <= 128
+    kname = ("encode_gf8_bs128u_kernel" if bitsliced else "encode_gf8_kernel" if k <= 64
+             else "enc16_a/b/c (GF(2^16) passes)")
+    col_dom = t_col >= t_row
+    dominant = ((kname + " column pass", col_bytes, t_col) if col_dom else (kname + " row pass", row_bytes, t_row))
     ach = dominant[1] / dominant[2] / 1e9
     # HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC
     # passes (scripts/pmc_summary.py; FETCH_SIZE x2 gfx950 correction), matched by
-    # kernel and grid size -- null when no matching profile exists.
+    # kernel name (<MODE, PASS>: PASS 1 = column pass) -- null when no matching
+    # profile exists (e.g. the multi-kernel GF(2^16) passes).
     traffic = None
-    chunks = (S + 255) // 256 if k <= 128 else (S + 127) // 128
-    ncw = (W if t_col >= t_row else k) * B
-    grid_threads = (ncw * chunks + 3) // 4 * 256
     pmc_path = os.path.join(ROOT, "profiles", "pmc_latest.json")
-    if os.path.exists(pmc_path):
+    if bitsliced and os.path.exists(pmc_path):
+        want = "encode_gf8_bs128u_kernel<0, %d>" % (1 if col_dom else 0)
         for row in json.load(open(pmc_path)).get("launches", []):
-            if row["grid_threads"] == grid_threads and ("<%d>" % (1 << (k - 1).bit_length()) in row["kernel"]):
+            if want in row["kernel"] and row.get("batch_squares", B) == B:
                 traffic = int(row["traffic_bytes"])
     out = {
         "metric": "GiB/s device-resident 2D RS encode, k=128 square, 512 B shares; % HBM peak",
@@ -404,7 +417,8 @@ def main():
         out["cpu_baseline"] = None if a.no_cpu_baseline else cpu_baseline(k, S, a.cpu_seconds)
     if rank == 0 and world == 1 and not a.no_roots:
         out["with_roots"] = bench_roots(local, L, R, buf, k, S, B, a.steps)
-    buf.free()
+    for b in bufs:
+        b.free()
     if rank == 0 and world == 1 and not a.no_c3:
         out["c3"] = bench_c3(local, L, R)
     if not a.no_c5:

@@ -21,6 +21,7 @@
 // lanes share each twiddle (wave-uniform SGPR table loads).
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <cstdlib>
 #include <utility>
 #include "gf16.hpp"
 #include "rsm_kernels.hpp"
@@ -531,11 +532,26 @@ __global__ __launch_bounds__(256) void dec16_p5(Dec16 p) {  // group: FFT low + 
 
 inline uint32_t blocks_for(uint64_t tasks) { return (uint32_t)((tasks + 3) / 4); }
 
+// Work-array bytes per encode launch triple (A, B, C).  A batch whose work arrays
+// fit in ~64 MiB stays resident in the 256 MiB Infinity Cache between the passes
+// (MI355X_MICROARCH.md: a table stays resident while it and every byte streamed
+// between two uses fit in ~256 MiB), so only the codewords' own input and parity
+// reach HBM.  RSM_GF16_BATCH_MB overrides (A/B measurements).
+static uint64_t gf16_batch_bytes() {
+    static const uint64_t b = [] {
+        const char* v = getenv("RSM_GF16_BATCH_MB");
+        const uint64_t mb = v ? strtoull(v, nullptr, 10) : 0;
+        return (mb ? mb : 64ull) << 20;
+    }();
+    return b;
+}
+
 template <int M>
 hipError_t run_encode(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st) {
     const uint32_t chunks = (cs.S + 511) / 512;
     const uint64_t per_cw = (uint64_t)M * cs.S;
-    const uint32_t batch = (uint32_t)(g.scratch_bytes / per_cw);
+    uint32_t batch = (uint32_t)((g.scratch_bytes < gf16_batch_bytes() ? g.scratch_bytes : gf16_batch_bytes()) / per_cw);
+    if (batch == 0) batch = (uint32_t)(g.scratch_bytes / per_cw);
     if (batch == 0) return hipErrorOutOfMemory;
     for (uint32_t q0 = 0; q0 < cs.count; q0 += batch) {
         Enc16 p{cs, Res{g.perm, g.skew}, g.scratch, q0, cs.count - q0 < batch ? cs.count - q0 : batch, chunks};

@@ -1,32 +1,25 @@
 // kernels_gf8_bs.hip -- bit-sliced GF(2^8) encode for M = 128 (65 <= k <= 128).
 //
 // The byte-table kernel (kernels_gf8.hip) spends ~10 VALU per 4 bytes per GF
-// multiply and is VALU-bound (SQ counters: ~98% of VALU issue cycles on the
-// column pass).  Here 32 bytes of a symbol are 8 bit-planes and a multiply by a
-// constant is ~16 VALU per 32 bytes (bs8.hpp): 4.7K VALU per wave-set against
-// 9.4K.  A lane can hold 16 symbols x 8 planes (128 VGPRs), not the whole
-// 128-symbol codeword, so the transform is split between the 8 wavefronts of a
-// workgroup (bs8.hpp):
+// multiply and is VALU-bound.  Here 32 bytes of a symbol are 8 bit-planes and a
+// multiply by a constant is a short network of 3-input XORs (bs8.hpp,
+// gen/bs8_net.hpp).  A lane can hold 16 symbols x 8 planes (128 VGPRs), not the
+// whole 128-symbol codeword, so the transform is split between the 8 wavefronts
+// of a workgroup (bs8.hpp):
 //
 //   set       = 64 lanes x 32 bytes = 2 KiB of share width (e.g. four 512-byte
 //               codewords), all 128 symbols of it;
 //   wave w    : small layout, symbols e = 16w + j: IFFT layers d = 1,2,4
-//   LDS       : 2 rounds x 4 planes, [symbol][lane] x 16 B = 128 KiB
-//   wave w    : large layout, symbols e = 8h + w: IFFT d = 8..64, FFT d = 64..8
+//   LDS       : exchange, one bit-plane per round ([symbol][lane] x 4 B)
+//   wave w    : large layout, symbols e = 8h + w: IFFT d = 8..32, the merged
+//               d = 64 pair, FFT d = 32..8
 //   LDS back, FFT layers d = 4,2,1, planes -> bytes, store.
 //
-// The small layers' twiddles depend on w, so the whole per-wave program is a
-// template on w and the kernel branches once, at entry, into one of 8 copies:
-// no control-flow merge carries the 128 planes (a merge costs ~250 register
-// copies per wave and spills -- measured).
-//
-// Persistent: one workgroup per CU walks sets t = blockIdx.x, += gridDim.x, and
-// loads set t+G while computing set t -- symbols j >= 8 of each wave into 64
-// VGPRs (issued once the LDS buffer is released), j < 8 by LDS-DMA into the
-// 128 KiB exchange buffer (issued after the second exchange).  Both are waited
-// for with an explicit vmcnt that leaves the previous set's 32 stores in flight.
-// (With one set per workgroup, memory and compute phases of the CU do not
-// overlap: measured 4.2 TB/s for loads + stores with no arithmetic at all.)
+// All eight waves run ONE instruction stream: only the small layers' twiddles
+// depend on w, and each direction is one asm statement that branches on w inside
+// (bs8_small.inc).  Eight template copies of the whole per-wave program overflow
+// the instruction cache (measured 1.8x slower) and a control-flow merge of the
+// 128 planes costs ~250 register copies per wave (measured).
 //
 // Memory: lane l holds bytes [16l, 16l+16) and [1024+16l, +16) of the set's 2 KiB
 // (two dwordx4 per symbol; every wave instruction covers 1 KiB contiguous per
@@ -44,12 +37,6 @@ namespace {
 
 constexpr uint32_t kOobBs = 0x80000000u;
 constexpr uint32_t kSetBytes = 2048;
-
-__device__ __forceinline__ uint64_t cw_rel_bs(const CodewordSet& cs, uint32_t q) {
-    const uint32_t sq = q / cs.per_square;
-    const uint32_t t = q - sq * cs.per_square;
-    return (uint64_t)sq * cs.square_stride + (uint64_t)t * cs.cw_stride;
-}
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 
@@ -121,43 +108,10 @@ __device__ __forceinline__ void dma16(uint32_t lds_byte, uint32_t voff, v4u srd,
         : "memory");
 }
 
-template <int A>
-__device__ __forceinline__ void issue_dma(const CodewordSet& cs, const SetAddr& a, uint32_t lds_base) {
-    const uint32_t k = cs.k, es = (uint32_t)cs.elem_stride;
-    bs8::sfor<kPre>([&](auto J) {
-        constexpr int j = decltype(J)::value;
-        const uint32_t so = sym_off(16u * A + j, k, 0, es);
-        dma16(lds_base + ((A * kPre + j) * 2 + 0) * 1024u, a.off[0], a.rs, so);
-        dma16(lds_base + ((A * kPre + j) * 2 + 1) * 1024u, a.off[1], a.rs, so);
-    });
-}
-
-template <int A>
-__device__ __forceinline__ void issue_direct(const CodewordSet& cs, const SetAddr& a, uint32_t (&P)[16 - kPre][8]) {
-    const uint32_t k = cs.k, es = (uint32_t)cs.elem_stride;
-    const __amdgpu_buffer_rsrc_t rs = as_rsrc(a.rs);
-    bs8::sfor<16 - kPre>([&](auto J) {
-        constexpr int j = decltype(J)::value;
-        const uint32_t so = sym_off(16u * A + kPre + j, k, 0, es);
-        const v4u x = __builtin_amdgcn_raw_buffer_load_b128(rs, a.off[0], so, 0);
-        const v4u y = __builtin_amdgcn_raw_buffer_load_b128(rs, a.off[1], so, 0);
-        P[j][0] = x.x; P[j][1] = x.y; P[j][2] = x.z; P[j][3] = x.w;
-        P[j][4] = y.x; P[j][5] = y.y; P[j][6] = y.z; P[j][7] = y.w;
-    });
-}
-
-__device__ __forceinline__ void lds_barrier() {
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
-
 // LDS traffic as inline asm with immediate offsets: left to the compiler, the 32
 // loop-invariant per-symbol addresses are hoisted out of the set loop into 16+
 // VGPRs and the prefetch registers spill.  A read group waits for its own data
 // (lgkmcnt(0) inside the statement), so the compiler never sees stale outputs.
-template <uint32_t OFF>
-__device__ __forceinline__ void ds_w16(uint32_t base, v4u v) {
-    asm volatile("ds_write_b128 %0, %1 offset:%2" : : "v"(base), "v"(v), "i"(OFF) : "memory");
-}
 template <uint32_t O0, uint32_t STEP>
 __device__ __forceinline__ void ds_r16x8(uint32_t base, v4u (&r)[8]) {
     asm volatile(
@@ -176,176 +130,6 @@ __device__ __forceinline__ void ds_r16x8(uint32_t base, v4u (&r)[8]) {
         : "memory");
 }
 
-// Exchange buffer [symbol e][lane] x 16 B: byte e*1024 + 16*lane.  base0 covers
-// e < 64, base1 = base0 + 64 KiB covers e >= 64 (ds offsets are 16-bit).
-template <int A>
-struct XLayout {
-    // small layout e = 16A + j (all 16 symbols on one side of 64)
-    static constexpr bool small_hi = A >= 4;
-    static constexpr uint32_t small_off(int j) { return (uint32_t)((16 * A + j - (small_hi ? 64 : 0)) * 1024); }
-    // large layout e = 8j + A: j < 8 on base0, j >= 8 on base1
-    static constexpr uint32_t large_off(int j) { return (uint32_t)((8 * (j & 7) + A) * 1024); }
-};
-
-// Moves the 16 symbols of wave A between the small layout (e = 16A + j) and
-// the large layout (e = 8j + A), 4 planes per round.
-template <bool TO_LARGE, int A>
-__device__ __forceinline__ void exchange(uint32_t (&X)[16][8], uint32_t base0) {
-    using Lx = XLayout<A>;
-    const uint32_t base1 = base0 + 65536u;
-    const uint32_t bsmall = Lx::small_hi ? base1 : base0;
-    bs8::sfor<2>([&](auto R) {
-        constexpr int r = decltype(R)::value;
-        bs8::sfor<16>([&](auto J) {
-            constexpr int j = decltype(J)::value;
-            v4u v;
-            v.x = X[j][4 * r + 0]; v.y = X[j][4 * r + 1]; v.z = X[j][4 * r + 2]; v.w = X[j][4 * r + 3];
-            if constexpr (TO_LARGE) ds_w16<Lx::small_off(j)>(bsmall, v);
-            else ds_w16<Lx::large_off(j)>(j < 8 ? base0 : base1, v);
-        });
-        lds_barrier();
-        // read back in two groups of 8 (32 VGPRs of temporaries, not 64: the next
-        // set's direct loads may be in flight in P)
-        bs8::sfor<2>([&](auto Hh) {
-            constexpr int hh = decltype(Hh)::value;
-            v4u g[8];
-            if constexpr (TO_LARGE) ds_r16x8<Lx::large_off(8 * hh), 8192>(hh ? base1 : base0, g);
-            else ds_r16x8<Lx::small_off(8 * hh), 1024>(bsmall, g);
-            bs8::sfor<8>([&](auto J) {
-                constexpr int j = 8 * hh + decltype(J)::value;
-                const v4u v = g[j & 7];
-                X[j][4 * r + 0] = v.x; X[j][4 * r + 1] = v.y; X[j][4 * r + 2] = v.z; X[j][4 * r + 3] = v.w;
-            });
-        });
-        lds_barrier();
-    });
-}
-
-// The whole per-wave program for wave A (compile-time).  The set loop is rotated
-// so that a set's direct loads are issued and consumed in one iteration (the
-// compiler then counts them exactly: its waits leave the 32 stores of the
-// previous set in flight); only the planes X and the LDS-DMA cross iterations.
-//   iteration:  [issue direct loads of set t+G] small FFT(t), store(t)
-//               | wait vmcnt(32): DMA + direct loads of t+G landed
-//               | first half of t+G: read DMA, transpose, small IFFT, exchange,
-//                 large layers, exchange back, DMA of t+2G.
-// MODE bits (diagnostics; 0 = production): 1 = direct loads one iteration earlier,
-// 2 = no arithmetic (memory + LDS only), 4 = no global memory (compute + LDS only)
-template <int A, int MODE>
-__device__ __forceinline__ void bs_wave(const CodewordSet& cs, uint32_t sets, v4u* lds) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t lds_base = (uint32_t)(uintptr_t)lds;
-    const uint32_t xbase = lds_base + lane * 16u;
-    const uint32_t k = cs.k, es = (uint32_t)cs.elem_stride, oo = (uint32_t)cs.out_offset;
-    const uint32_t G = gridDim.x;
-    constexpr bool EARLY = MODE & 1, ARITH = !(MODE & 2);
-    const bool MEM = !(MODE & 4) || cs.S == 1;  // runtime-false in mode 4 (keeps the code alive)
-    uint32_t X[16][8];
-    uint32_t P[16 - kPre][8];
-
-    // symbols of a set whose DMA and direct loads have landed -> planes -> the
-    // first half of the transform, then the next-but-one set's DMA.
-    auto first_half = [&](uint32_t t) __attribute__((always_inline)) {
-        asm volatile("s_barrier" ::: "memory");  // every wave's DMA share has landed
-        {
-            v4u g[2][8];  // DMA buffer [wave][j][half][lane] x 16 B
-            const uint32_t b = xbase + A * (kPre * 2048u);
-            ds_r16x8<0, 1024>(b, g[0]);
-            ds_r16x8<8192, 1024>(b, g[1]);
-            bs8::sfor<kPre>([&](auto J) {
-                constexpr int j = decltype(J)::value;
-                const v4u x = g[(2 * j) >> 3][(2 * j) & 7], y = g[(2 * j + 1) >> 3][(2 * j + 1) & 7];
-                X[j][0] = x.x; X[j][1] = x.y; X[j][2] = x.z; X[j][3] = x.w;
-                X[j][4] = y.x; X[j][5] = y.y; X[j][6] = y.z; X[j][7] = y.w;
-            });
-        }
-        bs8::sfor<16 - kPre>([&](auto J) {
-            constexpr int j = decltype(J)::value;
-            bs8::sfor<8>([&](auto I) { X[kPre + j][decltype(I)::value] = P[j][decltype(I)::value]; });
-        });
-        lds_barrier();  // DMA buffer consumed by every wave
-        // EARLY: the next set's direct loads go out now, a whole iteration ahead
-        if (EARLY && MEM && t + G < sets) issue_direct<A>(cs, set_addr(cs, t + G, lane), P);
-        if constexpr (ARITH) {
-            bs8::sfor<16>([&](auto J) { bs8::transpose8(X[decltype(J)::value]); });
-            bs8::small_ifft<A>(X);
-        }
-        exchange<true, A>(X, xbase);
-        if constexpr (ARITH) bs8::large_ifft_fft(X);
-        exchange<false, A>(X, xbase);
-        if (MEM && t + G < sets) issue_dma<A>(cs, set_addr(cs, t + G, lane), lds_base);
-    };
-
-    uint32_t t = blockIdx.x;
-    {
-        const SetAddr a = set_addr(cs, t, lane);
-        if (MEM) {
-            issue_direct<A>(cs, a, P);
-            issue_dma<A>(cs, a, lds_base);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    first_half(t);
-    for (;;) {
-        const uint32_t tn = t + G;
-        const bool more = tn < sets;
-        if (!EARLY && MEM && more) issue_direct<A>(cs, set_addr(cs, tn, lane), P);
-        if constexpr (ARITH) bs8::small_fft<A>(X);
-        {
-            const SetAddr a = set_addr(cs, t, lane);
-            const __amdgpu_buffer_rsrc_t ro = as_rsrc(a.ro);
-            bs8::sfor<16>([&](auto J) {
-                constexpr int j = decltype(J)::value;
-                if constexpr (ARITH) bs8::transpose8(X[j]);
-                const uint32_t so = sym_off(16u * A + j, k, oo, es);
-                v4u x, y;
-                x.x = X[j][0]; x.y = X[j][1]; x.z = X[j][2]; x.w = X[j][3];
-                y.x = X[j][4]; y.y = X[j][5]; y.z = X[j][6]; y.w = X[j][7];
-                if (MEM) {
-                    __builtin_amdgcn_raw_buffer_store_b128(x, ro, a.off[0], so, 0);
-                    __builtin_amdgcn_raw_buffer_store_b128(y, ro, a.off[1], so, 0);
-                }
-            });
-        }
-        if (!more) break;
-        t = tn;
-        // issue order: DMA(t) [16], direct(t) [16], stores(t - G) [32]
-        asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
-        first_half(t);
-    }
-}
-
-}  // namespace
-
-template <int MODE>
-__global__ __launch_bounds__(512, 1) void encode_gf8_bs128_kernel(CodewordSet cs, uint32_t sets) {
-    __shared__ v4u lds[128 * 64];
-    if (blockIdx.x >= sets) return;
-    switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
-        case 0: bs_wave<0, MODE>(cs, sets, lds); break;
-        case 1: bs_wave<1, MODE>(cs, sets, lds); break;
-        case 2: bs_wave<2, MODE>(cs, sets, lds); break;
-        case 3: bs_wave<3, MODE>(cs, sets, lds); break;
-        case 4: bs_wave<4, MODE>(cs, sets, lds); break;
-        case 5: bs_wave<5, MODE>(cs, sets, lds); break;
-        case 6: bs_wave<6, MODE>(cs, sets, lds); break;
-        default: bs_wave<7, MODE>(cs, sets, lds); break;
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Streaming form (bs128s): every load of set t+G is issued at the START of set
-// t, so HBM traffic runs under the whole transform instead of its tail.
-//   LDS  D [wave 8][j 8][half 2][lane 64] x 16 B = 128 KiB: symbols j < 8 of each
-//        wave by LDS-DMA; each wave reads and re-fills only its own 16 KiB, so
-//        the DMA needs no barrier, only the wave's own vmcnt.
-//   LDS  E [symbol 128][lane 64] x 4 B = 32 KiB: the layout exchange, one bit
-//        plane per round (16 ds_write_b32, barrier, 16 ds_read_b32 in place,
-//        barrier), 8 rounds each way.
-//   VGPR P: symbols j >= 8 of the next set (64 registers).
-// Iteration t: read D -> X[0..7], X[8..15] = P; issue DMA + direct loads of
-// t+G; transform; store t; wait vmcnt(32) (the 32 stores may stay in flight).
-// ---------------------------------------------------------------------------
 constexpr uint32_t kDmaBytes = 128u * 1024u;
 constexpr uint32_t kXchBytes = 32u * 1024u;
 
@@ -384,117 +168,6 @@ __device__ __forceinline__ void xch_to_small(uint32_t (&X)[16][8], uint32_t wb, 
 #undef RSM_XR
 #undef RSM_XOPS
 
-// MODE bits (diagnostics; 0 = production): 2 = no arithmetic, 4 = no global memory
-template <int A, int MODE>
-__device__ __forceinline__ void bs_stream_wave(const CodewordSet& cs, uint32_t sets, uint32_t lds_base) {
-    constexpr bool ARITH = !(MODE & 2);
-    const bool MEM = !(MODE & 4) || cs.S == 1;  // runtime-false in mode 4 (keeps the code alive)
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t G = gridDim.x;
-    const uint32_t k = cs.k, es = (uint32_t)cs.elem_stride, oo = (uint32_t)cs.out_offset;
-    const uint32_t dread = lds_base + A * 16384u + lane * 16u;
-    const uint32_t ebase = lds_base + kDmaBytes + lane * 4u;
-    const uint32_t e_small = ebase + 4096u * A, e_large = ebase + 256u * A;
-    uint32_t X[16][8];
-    uint32_t P[16 - kPre][8];
-
-    uint32_t t = blockIdx.x;
-    SetAddr a = set_addr(cs, t, lane);
-    if (MEM) {
-        issue_dma<A>(cs, a, lds_base);
-        issue_direct<A>(cs, a, P);
-    }
-    // vmcnt(0) through the builtin (gfx9 encoding: vmcnt 0, expcnt 7, lgkmcnt 15):
-    // the compiler sees it, so its own wait for P at the loop head stays vmcnt(32)
-    __builtin_amdgcn_s_waitcnt(0x0F70);
-    for (;;) {
-        {
-            v4u g[8];
-            bs8::sfor<2>([&](auto Hh) {
-                constexpr int hh = decltype(Hh)::value;
-                ds_r16x8<8192 * hh, 1024>(dread, g);
-                bs8::sfor<4>([&](auto J) {
-                    constexpr int j = 4 * hh + decltype(J)::value;
-                    const v4u x = g[2 * (j & 3)], y = g[2 * (j & 3) + 1];
-                    X[j][0] = x.x; X[j][1] = x.y; X[j][2] = x.z; X[j][3] = x.w;
-                    X[j][4] = y.x; X[j][5] = y.y; X[j][6] = y.z; X[j][7] = y.w;
-                });
-            });
-        }
-        bs8::sfor<16 - kPre>([&](auto J) {
-            constexpr int j = decltype(J)::value;
-            bs8::sfor<8>([&](auto I) { X[kPre + j][decltype(I)::value] = P[j][decltype(I)::value]; });
-        });
-        const uint32_t tn = t + G;
-        const bool more = tn < sets;
-        SetAddr an = a;
-        if (more) {
-            an = set_addr(cs, tn, lane);
-            if (MEM) {
-                issue_dma<A>(cs, an, lds_base);
-                issue_direct<A>(cs, an, P);
-            }
-        }
-        if constexpr (ARITH) {
-            bs8::sfor<16>([&](auto J) { bs8::transpose8_dev(X[decltype(J)::value]); });
-            bs8::small_ifft<A>(X);
-        }
-        bs8::sfor<8>([&](auto Pp) { xch_to_large<decltype(Pp)::value>(X, e_small, e_large); });
-        if constexpr (ARITH) bs8::large_ifft_fft(X);
-        bs8::sfor<8>([&](auto Pp) { xch_to_small<decltype(Pp)::value>(X, e_large, e_small); });
-        if constexpr (ARITH) bs8::small_fft<A>(X);
-        {
-            const __amdgpu_buffer_rsrc_t ro = as_rsrc(a.ro);
-            bs8::sfor<16>([&](auto J) {
-                constexpr int j = decltype(J)::value;
-                if constexpr (ARITH) bs8::transpose8_dev(X[j]);
-                const uint32_t so = sym_off(16u * A + j, k, oo, es);
-                v4u x, y;
-                x.x = X[j][0]; x.y = X[j][1]; x.z = X[j][2]; x.w = X[j][3];
-                y.x = X[j][4]; y.y = X[j][5]; y.z = X[j][6]; y.w = X[j][7];
-                if (MEM) {
-                    __builtin_amdgcn_raw_buffer_store_b128(x, ro, a.off[0], so, 0);
-                    __builtin_amdgcn_raw_buffer_store_b128(y, ro, a.off[1], so, 0);
-                }
-            });
-        }
-        if (!more) break;
-        t = tn;
-        a = an;
-        // issue order: DMA(t) [16], direct(t) [16], stores(t - G) [32]
-        asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
-    }
-}
-
-template <int MODE>
-__global__ __launch_bounds__(512, 1) void encode_gf8_bs128s_kernel(CodewordSet cs, uint32_t sets) {
-    __shared__ uint32_t lds[(kDmaBytes + kXchBytes) / 4];
-    if (blockIdx.x >= sets) return;
-    const uint32_t base = (uint32_t)(uintptr_t)lds;
-    if constexpr ((MODE & 8) != 0) {  // diagnostic: every wave runs wave 0's program (wrong output)
-        bs_stream_wave<0, MODE>(cs, sets, base);
-        return;
-    }
-    switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
-        case 0: bs_stream_wave<0, MODE>(cs, sets, base); break;
-        case 1: bs_stream_wave<1, MODE>(cs, sets, base); break;
-        case 2: bs_stream_wave<2, MODE>(cs, sets, base); break;
-        case 3: bs_stream_wave<3, MODE>(cs, sets, base); break;
-        case 4: bs_stream_wave<4, MODE>(cs, sets, base); break;
-        case 5: bs_stream_wave<5, MODE>(cs, sets, base); break;
-        case 6: bs_stream_wave<6, MODE>(cs, sets, base); break;
-        default: bs_stream_wave<7, MODE>(cs, sets, base); break;
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Unified streaming form (bs128u): the bs128s pipeline with the wave index A a
-// runtime (wave-uniform) value, so all eight waves run ONE instruction stream;
-// only the small-layout layers branch on A, inside one asm statement each
-// (bs8_small.inc).  Eight template copies of the whole per-wave program do not
-// fit the instruction cache (bs128s: 1.8x slower than the same code run by all
-// waves).
-// ---------------------------------------------------------------------------
 __device__ __forceinline__ void issue_dma_rt(const CodewordSet& cs, const SetAddr& a, uint32_t lds_base, uint32_t A) {
     const uint32_t k = cs.k, es = (uint32_t)cs.elem_stride;
     bs8::sfor<kPre>([&](auto J) {
@@ -520,9 +193,13 @@ __device__ __forceinline__ void issue_direct_rt(const CodewordSet& cs, const Set
     });
 }
 
-// MODE bits (diagnostics; 0 = production): 2 = no arithmetic, 4 = no global memory
+// MODE bits (diagnostics; 0 = production): 2 = no arithmetic, 4 = no global memory.
+// REV: sets are taken in reverse order (the column pass walks the squares the row
+// pass just wrote from the most recent one back, so the first squares it reads are
+// still in the 256 MiB Infinity Cache).
 template <int MODE>
-__device__ __forceinline__ void bs_uni_wave(const CodewordSet& cs, uint32_t sets, uint32_t lds_base, uint32_t A) {
+__device__ __forceinline__ void bs_uni_wave(const CodewordSet& cs, uint32_t sets, uint32_t rev, uint32_t lds_base,
+                                            uint32_t A) {
     constexpr bool ARITH = !(MODE & 2);
     const bool MEM = !(MODE & 4) || cs.S == 1;  // runtime-false in mode 4 (keeps the code alive)
     const uint32_t lane = threadIdx.x & 63u;
@@ -534,8 +211,9 @@ __device__ __forceinline__ void bs_uni_wave(const CodewordSet& cs, uint32_t sets
     uint32_t X[16][8];
     uint32_t P[16 - kPre][8];
 
+    auto addr = [&](uint32_t tt) { return set_addr(cs, rev ? sets - 1u - tt : tt, lane); };
     uint32_t t = blockIdx.x;
-    SetAddr a = set_addr(cs, t, lane);
+    SetAddr a = addr(t);
     if (MEM) {
         issue_dma_rt(cs, a, lds_base, A);
         issue_direct_rt(cs, a, A, P);
@@ -563,7 +241,7 @@ __device__ __forceinline__ void bs_uni_wave(const CodewordSet& cs, uint32_t sets
         const bool more = tn < sets;
         SetAddr an = a;
         if (more) {
-            an = set_addr(cs, tn, lane);
+            an = addr(tn);
             if (MEM) {
                 issue_dma_rt(cs, an, lds_base, A);
                 issue_direct_rt(cs, an, A, P);
@@ -600,12 +278,16 @@ __device__ __forceinline__ void bs_uni_wave(const CodewordSet& cs, uint32_t sets
     }
 }
 
-template <int MODE>
-__global__ __launch_bounds__(512, 1) void encode_gf8_bs128u_kernel(CodewordSet cs, uint32_t sets) {
+// PASS only names the launch in profiles (0 row pass, 1 column pass / other).
+template <int MODE, int PASS>
+__global__ __launch_bounds__(512, 1) void encode_gf8_bs128u_kernel(CodewordSet cs, uint32_t sets, uint32_t rev) {
     __shared__ uint32_t lds[(kDmaBytes + kXchBytes) / 4];
     if (blockIdx.x >= sets) return;
-    bs_uni_wave<MODE>(cs, sets, (uint32_t)(uintptr_t)lds, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
+    bs_uni_wave<MODE>(cs, sets, rev, (uint32_t)(uintptr_t)lds, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
 }
+
+}  // namespace
+
 
 // True when every offset the kernel forms stays below the buffer-resource limit
 // (2^31): the set's codeword span + the largest symbol offset.
@@ -633,25 +315,25 @@ hipError_t launch_encode_gf8_bs128(const CodewordSet& cs, hipStream_t st) {
     const uint64_t sets = ((uint64_t)cs.count * cs.S + kSetBytes - 1) / kSetBytes;
     if (sets == 0) return hipSuccess;
     const uint32_t grid = (uint32_t)(sets < device_cus() ? sets : device_cus());
-    static const int variant = [] {
-        const char* v = getenv("RSM_BS_VARIANT");
+    // RSM_BS_MODE: diagnostics (2 = no arithmetic, 4 = no global memory; wrong output)
+    // RSM_BS_REV=0: column pass in forward set order (A/B of the cache-reuse order)
+    static const int mode = [] {
+        const char* v = getenv("RSM_BS_MODE");
         return v ? atoi(v) : 0;
     }();
-    switch (variant) {
-#define RSM_BS_CASE(m) \
-    case m: hipLaunchKernelGGL(encode_gf8_bs128_kernel<m>, dim3(grid), dim3(512), 0, st, cs, (uint32_t)sets); break;
-        RSM_BS_CASE(1) RSM_BS_CASE(2) RSM_BS_CASE(3) RSM_BS_CASE(4) RSM_BS_CASE(5)
-#undef RSM_BS_CASE
-#define RSM_BS_CASE(m) \
-    case 10 + m: hipLaunchKernelGGL(encode_gf8_bs128s_kernel<m>, dim3(grid), dim3(512), 0, st, cs, (uint32_t)sets); break;
-        RSM_BS_CASE(0) RSM_BS_CASE(2) RSM_BS_CASE(4) RSM_BS_CASE(8) RSM_BS_CASE(12)
-#undef RSM_BS_CASE
-#define RSM_BS_CASE(m) \
-    case 30 + m: hipLaunchKernelGGL(encode_gf8_bs128u_kernel<m>, dim3(grid), dim3(512), 0, st, cs, (uint32_t)sets); break;
-        RSM_BS_CASE(0) RSM_BS_CASE(2) RSM_BS_CASE(4)
-#undef RSM_BS_CASE
-        default: hipLaunchKernelGGL(encode_gf8_bs128u_kernel<0>, dim3(grid), dim3(512), 0, st, cs, (uint32_t)sets);
-    }
+    static const uint32_t rev_col = [] {
+        const char* v = getenv("RSM_BS_REV");
+        return v ? (uint32_t)(atoi(v) != 0) : 1u;
+    }();
+    const bool row = cs.elem_stride == cs.S;
+    const uint32_t rev = row ? 0u : rev_col;
+#define RSM_BS_LAUNCH(m, p) \
+    hipLaunchKernelGGL((encode_gf8_bs128u_kernel<m, p>), dim3(grid), dim3(512), 0, st, cs, (uint32_t)sets, rev)
+    if (mode == 2) RSM_BS_LAUNCH(2, 1);
+    else if (mode == 4) RSM_BS_LAUNCH(4, 1);
+    else if (row) RSM_BS_LAUNCH(0, 0);
+    else RSM_BS_LAUNCH(0, 1);
+#undef RSM_BS_LAUNCH
     return hipGetLastError();
 }
 

@@ -1,15 +1,20 @@
 #!/bin/bash
-# A/B of encode kernel variants (RSM_BS_VARIANT): correctness (phase 0, CHECK) + row/col timing.
+# A/B of the M = 128 encode kernel: correctness of both passes vs the oracle, then
+# row / column / whole-step timing, for RSM_BS_MODE (0 production, 2 no
+# arithmetic, 4 no global memory -- diagnostics, wrong output) x RSM_BS_REV.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-for v in ${VARIANTS:-0 10}; do
-  RSM_BS_VARIANT=$v CHECK=1 timeout -k 10 60 python3 scripts/run_extend.py 20 16 3 > /tmp/o.txt 2>&1 || { cat /tmp/o.txt; exit 3; }
-  echo "v=$v $(cat /tmp/o.txt)"
-  for ph in 1 2; do
+for cfg in ${CONFIGS:-"0 1" "0 0" "2 1" "4 1"}; do
+  set -- $cfg; m=$1; r=$2
+  if [ "$m" = 0 ]; then
+    RSM_BS_MODE=$m RSM_BS_REV=$r CHECK=1 timeout -k 10 60 python3 scripts/run_extend.py 20 16 3 > /tmp/o.txt 2>&1 || { cat /tmp/o.txt; exit 3; }
+    echo "mode=$m rev=$r $(cat /tmp/o.txt)"
+  fi
+  for ph in 1 2 3; do
     for b in ${BATCHES:-16 64}; do
-      RSM_BS_VARIANT=$v timeout -k 10 60 python3 scripts/run_extend.py 30 $b $ph > /tmp/o.txt 2>&1 || { cat /tmp/o.txt; exit 3; }
-      echo "v=$v $(cat /tmp/o.txt)"
+      RSM_BS_MODE=$m RSM_BS_REV=$r timeout -k 10 60 python3 scripts/run_extend.py 30 $b $ph > /tmp/o.txt 2>&1 || { cat /tmp/o.txt; exit 3; }
+      echo "mode=$m rev=$r $(cat /tmp/o.txt)"
     done
   done
 done
