@@ -4,8 +4,9 @@
 // bit-planes (plane i = bit i of each of the 32 bytes).  Multiplication by a
 // compile-time constant exp(L) is then a fixed GF(2)-linear map of the planes:
 //   out_i = XOR_{j : bit i of (2^j * exp(L)) = 1} y_j
-// i.e. ~4 plane XORs per output plane, 2 per v_bitop3_b32 (3-input XOR) -- about
-// 16 VALU per 32 bytes, against 80 for the byte-table (v_perm) multiply.
+// written as v_bitop3_b32 (3-input XOR) networks with up to three shared
+// temporaries, searched at build time (gen/bs8_net.hpp) -- ~15 VALU per 32 bytes,
+// against 80 for the byte-table (v_perm) multiply.
 //
 // The additive-FFT schedule is the one of kernels_gf8.hip (IFFT_DIT layers
 // d = 1..M/2 with skew offset M-1, then FFT_DIT layers M/2..1 with offset -1;
@@ -39,94 +40,47 @@ RSM_HD void sfor(F&& f) {
     }(std::make_integer_sequence<int, N>{});
 }
 
-// acc ^= b ^ c  /  acc ^= b.  On the device each is one volatile instruction, so
-// the network runs in program order and updates its planes in place: left to
-// schedule compiler-generated XORs freely, LLVM hoists and shares terms across
-// butterflies and across the 8 per-wave variants of the small layers and spills
-// hundreds of VGPRs (measured: 355 spills, -25% throughput).  Plain 32-bit VALU
-// ops interlock on each other; the boundary to compiler-generated code (which
-// may copy these registers with 64-bit moves) is padded in kernels_gf8_bs.hip.
-RSM_HD void xor3_into(uint32_t& acc, uint32_t b, uint32_t c) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(acc) : "v"(b), "v"(c));
-#else
-    acc ^= b ^ c;
-#endif
-}
-RSM_HD void xor_into(uint32_t& acc, uint32_t b) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    asm volatile("v_xor_b32 %0, %0, %1" : "+v"(acc) : "v"(b));
-#else
-    acc ^= b;
-#endif
-}
-
-// rows[i] has bit j set iff bit i of (2^j * exp(L)) is set.
-struct Rows {
-    uint8_t r[8];
-};
-constexpr Rows mul_rows(unsigned L) {
-    Rows m{};
-    for (unsigned j = 0; j < 8; ++j) {
-        const unsigned p = gf8_mul_log(1u << j, L);
-        for (unsigned i = 0; i < 8; ++i)
-            if ((p >> i) & 1u) m.r[i] = static_cast<uint8_t>(m.r[i] | (1u << j));
-    }
-    return m;
-}
-
-constexpr int ctz8(unsigned m) {
-    int i = 0;
-    while (!((m >> i) & 1u)) ++i;
-    return i;
-}
-
-// acc ^= XOR of y[j] for the bits j of MASK, two planes per 3-input XOR.
-template <unsigned MASK>
-RSM_HD void acc_terms(uint32_t& acc, const uint32_t (&y)[8]) {
-    if constexpr (MASK != 0) {
-        constexpr int j1 = ctz8(MASK);
-        constexpr unsigned rest = MASK & (MASK - 1);
-        if constexpr (rest == 0) {
-            xor_into(acc, y[j1]);
-        } else {
-            constexpr int j2 = ctz8(rest);
-            xor3_into(acc, y[j1], y[j2]);
-            acc_terms<rest & (rest - 1)>(acc, y);
-        }
-    }
-}
-
-// x ^= y * exp(L)
-template <unsigned L>
-RSM_HD void muladd(uint32_t (&x)[8], const uint32_t (&y)[8]) {
-    constexpr Rows R = mul_rows(L);
-    sfor<8>([&](auto I) { acc_terms<R.r[decltype(I)::value]>(x[decltype(I)::value], y); });
-}
-
 #if defined(__HIPCC__)
 // Device butterflies: one generated asm block each (bs8_asm.inc, from
-// gen/gen_bs8_asm.cpp; the same networks as muladd below).  One block per
-// butterfly instead of one statement per instruction: the compiler pads every
-// asm boundary with an s_nop (a 4-cycle issue slot).
+// gen/gen_bs8_asm.cpp).  One block per butterfly instead of one statement per
+// instruction: the compiler pads every asm boundary with an s_nop (a 4-cycle
+// issue slot).
 #define RSM_BS8_DEV __device__ __forceinline__
 template <unsigned L>
 RSM_BS8_DEV void ifft2_asm(uint32_t (&x)[8], uint32_t (&y)[8]);
 template <unsigned L>
 RSM_BS8_DEV void fft2_asm(uint32_t (&x)[8], uint32_t (&y)[8]);
+template <unsigned L>
+RSM_BS8_DEV void mid2_asm(uint32_t (&x)[8], uint32_t (&y)[8]);
 #include "bs8_asm.inc"
 // small-layout layers of all eight waves, one asm statement each (branch on A inside)
 #include "bs8_small.inc"
 #endif
 
+// Host reference: the same networks, interpreted from the generated table.
+#include "bs8_net.inc"
+template <unsigned L>
+inline void muladd_host(uint32_t (&x)[8], const uint32_t (&y)[8]) {
+    uint32_t r[19] = {};
+    for (int i = 0; i < 8; ++i) r[i] = x[i], r[8 + i] = y[i];
+    for (int n = 0; n < kNetLen[L]; ++n) {
+        const NetOp& o = kNet[L][n];
+        const uint32_t v = o.kind == 0 ? r[o.a] : o.kind == 3 ? (r[o.a] ^ r[o.b] ^ r[o.c]) : (r[o.a] ^ r[o.b]);
+        r[o.dst] = o.kind >= 2 ? v : (r[o.dst] ^ v);
+    }
+    for (int i = 0; i < 8; ++i) x[i] = r[i];
+}
+
 // IFFT_DIT2: y ^= x; x ^= y*L.   FFT_DIT2: x ^= y*L; y ^= x.   L == 255: XOR only.
+// MID: y ^= x; x ^= y*L; y ^= x -- an IFFT_DIT2 (twiddle L1) directly followed by an
+// FFT_DIT2 (L2) on the same pair, since x ^= L1*y' ^ L2*y' = (exp L1 + exp L2)*y'.
 template <unsigned L>
 RSM_HD void ifft2(uint32_t (&x)[8], uint32_t (&y)[8]) {
 #if defined(__HIP_DEVICE_COMPILE__)
     ifft2_asm<L>(x, y);
 #else
-    sfor<8>([&](auto I) { xor_into(y[decltype(I)::value], x[decltype(I)::value]); });
-    if constexpr (L != 255u) muladd<L>(x, y);
+    for (int i = 0; i < 8; ++i) y[i] ^= x[i];
+    if constexpr (L != 255u) muladd_host<L>(x, y);
 #endif
 }
 template <unsigned L>
@@ -134,9 +88,25 @@ RSM_HD void fft2(uint32_t (&x)[8], uint32_t (&y)[8]) {
 #if defined(__HIP_DEVICE_COMPILE__)
     fft2_asm<L>(x, y);
 #else
-    if constexpr (L != 255u) muladd<L>(x, y);
-    sfor<8>([&](auto I) { xor_into(y[decltype(I)::value], x[decltype(I)::value]); });
+    if constexpr (L != 255u) muladd_host<L>(x, y);
+    for (int i = 0; i < 8; ++i) y[i] ^= x[i];
 #endif
+}
+template <unsigned L>
+RSM_HD void mid2(uint32_t (&x)[8], uint32_t (&y)[8]) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    mid2_asm<L>(x, y);
+#else
+    for (int i = 0; i < 8; ++i) y[i] ^= x[i];
+    if constexpr (L != 255u) muladd_host<L>(x, y);
+    for (int i = 0; i < 8; ++i) y[i] ^= x[i];
+#endif
+}
+
+// Leopard's log of zero is 255; the log of exp(L1) + exp(L2).
+constexpr unsigned elem_of_log(unsigned L) { return L == 255u ? 0u : kGf8.exp[L]; }
+constexpr unsigned log_of_sum(unsigned L1, unsigned L2) {
+    return (elem_of_log(L1) ^ elem_of_log(L2)) == 0 ? 255u : kGf8.log[elem_of_log(L1) ^ elem_of_log(L2)];
 }
 
 // 8x8 bit-matrix transpose applied to each of the 4 byte lanes of 8 words:
@@ -231,9 +201,12 @@ RSM_HD void small_fft(uint32_t (&X)[16][8]) {
 
 // Large layers: registers h = 0..15 hold symbols e = 8h + g (any g < 8): the
 // pairing bit is a bit of h and the block start 8*(h & ~(2dh-1)) does not
-// depend on g, so one code path serves every g.
+// depend on g, so one code path serves every g.  The encoder's last IFFT layer
+// (d = 64, SKEW[kOffEnc + 64]) and first FFT layer (d = 64, SKEW[63]) act on the
+// same pairs with nothing in between: one merged butterfly, one multiply.
+inline constexpr unsigned kMidLog = log_of_sum(kGf8.skew[kOffEnc + 64], kGf8.skew[63]);
 RSM_HD void large_ifft_fft(uint32_t (&X)[16][8]) {
-    sfor<4>([&](auto LG) {  // IFFT d = 8, 16, 32, 64
+    sfor<3>([&](auto LG) {  // IFFT d = 8, 16, 32
         constexpr int dh = 1 << decltype(LG)::value;
         sfor<16 / (2 * dh)>([&](auto B) {
             constexpr int hb = decltype(B)::value * 2 * dh;
@@ -241,8 +214,9 @@ RSM_HD void large_ifft_fft(uint32_t (&X)[16][8]) {
             sfor<dh>([&](auto Q) { ifft2<L>(X[hb + decltype(Q)::value], X[hb + decltype(Q)::value + dh]); });
         });
     });
-    sfor<4>([&](auto LG) {  // FFT d = 64, 32, 16, 8
-        constexpr int dh = 8 >> decltype(LG)::value;
+    sfor<8>([&](auto Q) { mid2<kMidLog>(X[decltype(Q)::value], X[decltype(Q)::value + 8]); });
+    sfor<3>([&](auto LG) {  // FFT d = 32, 16, 8
+        constexpr int dh = 4 >> decltype(LG)::value;
         sfor<16 / (2 * dh)>([&](auto B) {
             constexpr int hb = decltype(B)::value * 2 * dh;
             constexpr unsigned L = kGf8.skew[-1 + 8 * hb + 8 * dh];

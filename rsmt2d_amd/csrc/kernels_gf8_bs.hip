@@ -218,7 +218,12 @@ __device__ __forceinline__ void bs_uni_wave(const CodewordSet& cs, uint32_t sets
         issue_dma_rt(cs, a, lds_base, A);
         issue_direct_rt(cs, a, A, P);
     }
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), visible to the compiler (see bs_stream_wave)
+    // vmcnt(0) through the builtin (gfx9 encoding: vmcnt 0, expcnt 7, lgkmcnt 15): the
+    // compiler sees it, so its own wait for P at the loop head stays vmcnt(32).  LDS-DMA
+    // data is read only after the wave's vmcnt AND a barrier (cdna_hip_programming.md
+    // §5.7 item 1).
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    asm volatile("s_barrier" ::: "memory");
     for (;;) {
         {
             v4u g[8];
@@ -268,13 +273,20 @@ __device__ __forceinline__ void bs_uni_wave(const CodewordSet& cs, uint32_t sets
                     __builtin_amdgcn_raw_buffer_store_b128(x, ro, a.off[0], so, 0);
                     __builtin_amdgcn_raw_buffer_store_b128(y, ro, a.off[1], so, 0);
                 }
+                // The next statement is an asm block whose early-clobber temporaries the
+                // compiler may place in the data registers of the store just issued; a
+                // dwordx4 store reads its data over several cycles and the hazard
+                // recognizer does not look inside asm, so pad here (without it the last
+                // lane groups of the second store intermittently wrote the temporaries).
+                asm volatile("s_nop 2" ::: "memory");
             });
         }
         if (!more) break;
         t = tn;
         a = an;
-        // issue order: DMA(t) [16], direct(t) [16], stores(t - G) [32]
-        asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+        // issue order: DMA(t) [16], direct(t) [16], stores(t - G) [32]; then the
+        // barrier that makes the landed LDS-DMA data readable
+        asm volatile("s_waitcnt vmcnt(32)\n\ts_barrier" ::: "memory");
     }
 }
 

@@ -5,8 +5,9 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-for cfg in ${CONFIGS:-"0 1" "0 0" "2 1" "4 1"}; do
-  set -- $cfg; m=$1; r=$2
+# CONFIGS: MODE_REV tokens
+for cfg in ${CONFIGS:-0_1 0_0 2_1 4_1}; do
+  m=${cfg%_*}; r=${cfg#*_}
   if [ "$m" = 0 ]; then
     RSM_BS_MODE=$m RSM_BS_REV=$r CHECK=1 timeout -k 10 60 python3 scripts/run_extend.py 20 16 3 > /tmp/o.txt 2>&1 || { cat /tmp/o.txt; exit 3; }
     echo "mode=$m rev=$r $(cat /tmp/o.txt)"

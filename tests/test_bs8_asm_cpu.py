@@ -1,0 +1,113 @@
+"""CPU check of the GENERATED device butterflies the bit-sliced M = 128 encode
+kernel executes (rsmt2d_amd/csrc/bs8_asm.inc and bs8_small.inc, written by
+gen/gen_bs8_asm.cpp and gen/gen_bs8_small.cpp).  Every v_xor_b32 / v_bitop3_b32
+line is parsed and executed on random bit-planes and the result compared with the
+butterfly computed byte by byte from the oracle's GF(2^8) tables (klauspost
+leopard8 restatement, SURVEY.md A.4: IFFT_DIT2 y ^= x; x ^= y*exp(L) --
+FFT_DIT2 x ^= y*exp(L); y ^= x -- L == 255 XOR only).  The GPU code never runs
+here: this pins the instruction text the kernel runs, shared-temporary networks
+and the merged middle butterfly included."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+import oracle
+
+CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "rsmt2d_amd", "csrc")
+INS = re.compile(r'"(v_xor_b32|v_bitop3_b32) %(\d+), %(\d+), %(\d+)(?:, %(\d+) bitop3:0x96)?')
+
+
+def parse(text):
+    ops = []
+    for m in INS.finditer(text):
+        c = int(m.group(5)) if m.group(5) else -1
+        assert (m.group(1) == "v_bitop3_b32") == (c >= 0), m.group(0)
+        ops.append((int(m.group(2)), int(m.group(3)), int(m.group(4)), c))
+    return ops
+
+
+def execute(ops, regs):
+    for d, a, b, c in ops:
+        regs[d] = regs[a] ^ regs[b] ^ (regs[c] if c >= 0 else 0)
+
+
+@pytest.fixture(scope="module")
+def gf():
+    exp, log, skew, _ = oracle.tables8()
+    exp, log = exp.astype(np.int64), log.astype(np.int64)
+
+    def mul(v, L):  # v * exp(L), Leopard mulLog; L == 255 is the zero multiplier
+        if L == 255:
+            return np.zeros_like(v)
+        s = log[v] + L
+        s = (s + (s >> 8)) & 255
+        return np.where(v == 0, 0, exp[s]).astype(np.uint8)
+    return mul, [int(x) for x in skew]
+
+
+def planes(b):  # 32 bytes -> 8 u32 planes (bit n of plane i = bit i of byte n)
+    bits = np.unpackbits(b[:, None], axis=1, bitorder="little")
+    return [int(np.packbits(bits[:, i], bitorder="little").view("<u4")[0]) for i in range(8)]
+
+
+def unplanes(p):
+    return np.array([sum(((p[i] >> n) & 1) << i for i in range(8)) for n in range(32)], np.uint8)
+
+
+def butterfly(kind, L, x, y, mul):
+    if kind == "ifft2_asm":
+        y = y ^ x
+        x = x ^ mul(y, L)
+    elif kind == "fft2_asm":
+        x = x ^ mul(y, L)
+        y = y ^ x
+    else:  # mid2_asm
+        y = y ^ x
+        x = x ^ mul(y, L)
+        y = y ^ x
+    return x, y
+
+
+@pytest.mark.parametrize("name", ["ifft2_asm", "fft2_asm", "mid2_asm"])
+def test_butterfly_blocks(gf, name):
+    mul, _ = gf
+    text = open(os.path.join(CSRC, "bs8_asm.inc")).read()
+    blocks = re.findall(r"void %s<(\d+)>\(.*?\{(.*?)\n\}" % name, text, re.S)
+    assert sorted(int(L) for L, _ in blocks) == list(range(256))
+    rng = np.random.default_rng(8)
+    for L, body in blocks:
+        L = int(L)
+        x = rng.integers(0, 256, 32, dtype=np.uint8)
+        y = rng.integers(0, 256, 32, dtype=np.uint8)
+        regs = planes(x) + planes(y) + [int(v) for v in rng.integers(0, 2**32, 3)]  # garbage temporaries
+        execute(parse(body), regs)
+        wx, wy = butterfly(name, L, x, y, mul)
+        assert unplanes(regs[:8]).tobytes() == wx.tobytes(), (name, L)
+        assert unplanes(regs[8:16]).tobytes() == wy.tobytes(), (name, L)
+
+
+@pytest.mark.parametrize("name,inverse", [("small_ifft_all", True), ("small_fft_all", False)])
+def test_small_layer_blocks(gf, name, inverse):
+    """The per-wave small layers (symbols e = 16A + j, d = 1, 2, 4; bs8.hpp)."""
+    mul, skew = gf
+    text = open(os.path.join(CSRC, "bs8_small.inc")).read()
+    fn = re.search(r"void %s\(.*?\{(.*?)\n\}" % name, text, re.S).group(1)
+    parts = re.split(r"\.L%s(\d)_%%=:" % name, fn)
+    bodies = {int(parts[i]): parts[i + 1] for i in range(1, len(parts), 2)}
+    assert sorted(bodies) == list(range(8))
+    rng = np.random.default_rng(9)
+    for A, body in bodies.items():
+        sym = [rng.integers(0, 256, 32, dtype=np.uint8) for _ in range(16)]
+        regs = sum((planes(s) for s in sym), []) + [int(v) for v in rng.integers(0, 2**32, 3)]
+        execute(parse(body), regs)
+        ref = [s.copy() for s in sym]
+        for d in ((1, 2, 4) if inverse else (4, 2, 1)):
+            for b in range(0, 16, 2 * d):
+                L = skew[127 + 16 * A + b + d] if inverse else skew[-1 + 16 * A + b + d]
+                for q in range(d):
+                    ref[b + q], ref[b + q + d] = butterfly("ifft2_asm" if inverse else "fft2_asm", L,
+                                                           ref[b + q], ref[b + q + d], mul)
+        for j in range(16):
+            assert unplanes(regs[8 * j:8 * j + 8]).tobytes() == ref[j].tobytes(), (name, A, j)
