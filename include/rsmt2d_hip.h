@@ -104,6 +104,12 @@ int rsm_encode_batch_dev(rsm_ctx* ctx, const void* d_in, void* d_out, uint32_t k
  * width <= 2048.  Asynchronous on `stream`. */
 int rsm_roots_dev(rsm_ctx* ctx, const void* d_eds, uint32_t width, uint32_t share_size, void* d_roots,
                   void* stream);
+/* rsm_roots_dev over `count` consecutive squares ([count][width][width][share_size],
+ * as rsm_extend_squares_dev lays them out): d_roots receives [count][2][width][32]
+ * bytes.  One launch pair for the batch (BenchmarkExtensionWithRoots,
+ * extendeddatasquare_test.go:309-334, over many squares). */
+int rsm_roots_squares_dev(rsm_ctx* ctx, const void* d_eds, uint32_t width, uint32_t share_size, uint32_t count,
+                          void* d_roots, void* stream);
 /* Device-resident batched reconstruct of whole rows (axis 0) or columns (axis 1)
  * of one [2k][2k][S] square: d_presence is one byte per cell, d_indices the
  * vectors to rebuild (each must have >= k cells present).  Asynchronous. */

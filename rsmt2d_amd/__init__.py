@@ -118,6 +118,7 @@ SIGNATURES = {
     "rsm_extend_rows_dev": (_I32, [_VP, _VP, _U32, _U32, _U32, _U32, _VP]),
     "rsm_extend_cols_dev": (_I32, [_VP, _VP, _U32, _U32, _U32, _U32, _VP]),
     "rsm_roots_dev": (_I32, [_VP, _VP, _U32, _U32, _VP, _VP]),
+    "rsm_roots_squares_dev": (_I32, [_VP, _VP, _U32, _U32, _U32, _VP, _VP]),
     "rsm_encode_batch_dev": (_I32, [_VP, _VP, _VP, _U32, _U32, _U32, _U64, _U64, _VP]),
     "rsm_decode_vectors_dev": (_I32, [_VP, _VP, _VP, _U32, _U32, _I32, _VP, _U32, _VP]),
     "rsm_ctx_stream": (_VP, [_VP]),

@@ -97,7 +97,7 @@ __global__ __launch_bounds__(256) void leaf_hash_kernel(const uint8_t* __restric
         uint32_t w[16];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const v4u v = __builtin_nontemporal_load(p + blk * 4u + q);
+            const v4u v = p[blk * 4u + q];  // plain load: the other half of the 128-B line is the next block
             const uint32_t b0 = __builtin_bswap32(v.x), b1 = __builtin_bswap32(v.y);
             const uint32_t b2 = __builtin_bswap32(v.z), b3 = __builtin_bswap32(v.w);
             w[4 * q + 0] = shift8(prev, b0);
@@ -121,10 +121,13 @@ __global__ __launch_bounds__(256) void leaf_hash_kernel(const uint8_t* __restric
 
 constexpr uint32_t kMaxLevel1 = 1024;  // W <= 2048
 
-// One workgroup per tree: blockIdx.x < W -> row tree blockIdx.x, else column tree.
-// roots: [2][W][32] bytes (big-endian digest bytes, as Tree.Root() returns them).
+// One workgroup per tree: blockIdx.x < W -> row tree blockIdx.x, else column tree;
+// blockIdx.y = square of a batch.  roots: [squares][2][W][32] bytes (big-endian
+// digest bytes, as Tree.Root() returns them).
 __global__ __launch_bounds__(256) void tree_root_kernel(const uint32_t* __restrict__ leaf, uint32_t W,
                                                         uint8_t* __restrict__ roots) {
+    leaf += (uint64_t)blockIdx.y * W * W * 8u;
+    roots += (uint64_t)blockIdx.y * 2u * W * 32u;
     __shared__ uint32_t lvl[2][kMaxLevel1][8];
     __shared__ uint32_t sub[16][8];
     const uint32_t axis = blockIdx.x >= W ? 1u : 0u;
@@ -192,14 +195,16 @@ __global__ __launch_bounds__(256) void tree_root_kernel(const uint32_t* __restri
 
 bool roots_dev_supported(uint32_t W) { return W >= 2 && W <= 2 * kMaxLevel1 && W < (1u << 16); }
 
-// d_leaf: scratch of W*W*32 bytes.
-hipError_t launch_roots(const uint8_t* d_eds, uint32_t W, uint32_t S, uint32_t* d_leaf, uint8_t* d_roots,
-                        hipStream_t st) {
-    const uint32_t cells = W * W;
+// `squares` consecutive [W][W][S] squares; d_leaf: scratch of squares*W*W*32 bytes.
+// The cells of all squares are one leaf launch (a single square is only W*W
+// threads: one wave per SIMD on a 256-CU chip, latency-bound SHA rounds).
+hipError_t launch_roots(const uint8_t* d_eds, uint32_t W, uint32_t S, uint32_t squares, uint32_t* d_leaf,
+                        uint8_t* d_roots, hipStream_t st) {
+    const uint32_t cells = W * W * squares;
     hipLaunchKernelGGL(leaf_hash_kernel, dim3((cells + 255) / 256), dim3(256), 0, st, d_eds, cells, S, d_leaf);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(tree_root_kernel, dim3(2 * W), dim3(256), 0, st, d_leaf, W, d_roots);
+    hipLaunchKernelGGL(tree_root_kernel, dim3(2 * W, squares), dim3(256), 0, st, d_leaf, W, d_roots);
     return hipGetLastError();
 }
 

@@ -88,6 +88,7 @@ int extend_squares(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, uint32_
 // DefaultTree row + column roots of a device-resident complete [W][W][S] square:
 // d_roots receives 2*W*32 bytes (row roots, then column roots).  RSM_EUNSUPPORTED
 // when W is outside roots_dev_supported().
-int device_roots(rsm_ctx* ctx, const uint8_t* d_eds, uint32_t W, uint32_t S, uint8_t* d_roots, hipStream_t st);
+int device_roots(rsm_ctx* ctx, const uint8_t* d_eds, uint32_t W, uint32_t S, uint8_t* d_roots, hipStream_t st,
+                 uint32_t squares = 1);
 
 }  // namespace rsm

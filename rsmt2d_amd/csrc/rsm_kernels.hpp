@@ -54,10 +54,10 @@ hipError_t launch_decode_gf8(const DecodeSet& ds, hipStream_t st);
 struct Gf16Dev;
 hipError_t launch_encode_gf16(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st);
 hipError_t launch_decode_gf16(const DecodeSet& ds, const Gf16Dev& g, hipStream_t st);
-// Merkle roots (kernels_sha.hip): d_leaf scratch of W*W*32 bytes
+// Merkle roots (kernels_sha.hip): d_leaf scratch of squares*W*W*32 bytes
 bool roots_dev_supported(uint32_t W);
-hipError_t launch_roots(const uint8_t* d_eds, uint32_t W, uint32_t S, uint32_t* d_leaf, uint8_t* d_roots,
-                        hipStream_t st);
+hipError_t launch_roots(const uint8_t* d_eds, uint32_t W, uint32_t S, uint32_t squares, uint32_t* d_leaf,
+                        uint8_t* d_roots, hipStream_t st);
 hipError_t launch_fill_random(void* p, uint64_t bytes, uint64_t seed, hipStream_t st);
 hipError_t launch_compare(const uint8_t* a, const uint8_t* b, uint64_t n, uint32_t* mismatch, hipStream_t st);
 hipError_t launch_compare_parity(const uint8_t* a, const uint8_t* b, uint32_t k, uint32_t S, uint32_t axis,

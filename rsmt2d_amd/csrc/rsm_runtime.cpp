@@ -194,12 +194,15 @@ int extend_squares(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, uint32_
     return launch_encode(ctx, cols, st);
 }
 
-int device_roots(rsm_ctx* ctx, const uint8_t* d_eds, uint32_t W, uint32_t S, uint8_t* d_roots, hipStream_t st) {
+int device_roots(rsm_ctx* ctx, const uint8_t* d_eds, uint32_t W, uint32_t S, uint8_t* d_roots, hipStream_t st,
+                 uint32_t squares) {
     if (!roots_dev_supported(W)) return fail(RSM_EUNSUPPORTED, "device roots: width %u not supported", W);
+    if ((uint64_t)W * W * squares >= (1ull << 32) || squares > 65535)
+        return fail(RSM_EINVAL, "device roots: %u squares of width %u exceed one launch", squares, W);
     DevBuf& leaf = ctx->dev_buf(30);
-    hipError_t e = leaf.ensure((size_t)W * W * 32);
+    hipError_t e = leaf.ensure((size_t)W * W * 32 * squares);
     if (e != hipSuccess) return hip_fail(e, "hipMalloc (leaf digests)");
-    if ((e = launch_roots(d_eds, W, S, static_cast<uint32_t*>(leaf.ptr), d_roots, st)) != hipSuccess)
+    if ((e = launch_roots(d_eds, W, S, squares, static_cast<uint32_t*>(leaf.ptr), d_roots, st)) != hipSuccess)
         return hip_fail(e, "roots kernel launch");
     return RSM_OK;
 }
@@ -444,6 +447,16 @@ int rsm_roots_dev(rsm_ctx* ctx, const void* d_eds, uint32_t width, uint32_t shar
     std::lock_guard<std::mutex> lk(ctx->mu);
     return device_roots(ctx, static_cast<const uint8_t*>(d_eds), width, share_size, static_cast<uint8_t*>(d_roots),
                         stream ? static_cast<hipStream_t>(stream) : ctx->stream);
+}
+
+int rsm_roots_squares_dev(rsm_ctx* ctx, const void* d_eds, uint32_t width, uint32_t share_size, uint32_t count,
+                          void* d_roots, void* stream) {
+    if (!ctx || !d_eds || !d_roots || width == 0) return fail(RSM_EINVAL, "rsm_roots_squares_dev: bad arguments");
+    if (int rc = validate_chunk_size(share_size)) return rc;
+    if (count == 0) return RSM_OK;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    return device_roots(ctx, static_cast<const uint8_t*>(d_eds), width, share_size, static_cast<uint8_t*>(d_roots),
+                        stream ? static_cast<hipStream_t>(stream) : ctx->stream, count);
 }
 
 int rsm_encode_batch_dev(rsm_ctx* ctx, const void* d_in, void* d_out, uint32_t k, uint32_t share_size,

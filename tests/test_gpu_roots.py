@@ -55,3 +55,20 @@ def test_eds_roots_device_path(lib, rng):
     sq = crossword.Square(eds.Flattened())
     assert eds.RowRoots() == sq.roots(crossword.Row)
     assert eds.ColRoots() == sq.roots(crossword.Col)
+
+
+def test_batched_roots_match_per_square(lib):
+    """rsm_roots_squares_dev over 3 squares == rsm_roots_dev of each (pinned above)."""
+    W, S, n = 24, 64, 3
+    eds = oracle.splitmix64_bytes(n * W * W * S, seed=77).reshape(n, W, W, S)
+    buf = R.DeviceBuffer(eds.nbytes)
+    buf.upload(np.ascontiguousarray(eds))
+    out = R.DeviceBuffer(n * 2 * W * 32)
+    R._check(lib.rsm_roots_squares_dev(buf.ctx, buf.ptr, W, S, n, out.ptr, None))
+    R._check(lib.rsm_sync(buf.ctx))
+    raw = out.download()
+    buf.free()
+    out.free()
+    for i in range(n):
+        got = [raw[(2 * W * i + j) * 32:(2 * W * i + j + 1) * 32].tobytes() for j in range(2 * W)]
+        assert got == _device_roots(lib, eds[i]), i
