@@ -373,8 +373,10 @@ def main():
     pmc_path = os.path.join(ROOT, "profiles", "pmc_latest.json")
     if bitsliced and os.path.exists(pmc_path):
         want = "encode_gf8_bs128u_kernel<0, %d>" % (1 if col_dom else 0)
+        sets = (W if col_dom else k) * B * S // 2048
+        grid_threads = min(sets, 256) * 512  # persistent grid: one 512-thread workgroup per CU
         for row in json.load(open(pmc_path)).get("launches", []):
-            if want in row["kernel"] and row.get("batch_squares", B) == B:
+            if want in row["kernel"] and row["grid_threads"] == grid_threads:
                 traffic = int(row["traffic_bytes"])
     out = {
         "metric": "GiB/s device-resident 2D RS encode, k=128 square, 512 B shares; % HBM peak",

@@ -532,16 +532,17 @@ __global__ __launch_bounds__(256) void dec16_p5(Dec16 p) {  // group: FFT low + 
 
 inline uint32_t blocks_for(uint64_t tasks) { return (uint32_t)((tasks + 3) / 4); }
 
-// Work-array bytes per encode launch triple (A, B, C).  A batch whose work arrays
-// fit in ~64 MiB stays resident in the 256 MiB Infinity Cache between the passes
-// (MI355X_MICROARCH.md: a table stays resident while it and every byte streamed
-// between two uses fit in ~256 MiB), so only the codewords' own input and parity
-// reach HBM.  RSM_GF16_BATCH_MB overrides (A/B measurements).
+// Work-array bytes per encode launch triple (A, B, C).  Measured on config 4 (k=256,
+// S=2048) and 5 (k=512, S=512): capping a batch at 64 MiB so that its work arrays
+// stay in the Infinity Cache between the passes is SLOWER (175 vs 196 GiB/s, 0.90
+// vs 0.77 ms) than one launch triple over up to 1 GiB of work arrays -- the extra
+// launches cost more than the HBM round trips they save.  RSM_GF16_BATCH_MB
+// overrides (A/B measurements).
 static uint64_t gf16_batch_bytes() {
     static const uint64_t b = [] {
         const char* v = getenv("RSM_GF16_BATCH_MB");
         const uint64_t mb = v ? strtoull(v, nullptr, 10) : 0;
-        return (mb ? mb : 64ull) << 20;
+        return (mb ? mb : 1024ull) << 20;
     }();
     return b;
 }

@@ -128,7 +128,11 @@ __global__ __launch_bounds__(256) void tree_root_kernel(const uint32_t* __restri
                                                         uint8_t* __restrict__ roots) {
     leaf += (uint64_t)blockIdx.y * W * W * 8u;
     roots += (uint64_t)blockIdx.y * 2u * W * 32u;
-    __shared__ uint32_t lvl[2][kMaxLevel1][8];
+    // two ping-pong levels of W/2 digests, sized at launch (dynamic LDS): 8 KiB for
+    // W = 256 instead of a fixed 64 KiB, so 8 trees share a CU instead of 2
+    extern __shared__ uint32_t lvl_raw[];
+    const uint32_t half = W / 2;
+    auto lvl = [&](uint32_t buf, uint32_t j) -> uint32_t* { return lvl_raw + ((size_t)buf * half + j) * 8u; };
     __shared__ uint32_t sub[16][8];
     const uint32_t axis = blockIdx.x >= W ? 1u : 0u;
     const uint32_t idx = blockIdx.x - axis * W;
@@ -156,13 +160,13 @@ __global__ __launch_bounds__(256) void tree_root_kernel(const uint32_t* __restri
             } else {
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {
-                    L[i] = lvl[cur ^ 1u][2 * j][i];
-                    R[i] = lvl[cur ^ 1u][2 * j + 1][i];
+                    L[i] = lvl(cur ^ 1u, 2 * j)[i];
+                    R[i] = lvl(cur ^ 1u, 2 * j + 1)[i];
                 }
             }
             node_hash(L, R, o);
 #pragma unroll
-            for (int i = 0; i < 8; ++i) lvl[cur][j][i] = o[i];
+            for (int i = 0; i < 8; ++i) lvl(cur, j)[i] = o[i];
             if (((n >> hgt) & 1u) && j == cnt - 1) {
 #pragma unroll
                 for (int i = 0; i < 8; ++i) sub[hgt][i] = o[i];
@@ -204,7 +208,8 @@ hipError_t launch_roots(const uint8_t* d_eds, uint32_t W, uint32_t S, uint32_t s
     hipLaunchKernelGGL(leaf_hash_kernel, dim3((cells + 255) / 256), dim3(256), 0, st, d_eds, cells, S, d_leaf);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(tree_root_kernel, dim3(2 * W, squares), dim3(256), 0, st, d_leaf, W, d_roots);
+    hipLaunchKernelGGL(tree_root_kernel, dim3(2 * W, squares), dim3(256), (size_t)2 * (W / 2) * 32, st, d_leaf, W,
+                       d_roots);
     return hipGetLastError();
 }
 
