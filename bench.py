@@ -50,6 +50,7 @@ def parse():
     p.add_argument("--dist", action="store_true",
                    help="initialise torch.distributed even at N=1 (rehearses the sharded c5 path on one GPU)")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--one-stream", action="store_true", help="GF(2^8): do not alternate steps over two streams")
     return p.parse_args()
 
 
@@ -304,17 +305,33 @@ def main():
     bufs = [R.DeviceBuffer(B * sq_bytes, local) for _ in range(2)]
     for i, b in enumerate(bufs):
         b.fill_random(0x52534D543244 + 2 * rank + i)
+    R._check(L.rsm_sync(ctx))
     buf = bufs[0]
     nstep = [0]
+    # GF(2^8): consecutive steps alternate between two streams (each step's row and
+    # column passes stay ordered on its own stream), so one step's column-pass tail
+    # overlaps the next step's row-pass prologue.  GF(2^16) shares the context's work
+    # arrays between launches: one stream.
+    import ctypes
+    streams = [None]
+    if k <= 128 and not a.one_stream:
+        s2 = ctypes.c_void_p()
+        R._check(L.rsm_stream_create(ctx, ctypes.byref(s2)))
+        streams.append(s2)
 
     def step():
-        b = bufs[nstep[0] & 1]
+        i = nstep[0]
         nstep[0] += 1
-        R._check(L.rsm_extend_squares_dev(ctx, b.ptr, k, S, B, None))
+        R._check(L.rsm_extend_squares_dev(ctx, bufs[i & 1].ptr, k, S, B, streams[i % len(streams)]))
+
+    def sync_all():
+        R._check(L.rsm_sync(ctx))
+        for st in streams[1:]:
+            R._check(L.rsm_stream_sync(st))
 
     for _ in range(a.warmup):
         step()
-    R._check(L.rsm_sync(ctx))
+    sync_all()
     # correctness gate on one square before timing (the oracle is the checker only)
     if rank == 0:
         import oracle
@@ -329,11 +346,11 @@ def main():
             torch.cuda.synchronize()
 
     barrier()
-    R._check(L.rsm_sync(ctx))
+    sync_all()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
-    R._check(L.rsm_sync(ctx))
+    sync_all()
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
@@ -419,6 +436,8 @@ def main():
         out["with_roots"] = bench_roots(local, L, R, buf, k, S, B, a.steps)
     for b in bufs:
         b.free()
+    for st in streams[1:]:
+        R._check(L.rsm_stream_destroy(ctx, st))
     if rank == 0 and world == 1 and not a.no_c3:
         out["c3"] = bench_c3(local, L, R)
     if not a.no_c5:

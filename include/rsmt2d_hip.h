@@ -128,6 +128,13 @@ int rsm_memcpy(rsm_ctx* ctx, void* dst, const void* src, uint64_t bytes, int kin
 /* SplitMix64 byte stream (seeded synthetic shares), asynchronous on the ctx stream. */
 int rsm_dev_fill_random(rsm_ctx* ctx, void* d, uint64_t bytes, uint64_t seed);
 int rsm_sync(rsm_ctx* ctx);
+/* Extra HIP streams on the context's device, for callers that pipeline independent
+ * batches (e.g. step n's column pass beside step n+1's row pass on another
+ * stream).  GF(2^16) encodes share the context's work arrays: keep them on one
+ * stream. */
+int rsm_stream_create(rsm_ctx* ctx, void** out);
+int rsm_stream_destroy(rsm_ctx* ctx, void* stream);
+int rsm_stream_sync(void* stream);
 /* Event-timed extension of `count` in-place squares on the ctx stream, averaged
  * over `reps`: row pass, column pass and their sum, in milliseconds. */
 int rsm_time_extend(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size, uint32_t count,

@@ -127,6 +127,9 @@ SIGNATURES = {
     "rsm_memcpy": (_I32, [_VP, _VP, _VP, _U64, _I32]),
     "rsm_dev_fill_random": (_I32, [_VP, _VP, _U64, _U64]),
     "rsm_sync": (_I32, [_VP]),
+    "rsm_stream_create": (_I32, [_VP, ctypes.POINTER(_VP)]),
+    "rsm_stream_destroy": (_I32, [_VP, _VP]),
+    "rsm_stream_sync": (_I32, [_VP]),
     "rsm_time_extend": (_I32, [_VP, _VP, _U32, _U32, _U32, _U32, ctypes.POINTER(ctypes.c_float),
                                ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
     "rsm_default_tree_root": (_I32, [_VP, _I32, _U32, _VP, _U32, _U32, _VP, _VP]),

@@ -95,17 +95,21 @@ constexpr int kPre = 8;  // symbols j < kPre of each wave arrive by LDS-DMA
 // LDS-DMA (buffer_load_dwordx4 ... lds): 16 B per lane to M0 + 16*lane.  Inline
 // asm, so the compiler neither tracks nor conservatively drains it; the caller
 // waits with an explicit vmcnt.
+template <bool NT>
 __device__ __forceinline__ void dma16(uint32_t lds_byte, uint32_t voff, v4u srd, uint32_t soff) {
     uint32_t keep;  // M0 is compiler-reserved: save and restore it around the DMA
-    asm volatile(
-        "s_mov_b32 %0, m0\n\t"
-        "s_mov_b32 m0, %1\n\t"
-        "s_nop 4\n\t"
-        "buffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
-        "s_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "s"(lds_byte), "v"(voff), "s"(srd), "s"(soff)
-        : "memory");
+    if constexpr (NT)
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 4\n\t"
+                     "buffer_load_dwordx4 %2, %3, %4 offen nt lds\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "s"(lds_byte), "v"(voff), "s"(srd), "s"(soff)
+                     : "memory");
+    else
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 4\n\t"
+                     "buffer_load_dwordx4 %2, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "s"(lds_byte), "v"(voff), "s"(srd), "s"(soff)
+                     : "memory");
 }
 
 // LDS traffic as inline asm with immediate offsets: left to the compiler, the 32
@@ -186,17 +190,19 @@ __device__ __forceinline__ void xch_to_small(uint32_t (&X)[16][8], uint32_t wb, 
 #undef RSM_W_LARGE
 #undef RSM_SYNC
 
+template <bool NT>
 __device__ __forceinline__ void issue_dma_rt(const CodewordSet& cs, const SetAddr& a, uint32_t lds_base, uint32_t A) {
     const uint32_t k = cs.k, es = (uint32_t)cs.elem_stride;
     bs8::sfor<kPre>([&](auto J) {
         constexpr int j = decltype(J)::value;
         const uint32_t so = sym_off(16u * A + j, k, 0, es);
         const uint32_t l = lds_base + kXchBytes + A * (kPre * 2048u) + j * 2048u;
-        dma16(l, a.off[0], a.rs, so);
-        dma16(l + 1024u, a.off[1], a.rs, so);
+        dma16<NT>(l, a.off[0], a.rs, so);
+        dma16<NT>(l + 1024u, a.off[1], a.rs, so);
     });
 }
 
+template <bool NT>
 __device__ __forceinline__ void issue_direct_rt(const CodewordSet& cs, const SetAddr& a, uint32_t A,
                                                 uint32_t (&P)[16 - kPre][8]) {
     const uint32_t k = cs.k, es = (uint32_t)cs.elem_stride;
@@ -204,14 +210,15 @@ __device__ __forceinline__ void issue_direct_rt(const CodewordSet& cs, const Set
     bs8::sfor<16 - kPre>([&](auto J) {
         constexpr int j = decltype(J)::value;
         const uint32_t so = sym_off(16u * A + kPre + j, k, 0, es);
-        const v4u x = __builtin_amdgcn_raw_buffer_load_b128(rs, a.off[0], so, 0);
-        const v4u y = __builtin_amdgcn_raw_buffer_load_b128(rs, a.off[1], so, 0);
+        const v4u x = __builtin_amdgcn_raw_buffer_load_b128(rs, a.off[0], so, NT ? 2 : 0);
+        const v4u y = __builtin_amdgcn_raw_buffer_load_b128(rs, a.off[1], so, NT ? 2 : 0);
         P[j][0] = x.x; P[j][1] = x.y; P[j][2] = x.z; P[j][3] = x.w;
         P[j][4] = y.x; P[j][5] = y.y; P[j][6] = y.z; P[j][7] = y.w;
     });
 }
 
 // MODE bits: 8 = exchange writes by ds_write_addtid_b32 (production: 8);
+// 16 = non-temporal stores, 32 = non-temporal loads (A/B);
 // diagnostics: 2 = no arithmetic, 4 = no global memory.
 // REV: sets are taken in reverse order (the column pass walks the squares the row
 // pass just wrote from the most recent one back, so the first squares it reads are
@@ -219,7 +226,7 @@ __device__ __forceinline__ void issue_direct_rt(const CodewordSet& cs, const Set
 template <int MODE>
 __device__ __forceinline__ void bs_uni_wave(const CodewordSet& cs, uint32_t sets, uint32_t rev, uint32_t lds_base,
                                             uint32_t A) {
-    constexpr bool ARITH = !(MODE & 2), ADDTID = (MODE & 8) != 0;
+    constexpr bool ARITH = !(MODE & 2), ADDTID = (MODE & 8) != 0, NTS = (MODE & 16) != 0, NTL = (MODE & 32) != 0;
     const bool MEM = !(MODE & 4) || cs.S == 1;  // runtime-false in mode 4 (keeps the code alive)
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t G = gridDim.x;
@@ -236,8 +243,8 @@ __device__ __forceinline__ void bs_uni_wave(const CodewordSet& cs, uint32_t sets
     uint32_t t = blockIdx.x;
     SetAddr a = addr(t);
     if (MEM) {
-        issue_dma_rt(cs, a, lds_base, A);
-        issue_direct_rt(cs, a, A, P);
+        issue_dma_rt<NTL>(cs, a, lds_base, A);
+        issue_direct_rt<NTL>(cs, a, A, P);
     }
     // vmcnt(0) through the builtin (gfx9 encoding: vmcnt 0, expcnt 7, lgkmcnt 15): the
     // compiler sees it, so its own wait for P at the loop head stays vmcnt(32).  LDS-DMA
@@ -269,8 +276,8 @@ __device__ __forceinline__ void bs_uni_wave(const CodewordSet& cs, uint32_t sets
         if (more) {
             an = addr(tn);
             if (MEM) {
-                issue_dma_rt(cs, an, lds_base, A);
-                issue_direct_rt(cs, an, A, P);
+                issue_dma_rt<NTL>(cs, an, lds_base, A);
+                issue_direct_rt<NTL>(cs, an, A, P);
             }
         }
         if constexpr (ARITH) {
@@ -291,8 +298,8 @@ __device__ __forceinline__ void bs_uni_wave(const CodewordSet& cs, uint32_t sets
                 x.x = X[j][0]; x.y = X[j][1]; x.z = X[j][2]; x.w = X[j][3];
                 y.x = X[j][4]; y.y = X[j][5]; y.z = X[j][6]; y.w = X[j][7];
                 if (MEM) {
-                    __builtin_amdgcn_raw_buffer_store_b128(x, ro, a.off[0], so, 0);
-                    __builtin_amdgcn_raw_buffer_store_b128(y, ro, a.off[1], so, 0);
+                    __builtin_amdgcn_raw_buffer_store_b128(x, ro, a.off[0], so, NTS ? 2 : 0);
+                    __builtin_amdgcn_raw_buffer_store_b128(y, ro, a.off[1], so, NTS ? 2 : 0);
                 }
                 // The next statement is an asm block whose early-clobber temporaries the
                 // compiler may place in the data registers of the store just issued; a
@@ -366,6 +373,9 @@ hipError_t launch_encode_gf8_bs128(const CodewordSet& cs, hipStream_t st) {
     if (mode == 2) RSM_BS_LAUNCH(10, 1);
     else if (mode == 4) RSM_BS_LAUNCH(12, 1);
     else if (mode == 0) RSM_BS_LAUNCH(0, 1);  // A/B: per-lane-address exchange writes
+    else if (mode == 24) RSM_BS_LAUNCH(24, 1);
+    else if (mode == 40) RSM_BS_LAUNCH(40, 1);
+    else if (mode == 56) RSM_BS_LAUNCH(56, 1);
     else if (row) RSM_BS_LAUNCH(8, 0);
     else RSM_BS_LAUNCH(8, 1);
 #undef RSM_BS_LAUNCH

@@ -541,6 +541,29 @@ int rsm_dev_fill_random(rsm_ctx* ctx, void* d, uint64_t bytes, uint64_t seed) {
     return e == hipSuccess ? RSM_OK : hip_fail(e, "fill_random");
 }
 
+int rsm_stream_create(rsm_ctx* ctx, void** out) {
+    if (!ctx || !out) return fail(RSM_EINVAL, "rsm_stream_create: bad arguments");
+    *out = nullptr;
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    hipStream_t st = nullptr;
+    if ((e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking)) != hipSuccess) return hip_fail(e, "hipStreamCreate");
+    *out = static_cast<void*>(st);
+    return RSM_OK;
+}
+
+int rsm_stream_destroy(rsm_ctx* ctx, void* stream) {
+    if (!ctx || !stream) return fail(RSM_EINVAL, "rsm_stream_destroy: bad arguments");
+    hipError_t e = hipStreamDestroy(static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? RSM_OK : hip_fail(e, "hipStreamDestroy");
+}
+
+int rsm_stream_sync(void* stream) {
+    if (!stream) return fail(RSM_EINVAL, "rsm_stream_sync: NULL stream");
+    hipError_t e = hipStreamSynchronize(static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? RSM_OK : hip_fail(e, "hipStreamSynchronize");
+}
+
 int rsm_sync(rsm_ctx* ctx) {
     if (!ctx) return fail(RSM_EINVAL, "rsm_sync: NULL ctx");
     hipError_t e = hipStreamSynchronize(ctx->stream);
