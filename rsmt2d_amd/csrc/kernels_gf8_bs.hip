@@ -217,8 +217,8 @@ __device__ __forceinline__ void issue_direct_rt(const CodewordSet& cs, const Set
     });
 }
 
-// MODE bits: 8 = exchange writes by ds_write_addtid_b32 (production: 8);
-// 16 = non-temporal stores, 32 = non-temporal loads (A/B);
+// MODE bits: 8 = exchange writes by ds_write_addtid_b32, 32 = non-temporal loads
+// (production: 40), 16 = non-temporal stores (A/B);
 // diagnostics: 2 = no arithmetic, 4 = no global memory.
 // REV: sets are taken in reverse order (the column pass walks the squares the row
 // pass just wrote from the most recent one back, so the first squares it reads are
@@ -355,12 +355,14 @@ hipError_t launch_encode_gf8_bs128(const CodewordSet& cs, hipStream_t st) {
     const uint64_t sets = ((uint64_t)cs.count * cs.S + kSetBytes - 1) / kSetBytes;
     if (sets == 0) return hipSuccess;
     const uint32_t grid = (uint32_t)(sets < device_cus() ? sets : device_cus());
-    // RSM_BS_MODE: 8 production; 0 = ds_write_b32 exchange (A/B); diagnostics 2 = no
-    // arithmetic, 4 = no global memory (wrong output)
+    // RSM_BS_MODE: 40 production (addtid exchange + non-temporal loads: measured best,
+    // profiles/r01e_bench_ab.txt); A/B: 0 ds_write_b32 exchange, 8 default-policy
+    // loads, 24 nt stores, 56 nt loads + stores; diagnostics 2 = no arithmetic, 4 = no
+    // global memory (wrong output)
     // RSM_BS_REV=0: column pass in forward set order (A/B of the cache-reuse order)
     static const int mode = [] {
         const char* v = getenv("RSM_BS_MODE");
-        return v ? atoi(v) : 8;
+        return v ? atoi(v) : 40;
     }();
     static const uint32_t rev_col = [] {
         const char* v = getenv("RSM_BS_REV");
@@ -370,14 +372,17 @@ hipError_t launch_encode_gf8_bs128(const CodewordSet& cs, hipStream_t st) {
     const uint32_t rev = row ? 0u : rev_col;
 #define RSM_BS_LAUNCH(m, p) \
     hipLaunchKernelGGL((encode_gf8_bs128u_kernel<m, p>), dim3(grid), dim3(512), 0, st, cs, (uint32_t)sets, rev)
-    if (mode == 2) RSM_BS_LAUNCH(10, 1);
-    else if (mode == 4) RSM_BS_LAUNCH(12, 1);
-    else if (mode == 0) RSM_BS_LAUNCH(0, 1);  // A/B: per-lane-address exchange writes
-    else if (mode == 24) RSM_BS_LAUNCH(24, 1);
-    else if (mode == 40) RSM_BS_LAUNCH(40, 1);
-    else if (mode == 56) RSM_BS_LAUNCH(56, 1);
-    else if (row) RSM_BS_LAUNCH(8, 0);
-    else RSM_BS_LAUNCH(8, 1);
+    switch (mode) {
+        case 2: RSM_BS_LAUNCH(10, 1); break;  // diagnostics (wrong output)
+        case 4: RSM_BS_LAUNCH(12, 1); break;
+        case 0: RSM_BS_LAUNCH(0, 1); break;   // A/B variants
+        case 8: RSM_BS_LAUNCH(8, 1); break;
+        case 24: RSM_BS_LAUNCH(24, 1); break;
+        case 56: RSM_BS_LAUNCH(56, 1); break;
+        default:
+            if (row) RSM_BS_LAUNCH(40, 0);
+            else RSM_BS_LAUNCH(40, 1);
+    }
 #undef RSM_BS_LAUNCH
     return hipGetLastError();
 }
