@@ -361,13 +361,16 @@ def main():
     # per-kernel durations: HIP events on the launch stream (the context stream)
     import ctypes
     row_ms, col_ms, step_ms = ctypes.c_float(), ctypes.c_float(), ctypes.c_float()
-    rms, cms = [], []
-    for r in range(max(6, min(a.steps, 20))):  # one row + one column launch per call, batches alternating
+    rms, cms, sms = [], [], []
+    for r in range(max(6, min(a.steps, 20))):  # row, column, then one production step per call
         R._check(L.rsm_time_extend(ctx, bufs[r & 1].ptr, k, S, B, 1, ctypes.byref(row_ms), ctypes.byref(col_ms),
                                    ctypes.byref(step_ms)))
         rms.append(row_ms.value)
         cms.append(col_ms.value)
+        sms.append(step_ms.value)
     t_row, t_col = sum(rms) / len(rms) / 1e3, sum(cms) / len(cms) / 1e3
+    t_fused = sum(sms) / len(sms) / 1e3
+    fused = bool(L.rsm_extend_fused(k, S))
 
     ods_bytes = k * k * S
     total = world * B * a.steps * ods_bytes
@@ -381,6 +384,11 @@ def main():
              else "enc16_a/b/c (GF(2^16) passes)")
     col_dom = t_col >= t_row
     dominant = ((kname + " column pass", col_bytes, t_col) if col_dom else (kname + " row pass", row_bytes, t_row))
+    if fused:
+        # production k = 128 path: ONE launch per step runs both passes
+        # (encode_gf8_bs128f_kernel); its algorithmic bytes are the step's 4k^2 S
+        kname = "encode_gf8_bs128f_kernel"
+        dominant = (kname + " (fused row + column passes)", algo_step, t_fused)
     ach = dominant[1] / dominant[2] / 1e9
     # HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC
     # passes (scripts/pmc_summary.py; FETCH_SIZE x2 gfx950 correction), matched by
@@ -392,6 +400,8 @@ def main():
         # production template <MODE 40, PASS>; A/B modes (RSM_BS_MODE) launch PASS 1
         want = "encode_gf8_bs128u_kernel<%s, %d>" % (os.environ.get("RSM_BS_MODE", "40"), 1 if col_dom else 0)
         sets = (W if col_dom else k) * B * S // 2048
+        if fused:
+            want, sets = "encode_gf8_bs128f_kernel<40>", 3 * k * B * S // 2048
         grid_threads = min(sets, 256) * 512  # persistent grid: one 512-thread workgroup per CU
         for row in json.load(open(pmc_path)).get("launches", []):
             if want in row["kernel"] and row["grid_threads"] == grid_threads:
@@ -419,7 +429,8 @@ def main():
         "step_roofline": {"algorithmic_bytes": algo_step,
                           "achieved": round(algo_step / (elapsed / a.steps) / 1e9, 1),
                           "frac": round(algo_step / (elapsed / a.steps) / 1e9 / HBM_PEAK_GBS, 4),
-                          "row_pass_us": round(t_row * 1e6, 2), "col_pass_us": round(t_col * 1e6, 2)},
+                          "row_pass_us": round(t_row * 1e6, 2), "col_pass_us": round(t_col * 1e6, 2),
+                          "one_step_launch_us": round(t_fused * 1e6, 2), "fused": fused},
     }
     if rank == 0 and world == 1:
         # PCIe-inclusive host-memory rate (ComputeExtendedDataSquare from host buffers)

@@ -132,11 +132,24 @@ int rsm_sync(rsm_ctx* ctx);
  * batches (e.g. step n's column pass beside step n+1's row pass on another
  * stream).  GF(2^16) encodes share the context's work arrays: keep them on one
  * stream. */
+/* 1 when rsm_extend_squares_dev runs both passes of a (k, share_size) square
+ * as ONE launch (GF(2^8), k = 128, fused form enabled), else 0. */
+int rsm_extend_fused(uint32_t k, uint32_t share_size);
+/* Enable (1) or disable (0) the fused single-launch extension process-wide
+ * (default: off, or RSM_FUSED=1); returns the previous setting. */
+int rsm_set_fused(int on);
+/* Debug: with RSM_FUSED_TRACE set, the last fused launch on the ctx stream records
+ * per item (queue order) workgroup << 8 | iteration << 2 | path (1 first item,
+ * 2 prefetched, 3 loaded synchronously); copies min(n, items) words and the
+ * stuck-wait flag.  Returns the number of words copied or a negative code. */
+int rsm_fused_trace(rsm_ctx* ctx, uint32_t* out, uint32_t n, uint32_t* err);
 int rsm_stream_create(rsm_ctx* ctx, void** out);
 int rsm_stream_destroy(rsm_ctx* ctx, void* stream);
 int rsm_stream_sync(void* stream);
 /* Event-timed extension of `count` in-place squares on the ctx stream, averaged
- * over `reps`: row pass, column pass and their sum, in milliseconds. */
+ * over `reps`: row pass and column pass as separate launches, and `step` = one
+ * extension in the production form (the single fused launch where
+ * rsm_extend_fused() says so, else the two launches), in milliseconds. */
 int rsm_time_extend(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size, uint32_t count,
                     uint32_t reps, float* row_ms, float* col_ms, float* step_ms);
 

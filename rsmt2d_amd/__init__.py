@@ -127,6 +127,9 @@ SIGNATURES = {
     "rsm_memcpy": (_I32, [_VP, _VP, _VP, _U64, _I32]),
     "rsm_dev_fill_random": (_I32, [_VP, _VP, _U64, _U64]),
     "rsm_sync": (_I32, [_VP]),
+    "rsm_extend_fused": (_I32, [_U32, _U32]),
+    "rsm_set_fused": (_I32, [ctypes.c_int]),
+    "rsm_fused_trace": (_I32, [_VP, ctypes.POINTER(ctypes.c_uint32), _U32, ctypes.POINTER(ctypes.c_uint32)]),
     "rsm_stream_create": (_I32, [_VP, ctypes.POINTER(_VP)]),
     "rsm_stream_destroy": (_I32, [_VP, _VP]),
     "rsm_stream_sync": (_I32, [_VP]),

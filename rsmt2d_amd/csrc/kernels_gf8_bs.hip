@@ -326,6 +326,245 @@ __global__ __launch_bounds__(512, 1) void encode_gf8_bs128u_kernel(CodewordSet c
     bs_uni_wave<MODE>(cs, sets, rev, (uint32_t)(uintptr_t)lds, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
 }
 
+
+// ---------------------------------------------------------------------------
+// Fused two-pass extension (FusedPlan, rsm_kernels.hpp).  Items are handed out by
+// one device-scope queue head in this order: the row sets of squares 0..lag-1,
+// then per square s: the row sets of s + lag followed by the column sets of s,
+// then the remaining column sets.  A column set of square s needs all rn row sets
+// of s (its Q1 inputs).  Deadlock freedom: a workgroup waits only for items that
+// precede its own in queue order and only while it holds no unfinished item, so
+// the earliest unfinished item always progresses, whatever the residency.
+// Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility): producers store
+// `sc1`, every wave waits for its stores, a barrier, then ONE lane adds to the
+// square's counter (agent scope); the consumer polls with an `sc1` load, takes an
+// agent acquire, and every wave loads after a barrier that follows it.  Waits are
+// bounded: a stuck counter sets ctr[2] and lets the launch drain (wrong output,
+// never a hung GPU).
+__device__ __forceinline__ void fused_item(const FusedPlan& p, uint32_t u, uint32_t& row, uint32_t& set,
+                                           uint32_t& sq) {
+    const uint32_t pro = p.lag * p.rn, blk = p.rn + p.cn, mid = (p.count - p.lag) * blk;
+    if (u < pro) {
+        row = 1u; set = u; sq = u / p.rn;
+    } else if (u - pro < mid) {
+        const uint32_t v = u - pro, b = v / blk, o = v - b * blk;
+        if (o < p.rn) { row = 1u; sq = p.lag + b; set = sq * p.rn + o; }
+        else { row = 0u; sq = b; set = b * p.cn + (o - p.rn); }
+    } else {
+        row = 0u; set = (p.count - p.lag) * p.cn + (u - pro - mid); sq = set / p.cn;
+    }
+}
+
+constexpr uint32_t kSpinLimit = 1u << 20;  // polls (~1 s) before a wait is declared stuck
+
+template <int MODE>
+__device__ __forceinline__ void bs_fused_wave(const FusedPlan& p, uint32_t* lds, uint32_t lds_base, uint32_t A) {
+    constexpr bool ADDTID = (MODE & 8) != 0, NTL = (MODE & 32) != 0;
+    const uint32_t lane = threadIdx.x & 63u;
+    const bool t0 = threadIdx.x == 0;
+    const uint32_t dread = lds_base + kXchBytes + A * 16384u + lane * 16u;
+    const uint32_t s_small = __builtin_amdgcn_readfirstlane(lds_base + 4096u * A);
+    const uint32_t s_large = __builtin_amdgcn_readfirstlane(lds_base + 256u * A);
+    const uint32_t e_small = s_small + lane * 4u, e_large = s_large + lane * 4u;
+    uint32_t* const ctr = p.ctr;
+    uint32_t X[16][8];
+    uint32_t P[16 - kPre][8];
+
+    auto dequeue = [&]() { return __hip_atomic_fetch_add(&ctr[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    auto poll = [&](uint32_t sq) { return __hip_atomic_load(&ctr[3 + sq], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    auto signal = [&](uint32_t sq) {
+        __hip_atomic_fetch_add(&ctr[3 + sq], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    // thread 0: wait until square sq's row sets are all stored, then acquire
+    auto wait_rows = [&](uint32_t sq) {
+        for (uint32_t n = 0; poll(sq) < p.rn; ++n) {
+            if (n >= kSpinLimit) {
+                __hip_atomic_store(&ctr[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(4);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    };
+    // row sets read Q0 with the default policy (it stays in the Infinity Cache for
+    // the column sets); column sets read once, non-temporal (MODE 32)
+    auto issue = [&](uint32_t row, const SetAddr& a) {
+        if (row) {
+            issue_dma_rt<false>(p.rows, a, lds_base, A);
+            issue_direct_rt<false>(p.rows, a, A, P);
+        } else {
+            issue_dma_rt<NTL>(p.cols, a, lds_base, A);
+            issue_direct_rt<NTL>(p.cols, a, A, P);
+        }
+    };
+    auto addr = [&](uint32_t row, uint32_t set) { return set_addr(row ? p.rows : p.cols, set, lane); };
+
+    // prologue: first two items, first one loaded synchronously
+    if (t0) {
+        const uint32_t c = dequeue(), n = dequeue();
+        lds[0] = c;
+        lds[1] = n;
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    uint32_t cur = __builtin_amdgcn_readfirstlane(lds[0]);
+    uint32_t nxt = __builtin_amdgcn_readfirstlane(lds[1]);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    uint32_t crow = 0, cset = 0, csq = 0;
+    uint32_t pend = 0xFFFFFFFFu;  // square of a stored-but-unsignalled row set
+    if (cur < p.total) {
+        fused_item(p, cur, crow, cset, csq);
+        if (!crow && t0) wait_rows(csq);
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        issue(crow, addr(crow, cset));
+        if (t0) {
+            uint32_t r = 1u, nr = 0, ns = 0, nq = 0;
+            if (nxt < p.total) {
+                fused_item(p, nxt, nr, ns, nq);
+                if (!nr) {
+                    r = poll(nq) >= p.rn;
+                    if (r) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                }
+            }
+            lds[0] = nxt;
+            lds[2] = r;
+        }
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    uint32_t path = 1u, iter = 0u;
+    for (; cur < p.total;) {
+        if (p.trace && t0) p.trace[cur] = (blockIdx.x << 8) | ((iter & 63u) << 2) | path;
+        {
+            v4u g[8];
+            bs8::sfor<2>([&](auto Hh) {
+                constexpr int hh = decltype(Hh)::value;
+                ds_r16x8<8192 * hh, 1024>(dread, g);
+                bs8::sfor<4>([&](auto J) {
+                    constexpr int j = 4 * hh + decltype(J)::value;
+                    const v4u x = g[2 * (j & 3)], y = g[2 * (j & 3) + 1];
+                    X[j][0] = x.x; X[j][1] = x.y; X[j][2] = x.z; X[j][3] = x.w;
+                    X[j][4] = y.x; X[j][5] = y.y; X[j][6] = y.z; X[j][7] = y.w;
+                });
+            });
+        }
+        bs8::sfor<16 - kPre>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            bs8::sfor<8>([&](auto I) { X[kPre + j][decltype(I)::value] = P[j][decltype(I)::value]; });
+        });
+        // the slot (E words 0..2) holds the next item and its readiness; everyone reads
+        // it before the first exchange overwrites E
+        nxt = __builtin_amdgcn_readfirstlane(lds[0]);
+        const uint32_t rdy = __builtin_amdgcn_readfirstlane(lds[2]);
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        const bool more = nxt < p.total;
+        uint32_t nrow = 0, nset = 0, nsq = 0;
+        if (more) fused_item(p, nxt, nrow, nset, nsq);
+        const bool pre = more && rdy && !(p.flags & 1u);
+        if (pre) issue(nrow, addr(nrow, nset));
+        uint32_t nn = 0;
+        if (t0) nn = dequeue();
+
+        bs8::sfor<16>([&](auto J) { bs8::transpose8_dev(X[decltype(J)::value]); });
+        bs8::small_ifft_all(X, A);
+        bs8::sfor<8>([&](auto Pp) { xch_to_large<decltype(Pp)::value, ADDTID>(X, e_small, s_small, e_large); });
+        bs8::large_ifft_fft(X);
+        bs8::sfor<8>([&](auto Pp) { xch_to_small<decltype(Pp)::value, ADDTID>(X, e_large, s_large, e_small); });
+
+        // the dequeued id is first touched here: keep the compiler from hoisting its use
+        // (and the vmcnt(0) wait for it, which would drain this wave's prefetch loads)
+        // to the top of the set
+        asm volatile("" : "+v"(nn));
+        // thread 0: readiness of the item after next (poll now, read after the FFT)
+        uint32_t pv = 0, nnr = 1, nnq = 0;
+        if (t0 && nn < p.total) {
+            uint32_t ns2 = 0;
+            fused_item(p, nn, nnr, ns2, nnq);
+            if (!nnr) pv = poll(nnq);
+        }
+        bs8::small_fft_all(X, A);
+
+        // signal the previous row set (its stores were issued one set ago)
+        if (pend != 0xFFFFFFFFu) {
+            if (pre) asm volatile("s_waitcnt vmcnt(32)\n\ts_barrier" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+            if (t0) signal(pend);
+            pend = 0xFFFFFFFFu;
+        }
+        if (t0) {
+            uint32_t r = 1u;
+            if (nn < p.total && !nnr) {
+                r = pv >= p.rn;
+                if (r) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            }
+            lds[0] = nn;
+            lds[2] = r;
+        }
+        {
+            const SetAddr a = addr(crow, cset);
+            const __amdgpu_buffer_rsrc_t ro = as_rsrc(a.ro);
+            const uint32_t k = p.rows.k;
+            const uint32_t oo = (uint32_t)(crow ? p.rows.out_offset : p.cols.out_offset);
+            const uint32_t es = (uint32_t)(crow ? p.rows.elem_stride : p.cols.elem_stride);
+            bs8::sfor<16>([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                bs8::transpose8_dev(X[j]);
+                const uint32_t so = sym_off(16u * A + j, k, oo, es);
+                v4u x, y;
+                x.x = X[j][0]; x.y = X[j][1]; x.z = X[j][2]; x.w = X[j][3];
+                y.x = X[j][4]; y.y = X[j][5]; y.z = X[j][6]; y.w = X[j][7];
+                __builtin_amdgcn_raw_buffer_store_b128(x, ro, a.off[0], so, 16);  // sc1
+                __builtin_amdgcn_raw_buffer_store_b128(y, ro, a.off[1], so, 16);
+                asm volatile("s_nop 2" ::: "memory");  // store-data hazard, see bs_uni_wave
+            });
+        }
+        if (crow) pend = csq;
+        if (!more) break;
+        if (!pre) {
+            // slow path: publish our own row set first (the next item may need it),
+            // then wait for the next item's rows and load it synchronously
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            if (t0) {
+                if (pend != 0xFFFFFFFFu) signal(pend);
+                if (!nrow) wait_rows(nsq);
+            }
+            pend = 0xFFFFFFFFu;
+            asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+            issue(nrow, addr(nrow, nset));
+            __builtin_amdgcn_s_waitcnt(0x0F70);
+            asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+            path = 3u;
+        } else {
+            asm volatile("s_waitcnt vmcnt(32) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            path = 2u;
+        }
+        ++iter;
+        cur = nxt;
+        crow = nrow;
+        cset = nset;
+        csq = nsq;
+    }
+    // drain: every wave's stores, then the last row set's signal and the exit count;
+    // the last workgroup out re-zeroes the queue for the next launch on this buffer
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (t0) {
+        if (pend != 0xFFFFFFFFu) signal(pend);
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        const uint32_t done = __hip_atomic_fetch_add(&ctr[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (done == gridDim.x - 1u) {
+            __hip_atomic_store(&ctr[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (uint32_t s = 0; s < p.count; ++s)
+                __hip_atomic_store(&ctr[3 + s], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&ctr[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(512, 1) void encode_gf8_bs128f_kernel(FusedPlan p) {
+    __shared__ uint32_t lds[(kDmaBytes + kXchBytes) / 4];
+    bs_fused_wave<MODE>(p, lds, (uint32_t)(uintptr_t)lds, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
+}
+
 }  // namespace
 
 
@@ -384,6 +623,20 @@ hipError_t launch_encode_gf8_bs128(const CodewordSet& cs, hipStream_t st) {
             else RSM_BS_LAUNCH(40, 1);
     }
 #undef RSM_BS_LAUNCH
+    return hipGetLastError();
+}
+
+// The fused launch needs whole sets per square in both passes (k * S a multiple of
+// 2 KiB: every k = 128 square) and the plain row/column CodewordSets to qualify.
+bool bs128_fused_applicable(const CodewordSet& rows, const CodewordSet& cols) {
+    if (rows.k != 128 || ((uint64_t)rows.k * rows.S) % kSetBytes != 0) return false;
+    return bs128_applicable(rows) && bs128_applicable(cols);
+}
+
+hipError_t launch_extend_gf8_bs128_fused(const FusedPlan& p, hipStream_t st) {
+    if (p.total == 0) return hipSuccess;
+    const uint32_t grid = p.total < device_cus() ? p.total : device_cus();
+    hipLaunchKernelGGL((encode_gf8_bs128f_kernel<40>), dim3(grid), dim3(512), 0, st, p);
     return hipGetLastError();
 }
 

@@ -49,6 +49,11 @@ struct rsm_ctx {
     std::mutex gf16_mu;  // guards gf16 table upload / scratch growth
     std::map<int, std::unique_ptr<rsm::DevBuf>> bufs;
     std::map<int, std::unique_ptr<rsm::HostBuf>> hbufs;
+    // queue/counter words of the fused extension kernel, one buffer per stream (two
+    // launches in flight on different streams must not share a queue)
+    std::mutex fused_mu;
+    std::map<void*, std::unique_ptr<rsm::DevBuf>> fused_ctr;
+    uint32_t fused_trace_n = 0;  // items of the last traced fused launch (RSM_FUSED_TRACE)
     uint32_t* d_zero_index = nullptr;
     rsm::Gf16Dev gf16{};
     bool gf16_ready = false;

@@ -46,7 +46,27 @@ struct DecodeSet {
     uint32_t chunks;
 };
 
+// One launch that runs both passes of the 2D extension over `count` squares
+// (kernels_gf8_bs.hip, encode_gf8_bs128f_kernel): the row sets of square s and
+// the column sets of square s - lag are handed out from one device-wide queue,
+// and a column set waits for its square's row sets (per-square counters), so the
+// column pass re-reads Q0 and Q1 while they are still in the Infinity Cache.
+struct FusedPlan {
+    CodewordSet rows, cols;
+    uint32_t* ctr;   // [0] queue head, [1] exit count, [2] error flag, [3 + s] row sets done of square s
+    uint32_t count;  // squares
+    uint32_t lag;    // squares the column sets trail the row sets by (1 <= lag <= count)
+    uint32_t rn, cn; // sets per square: row pass, column pass
+    uint32_t total;  // count * (rn + cn)
+    uint32_t flags;  // debug: 1 = never prefetch (every item takes the synchronous path)
+    uint32_t* trace; // debug (nullable): trace[item] = workgroup << 8 | iteration << 2 | path
+};
+
 hipError_t launch_encode_gf8(const CodewordSet& cs, hipStream_t st);
+// fused two-pass M = 128 extension; ctr must hold count + 3 zeroed words (the
+// kernel leaves them zeroed again, except the error flag)
+bool bs128_fused_applicable(const CodewordSet& rows, const CodewordSet& cols);
+hipError_t launch_extend_gf8_bs128_fused(const FusedPlan& p, hipStream_t st);
 // bit-sliced M = 128 encode (kernels_gf8_bs.hip); launch_encode_gf8 picks it when applicable
 bool bs128_applicable(const CodewordSet& cs);
 hipError_t launch_encode_gf8_bs128(const CodewordSet& cs, hipStream_t st);

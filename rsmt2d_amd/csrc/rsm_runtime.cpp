@@ -3,6 +3,7 @@
 // The HIP kernels are the only compute path: every entry point that needs
 // arithmetic fails with RSM_EDEVICE when no GPU/HIP runtime is usable; there is
 // no CPU fallback anywhere in the product.
+#include <atomic>
 #include "rsm_internal.hpp"
 
 #include <cstdio>
@@ -156,6 +157,65 @@ int launch_decode(rsm_ctx* ctx, const DecodeSet& ds0, hipStream_t st) {
     return RSM_OK;
 }
 
+// The fused launch is opt-in (RSM_FUSED=1 or rsm_set_fused): measured no faster
+// than the two launches; RSM_FUSED_LAG sets FusedPlan::lag.
+std::atomic<int> g_fused{-1};
+bool fused_enabled() {
+    int v = g_fused.load(std::memory_order_relaxed);
+    if (v < 0) {
+        const char* e = getenv("RSM_FUSED");
+        v = (e != nullptr && atoi(e) != 0) ? 1 : 0;
+        g_fused.store(v, std::memory_order_relaxed);
+    }
+    return v != 0;
+}
+
+// Both passes in one launch (FusedPlan): the queue words live in a per-stream
+// buffer that the kernel leaves zeroed; a new or grown buffer is zeroed in stream
+// order before its first launch.
+int extend_fused(rsm_ctx* ctx, const CodewordSet& rows, const CodewordSet& cols, uint32_t count, hipStream_t st) {
+    static const uint32_t lag_env = [] {
+        const char* v = getenv("RSM_FUSED_LAG");
+        return v ? (uint32_t)atoi(v) : 4u;
+    }();
+    FusedPlan p{};
+    p.rows = rows;
+    p.cols = cols;
+    p.count = count;
+    p.lag = lag_env < 1 ? 1 : (lag_env > count ? count : lag_env);
+    p.rn = (uint32_t)((uint64_t)rows.k * rows.S / 2048);
+    p.cn = 2 * p.rn;
+    p.total = count * (p.rn + p.cn);
+    static const uint32_t flags_env = [] {
+        const char* v = getenv("RSM_FUSED_FLAGS");
+        return v ? (uint32_t)atoi(v) : 0u;
+    }();
+    p.flags = flags_env;
+    if (getenv("RSM_FUSED_TRACE")) {
+        DevBuf& tb = ctx->dev_buf(41);
+        if (tb.ensure((size_t)p.total * 4) != hipSuccess) return fail(RSM_EDEVICE, "fused trace buffer");
+        (void)hipMemsetAsync(tb.ptr, 0xFF, (size_t)p.total * 4, st);
+        p.trace = static_cast<uint32_t*>(tb.ptr);
+        ctx->fused_trace_n = p.total;
+    }
+    const size_t words = (size_t)count + 3;
+    {
+        std::lock_guard<std::mutex> g(ctx->fused_mu);
+        auto& b = ctx->fused_ctr[(void*)st];
+        if (!b) b = std::make_unique<DevBuf>();
+        if (b->cap < words * 4) {
+            hipError_t e = hipStreamSynchronize(st);  // an older, smaller buffer may still be in use
+            if (e == hipSuccess) e = b->ensure(((words * 4 + 4095) / 4096) * 4096);
+            if (e == hipSuccess) e = hipMemsetAsync(b->ptr, 0, b->cap, st);
+            if (e != hipSuccess) return hip_fail(e, "fused extension: queue buffer");
+        }
+        p.ctr = static_cast<uint32_t*>(b->ptr);
+    }
+    hipError_t e = launch_extend_gf8_bs128_fused(p, st);
+    if (e != hipSuccess) return hip_fail(e, "fused extension kernel launch");
+    return RSM_OK;
+}
+
 // Two-phase in-place extension of `count` squares (extendeddatasquare.go:154-227):
 //   phase 1: every row r < k: Q0 row -> Q1 row            (erasureExtendRow)
 //   phase 2: every column c < 2k: [Q0|Q1] column -> [Q2|Q3] column
@@ -176,6 +236,17 @@ int extend_squares(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, uint32_
     rows.count = k * count;
     rows.k = k;
     rows.S = S;
+    if (phases == 3 && fused_enabled() && field_bits(k) == 8) {
+        CodewordSet cols = rows;
+        cols.cw_stride = S;
+        cols.elem_stride = W * S;
+        cols.out_offset = (uint64_t)k * W * S;
+        cols.per_square = (uint32_t)W;
+        cols.count = (uint32_t)W * count;
+        rows.out_base = rows.base;
+        cols.out_base = cols.base;
+        if (bs128_fused_applicable(rows, cols)) return extend_fused(ctx, rows, cols, count, st);
+    }
     if (phases & 1) {
         int rc = launch_encode(ctx, rows, st);
         if (rc) return rc;
@@ -570,6 +641,33 @@ int rsm_sync(rsm_ctx* ctx) {
     return e == hipSuccess ? RSM_OK : hip_fail(e, "hipStreamSynchronize");
 }
 
+int rsm_fused_trace(rsm_ctx* ctx, uint32_t* out, uint32_t n, uint32_t* err) {
+    if (!ctx || !out) return fail(RSM_EINVAL, "rsm_fused_trace: bad arguments");
+    if (hipStreamSynchronize(ctx->stream) != hipSuccess) return fail(RSM_EDEVICE, "hipStreamSynchronize");
+    const uint32_t m = n < ctx->fused_trace_n ? n : ctx->fused_trace_n;
+    if (m && hipMemcpy(out, ctx->dev_buf(41).ptr, (size_t)m * 4, hipMemcpyDeviceToHost) != hipSuccess)
+        return fail(RSM_EDEVICE, "rsm_fused_trace: copy");
+    if (err) {
+        *err = 0;
+        auto it = ctx->fused_ctr.find((void*)ctx->stream);
+        if (it != ctx->fused_ctr.end() && it->second->ptr &&
+            hipMemcpy(err, static_cast<uint32_t*>(it->second->ptr) + 2, 4, hipMemcpyDeviceToHost) != hipSuccess)
+            return fail(RSM_EDEVICE, "rsm_fused_trace: error flag");
+    }
+    return (int)m;
+}
+
+int rsm_set_fused(int on) {
+    const int prev = fused_enabled() ? 1 : 0;
+    g_fused.store(on ? 1 : 0, std::memory_order_relaxed);
+    return prev;
+}
+
+int rsm_extend_fused(uint32_t k, uint32_t share_size) {
+    if (!fused_enabled() || k != 128 || validate_chunk_size(share_size) != RSM_OK) return 0;
+    return ((uint64_t)k * share_size) % 2048 == 0 ? 1 : 0;
+}
+
 int rsm_time_extend(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size, uint32_t count, uint32_t reps,
                     float* row_ms, float* col_ms, float* step_ms) {
     if (!ctx || !d_eds || reps == 0) return fail(RSM_EINVAL, "rsm_time_extend: bad arguments");
@@ -585,12 +683,20 @@ int rsm_time_extend(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size, 
         if (rc == RSM_OK) rc = extend_squares(ctx, static_cast<uint8_t*>(d_eds), k, share_size, count, ctx->stream, 2);
         (void)hipEventRecord(ev[2], ctx->stream);
         if (hipEventSynchronize(ev[2]) != hipSuccess) rc = fail(RSM_EDEVICE, "hipEventSynchronize");
-        float a = 0, b = 0;
+        float a = 0, b = 0, c = 0;
         (void)hipEventElapsedTime(&a, ev[0], ev[1]);
         (void)hipEventElapsedTime(&b, ev[1], ev[2]);
+        // step: the production form (one fused launch where it applies)
+        if (rc == RSM_OK) {
+            (void)hipEventRecord(ev[0], ctx->stream);
+            rc = extend_squares(ctx, static_cast<uint8_t*>(d_eds), k, share_size, count, ctx->stream, 3);
+            (void)hipEventRecord(ev[1], ctx->stream);
+            if (hipEventSynchronize(ev[1]) != hipSuccess) rc = fail(RSM_EDEVICE, "hipEventSynchronize");
+            (void)hipEventElapsedTime(&c, ev[0], ev[1]);
+        }
         acc[0] += a;
         acc[1] += b;
-        acc[2] += a + b;
+        acc[2] += c;
     }
     for (auto& x : ev) (void)hipEventDestroy(x);
     if (rc) return rc;
