@@ -239,7 +239,16 @@ __device__ __forceinline__ void bs_uni_wave(const CodewordSet& cs, uint32_t sets
     uint32_t X[16][8];
     uint32_t P[16 - kPre][8];
 
-    auto addr = [&](uint32_t tt) { return set_addr(cs, rev ? sets - 1u - tt : tt, lane); };
+    // rev bit 1: XCD-grouped order -- within every full group of G sets, block b
+    // (XCD b % 8 under round-robin placement) takes set (b % 8) * G/8 + b / 8, so the
+    // blocks of one XCD stream adjacent strips (speed only: any bijection is correct)
+    auto addr = [&](uint32_t tt) {
+        if ((rev & 2u) && (G & 7u) == 0 && (tt / G + 1u) * G <= sets) {
+            const uint32_t b = tt % G;
+            tt = tt - b + (b & 7u) * (G >> 3) + (b >> 3);
+        }
+        return set_addr(cs, (rev & 1u) ? sets - 1u - tt : tt, lane);
+    };
     uint32_t t = blockIdx.x;
     SetAddr a = addr(t);
     if (MEM) {
@@ -608,7 +617,12 @@ hipError_t launch_encode_gf8_bs128(const CodewordSet& cs, hipStream_t st) {
         return v ? (uint32_t)(atoi(v) != 0) : 1u;
     }();
     const bool row = cs.elem_stride == cs.S;
-    const uint32_t rev = row ? 0u : rev_col;
+    // RSM_BS_XCD=1: XCD-grouped set order (A/B)
+    static const uint32_t xcd = [] {
+        const char* v = getenv("RSM_BS_XCD");
+        return v ? (uint32_t)(atoi(v) & 3) : 0u;
+    }();
+    const uint32_t rev = (row ? 0u : rev_col) | (((xcd >> (row ? 0 : 1)) & 1u) << 1);
 #define RSM_BS_LAUNCH(m, p) \
     hipLaunchKernelGGL((encode_gf8_bs128u_kernel<m, p>), dim3(grid), dim3(512), 0, st, cs, (uint32_t)sets, rev)
     switch (mode) {
