@@ -132,6 +132,13 @@ int rsm_sync(rsm_ctx* ctx);
  * batches (e.g. step n's column pass beside step n+1's row pass on another
  * stream).  GF(2^16) encodes share the context's work arrays: keep them on one
  * stream. */
+/* Software-pipelined batches: ONE launch runs the row pass (Q0 -> Q1) of `count`
+ * squares at d_rows_eds AND the column pass ([Q0|Q1] -> [Q2|Q3]) of `count`
+ * squares at d_cols_eds (either may be NULL; the two batches must not overlap).
+ * A batch is fully extended by its row-pass call followed, in stream order, by its
+ * column-pass call -- e.g. call i passes batch i+1's rows and batch i's columns. */
+int rsm_extend_pipeline_dev(rsm_ctx* ctx, void* d_rows_eds, void* d_cols_eds, uint32_t k, uint32_t share_size,
+                            uint32_t count, void* stream);
 /* 1 when rsm_extend_squares_dev runs both passes of a (k, share_size) square
  * as ONE launch (GF(2^8), k = 128, fused form enabled), else 0. */
 int rsm_extend_fused(uint32_t k, uint32_t share_size);

@@ -128,6 +128,7 @@ SIGNATURES = {
     "rsm_dev_fill_random": (_I32, [_VP, _VP, _U64, _U64]),
     "rsm_sync": (_I32, [_VP]),
     "rsm_extend_fused": (_I32, [_U32, _U32]),
+    "rsm_extend_pipeline_dev": (_I32, [_VP, _VP, _VP, _U32, _U32, _U32, _VP]),
     "rsm_set_fused": (_I32, [ctypes.c_int]),
     "rsm_fused_trace": (_I32, [_VP, ctypes.POINTER(ctypes.c_uint32), _U32, ctypes.POINTER(ctypes.c_uint32)]),
     "rsm_stream_create": (_I32, [_VP, ctypes.POINTER(_VP)]),

@@ -196,7 +196,7 @@ __device__ __forceinline__ void issue_dma_rt(const CodewordSet& cs, const SetAdd
     bs8::sfor<kPre>([&](auto J) {
         constexpr int j = decltype(J)::value;
         const uint32_t so = sym_off(16u * A + j, k, 0, es);
-        const uint32_t l = lds_base + kXchBytes + A * (kPre * 2048u) + j * 2048u;
+        const uint32_t l = __builtin_amdgcn_readfirstlane(lds_base + kXchBytes + A * (kPre * 2048u) + j * 2048u);
         dma16<NT>(l, a.off[0], a.rs, so);
         dma16<NT>(l + 1024u, a.off[1], a.rs, so);
     });
@@ -574,6 +574,117 @@ __global__ __launch_bounds__(512, 1) void encode_gf8_bs128f_kernel(FusedPlan p) 
     bs_fused_wave<MODE>(p, lds, (uint32_t)(uintptr_t)lds, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
 }
 
+
+// ---------------------------------------------------------------------------
+// Dual launch (DualPlan): bs_uni_wave's persistent pipeline over the union of two
+// independent set lists.  Set t maps to (list, index); with nb == 2 na every group
+// of three consecutive t is one set of a and two of b.  No cross-workgroup hand-off:
+// the lists touch disjoint squares (the caller orders a batch's column pass after
+// its row pass with the stream).
+__device__ __forceinline__ void dual_item(const DualPlan& p, uint32_t t, uint32_t& isb, uint32_t& idx) {
+    if (p.nb == 2u * p.na) {
+        const uint32_t g = t / 3u, r = t - 3u * g;
+        isb = r != 0u;
+        idx = r == 0u ? g : 2u * g + (r - 1u);
+    } else {
+        isb = t >= p.na;
+        idx = isb ? t - p.na : t;
+    }
+}
+
+template <int MODE>
+__device__ __forceinline__ void bs_dual_wave(const DualPlan& p, uint32_t lds_base, uint32_t A) {
+    constexpr bool ADDTID = (MODE & 8) != 0, NTL = (MODE & 32) != 0;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t G = gridDim.x, sets = p.na + p.nb;
+    const uint32_t dread = lds_base + kXchBytes + A * 16384u + lane * 16u;
+    const uint32_t s_small = __builtin_amdgcn_readfirstlane(lds_base + 4096u * A);
+    const uint32_t s_large = __builtin_amdgcn_readfirstlane(lds_base + 256u * A);
+    const uint32_t e_small = s_small + lane * 4u, e_large = s_large + lane * 4u;
+    uint32_t X[16][8];
+    uint32_t P[16 - kPre][8];
+
+    auto issue = [&](uint32_t isb, const SetAddr& a) {
+        if (isb) {
+            issue_dma_rt<NTL>(p.b, a, lds_base, A);
+            issue_direct_rt<NTL>(p.b, a, A, P);
+        } else {
+            issue_dma_rt<NTL>(p.a, a, lds_base, A);
+            issue_direct_rt<NTL>(p.a, a, A, P);
+        }
+    };
+    auto addr = [&](uint32_t isb, uint32_t idx) { return set_addr(isb ? p.b : p.a, idx, lane); };
+
+    uint32_t t = blockIdx.x;
+    uint32_t cb = 0, ci = 0;
+    dual_item(p, t, cb, ci);
+    issue(cb, addr(cb, ci));
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    asm volatile("s_barrier" ::: "memory");
+    for (;;) {
+        {
+            v4u g[8];
+            bs8::sfor<2>([&](auto Hh) {
+                constexpr int hh = decltype(Hh)::value;
+                ds_r16x8<8192 * hh, 1024>(dread, g);
+                bs8::sfor<4>([&](auto J) {
+                    constexpr int j = 4 * hh + decltype(J)::value;
+                    const v4u x = g[2 * (j & 3)], y = g[2 * (j & 3) + 1];
+                    X[j][0] = x.x; X[j][1] = x.y; X[j][2] = x.z; X[j][3] = x.w;
+                    X[j][4] = y.x; X[j][5] = y.y; X[j][6] = y.z; X[j][7] = y.w;
+                });
+            });
+        }
+        bs8::sfor<16 - kPre>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            bs8::sfor<8>([&](auto I) { X[kPre + j][decltype(I)::value] = P[j][decltype(I)::value]; });
+        });
+        const uint32_t tn = t + G;
+        const bool more = tn < sets;
+        uint32_t nb = 0, ni = 0;
+        if (more) {
+            dual_item(p, tn, nb, ni);
+            issue(nb, addr(nb, ni));
+        }
+        bs8::sfor<16>([&](auto J) { bs8::transpose8_dev(X[decltype(J)::value]); });
+        bs8::small_ifft_all(X, A);
+        bs8::sfor<8>([&](auto Pp) { xch_to_large<decltype(Pp)::value, ADDTID>(X, e_small, s_small, e_large); });
+        bs8::large_ifft_fft(X);
+        bs8::sfor<8>([&](auto Pp) { xch_to_small<decltype(Pp)::value, ADDTID>(X, e_large, s_large, e_small); });
+        bs8::small_fft_all(X, A);
+        {
+            const SetAddr a = addr(cb, ci);
+            const __amdgpu_buffer_rsrc_t ro = as_rsrc(a.ro);
+            const uint32_t k = p.a.k;
+            const uint32_t oo = (uint32_t)(cb ? p.b.out_offset : p.a.out_offset);
+            const uint32_t es = (uint32_t)(cb ? p.b.elem_stride : p.a.elem_stride);
+            bs8::sfor<16>([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                bs8::transpose8_dev(X[j]);
+                const uint32_t so = sym_off(16u * A + j, k, oo, es);
+                v4u x, y;
+                x.x = X[j][0]; x.y = X[j][1]; x.z = X[j][2]; x.w = X[j][3];
+                y.x = X[j][4]; y.y = X[j][5]; y.z = X[j][6]; y.w = X[j][7];
+                __builtin_amdgcn_raw_buffer_store_b128(x, ro, a.off[0], so, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(y, ro, a.off[1], so, 0);
+                asm volatile("s_nop 2" ::: "memory");  // store-data hazard, see bs_uni_wave
+            });
+        }
+        if (!more) break;
+        t = tn;
+        cb = nb;
+        ci = ni;
+        asm volatile("s_waitcnt vmcnt(32)\n\ts_barrier" ::: "memory");
+    }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(512, 1) void encode_gf8_bs128p_kernel(DualPlan p) {
+    __shared__ uint32_t lds[(kDmaBytes + kXchBytes) / 4];
+    if (blockIdx.x >= p.na + p.nb) return;
+    bs_dual_wave<MODE>(p, (uint32_t)(uintptr_t)lds, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
+}
+
 }  // namespace
 
 
@@ -651,6 +762,14 @@ hipError_t launch_extend_gf8_bs128_fused(const FusedPlan& p, hipStream_t st) {
     if (p.total == 0) return hipSuccess;
     const uint32_t grid = p.total < device_cus() ? p.total : device_cus();
     hipLaunchKernelGGL((encode_gf8_bs128f_kernel<40>), dim3(grid), dim3(512), 0, st, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_encode_gf8_bs128_dual(const DualPlan& p, hipStream_t st) {
+    const uint32_t sets = p.na + p.nb;
+    if (sets == 0) return hipSuccess;
+    const uint32_t grid = sets < device_cus() ? sets : device_cus();
+    hipLaunchKernelGGL((encode_gf8_bs128p_kernel<40>), dim3(grid), dim3(512), 0, st, p);
     return hipGetLastError();
 }
 

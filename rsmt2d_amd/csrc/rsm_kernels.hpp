@@ -62,7 +62,17 @@ struct FusedPlan {
     uint32_t* trace; // debug (nullable): trace[item] = workgroup << 8 | iteration << 2 | path
 };
 
+// Two independent codeword batches in one persistent launch (kernels_gf8_bs.hip,
+// encode_gf8_bs128p_kernel): the row pass of one batch of squares and the column
+// pass of another, sets interleaved 1 : 2 when nb == 2 * na so that every CU mixes
+// the compute-heavier row sets with the memory-heavier column sets.
+struct DualPlan {
+    CodewordSet a, b;
+    uint32_t na, nb;  // sets of a, of b
+};
+
 hipError_t launch_encode_gf8(const CodewordSet& cs, hipStream_t st);
+hipError_t launch_encode_gf8_bs128_dual(const DualPlan& p, hipStream_t st);
 // fused two-pass M = 128 extension; ctr must hold count + 3 zeroed words (the
 // kernel leaves them zeroed again, except the error flag)
 bool bs128_fused_applicable(const CodewordSet& rows, const CodewordSet& cols);

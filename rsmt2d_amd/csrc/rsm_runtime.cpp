@@ -657,6 +657,48 @@ int rsm_fused_trace(rsm_ctx* ctx, uint32_t* out, uint32_t n, uint32_t* err) {
     return (int)m;
 }
 
+int rsm_extend_pipeline_dev(rsm_ctx* ctx, void* d_rows_eds, void* d_cols_eds, uint32_t k, uint32_t share_size,
+                            uint32_t count, void* stream) {
+    if (!ctx || k == 0 || (!d_rows_eds && !d_cols_eds)) return fail(RSM_EINVAL, "rsm_extend_pipeline_dev: bad arguments");
+    if (int rc = validate_chunk_size(share_size)) return rc;
+    if (count == 0) return RSM_OK;
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    const uint64_t W = 2ull * k, S = share_size;
+    CodewordSet rows{}, cols{};
+    rows.base = rows.out_base = static_cast<uint8_t*>(d_rows_eds);
+    rows.square_stride = W * W * S;
+    rows.cw_stride = W * S;
+    rows.elem_stride = S;
+    rows.out_offset = (uint64_t)k * S;
+    rows.per_square = k;
+    rows.count = k * count;
+    rows.k = k;
+    rows.S = share_size;
+    cols = rows;
+    cols.base = cols.out_base = static_cast<uint8_t*>(d_cols_eds);
+    cols.cw_stride = S;
+    cols.elem_stride = W * S;
+    cols.out_offset = (uint64_t)k * W * S;
+    cols.per_square = (uint32_t)W;
+    cols.count = (uint32_t)W * count;
+    const bool dual = field_bits(k) == 8 && d_rows_eds && d_cols_eds && bs128_applicable(rows) && bs128_applicable(cols);
+    if (!dual) {  // separate launches (independent batches: order does not matter)
+        if (d_rows_eds)
+            if (int rc = extend_squares(ctx, static_cast<uint8_t*>(d_rows_eds), k, share_size, count, st, 1)) return rc;
+        if (d_cols_eds)
+            if (int rc = extend_squares(ctx, static_cast<uint8_t*>(d_cols_eds), k, share_size, count, st, 2)) return rc;
+        return RSM_OK;
+    }
+    DualPlan p{};
+    p.a = rows;
+    p.b = cols;
+    p.na = (uint32_t)(((uint64_t)rows.count * S + 2047) / 2048);
+    p.nb = (uint32_t)(((uint64_t)cols.count * S + 2047) / 2048);
+    hipError_t e = launch_encode_gf8_bs128_dual(p, st);
+    if (e != hipSuccess) return hip_fail(e, "pipelined extension kernel launch");
+    return RSM_OK;
+}
+
 int rsm_set_fused(int on) {
     const int prev = fused_enabled() ? 1 : 0;
     g_fused.store(on ? 1 : 0, std::memory_order_relaxed);
