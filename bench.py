@@ -51,6 +51,10 @@ def parse():
                    help="initialise torch.distributed even at N=1 (rehearses the sharded c5 path on one GPU)")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--one-stream", action="store_true", help="GF(2^8): do not alternate steps over two streams")
+    p.add_argument("--schedule", choices=["pipelined", "two-launch"], default="two-launch",
+                   help="GF(2^8) M=128: 'pipelined' = one launch per step running the next batch's row pass "
+                        "with this batch's column pass (rsm_extend_pipeline_dev; A/B, slower than two launches "
+                        "alternating over two streams: profiles/r01g_pipeline_ab.txt)")
     return p.parse_args()
 
 
@@ -319,18 +323,31 @@ def main():
         R._check(L.rsm_stream_create(ctx, ctypes.byref(s2)))
         streams.append(s2)
 
+    pipelined = a.schedule == "pipelined" and 64 < k <= 128
+
     def step():
         i = nstep[0]
         nstep[0] += 1
         R._check(L.rsm_extend_squares_dev(ctx, bufs[i & 1].ptr, k, S, B, streams[i % len(streams)]))
+
+    def run(n):
+        if not pipelined:
+            for _ in range(n):
+                step()
+            return
+        # n complete extensions in n + 1 launches: launch i runs batch i+1's row pass
+        # and batch i's column pass (batches alternate between the two buffers)
+        R._check(L.rsm_extend_pipeline_dev(ctx, bufs[0].ptr, None, k, S, B, None))
+        for i in range(n):
+            rows = bufs[(i + 1) & 1].ptr if i + 1 < n else None
+            R._check(L.rsm_extend_pipeline_dev(ctx, rows, bufs[i & 1].ptr, k, S, B, None))
 
     def sync_all():
         R._check(L.rsm_sync(ctx))
         for st in streams[1:]:
             R._check(L.rsm_stream_sync(st))
 
-    for _ in range(a.warmup):
-        step()
+    run(max(1, a.warmup))
     sync_all()
     # correctness gate on one square before timing (the oracle is the checker only)
     if rank == 0:
@@ -348,8 +365,7 @@ def main():
     barrier()
     sync_all()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
+    run(a.steps)
     sync_all()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -371,6 +387,12 @@ def main():
     t_row, t_col = sum(rms) / len(rms) / 1e3, sum(cms) / len(cms) / 1e3
     t_fused = sum(sms) / len(sms) / 1e3
     fused = bool(L.rsm_extend_fused(k, S))
+    t_pipe = None
+    if pipelined:
+        pms = ctypes.c_float()
+        R._check(L.rsm_time_pipeline(ctx, bufs[1].ptr, bufs[0].ptr, k, S, B, max(6, min(a.steps, 20)),
+                                     ctypes.byref(pms)))
+        t_pipe = pms.value / 1e3
 
     ods_bytes = k * k * S
     total = world * B * a.steps * ods_bytes
@@ -385,10 +407,15 @@ def main():
     col_dom = t_col >= t_row
     dominant = ((kname + " column pass", col_bytes, t_col) if col_dom else (kname + " row pass", row_bytes, t_row))
     if fused:
-        # production k = 128 path: ONE launch per step runs both passes
-        # (encode_gf8_bs128f_kernel); its algorithmic bytes are the step's 4k^2 S
+        # opt-in: ONE launch per step runs both passes (encode_gf8_bs128f_kernel);
+        # its algorithmic bytes are the step's 4k^2 S
         kname = "encode_gf8_bs128f_kernel"
         dominant = (kname + " (fused row + column passes)", algo_step, t_fused)
+    if pipelined:
+        # one launch per step: batch i+1's row pass + batch i's column pass
+        # (encode_gf8_bs128p_kernel) -- one step's worth of algorithmic bytes, 4k^2 S B
+        kname = "encode_gf8_bs128p_kernel"
+        dominant = (kname + " (row pass of batch i+1 + column pass of batch i)", algo_step, t_pipe)
     ach = dominant[1] / dominant[2] / 1e9
     # HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC
     # passes (scripts/pmc_summary.py; FETCH_SIZE x2 gfx950 correction), matched by
@@ -402,6 +429,8 @@ def main():
         sets = (W if col_dom else k) * B * S // 2048
         if fused:
             want, sets = "encode_gf8_bs128f_kernel<40>", 3 * k * B * S // 2048
+        if pipelined:
+            want, sets = "encode_gf8_bs128p_kernel<40>", 3 * k * B * S // 2048
         grid_threads = min(sets, 256) * 512  # persistent grid: one 512-thread workgroup per CU
         for row in json.load(open(pmc_path)).get("launches", []):
             if want in row["kernel"] and row["grid_threads"] == grid_threads:
@@ -421,7 +450,8 @@ def main():
         "data": "synthetic (seeded SplitMix64 bytes, device-generated)",
         "config": {"workload": f"{a.workload}: {wl['desc']}", "k": k, "share_size": S,
                    "squares_per_step": B, "eds_bytes_per_step": B * sq_bytes,
-                   "parallelism": f"independent squares per GPU x{world}"},
+                   "parallelism": f"independent squares per GPU x{world}",
+                   "schedule": "pipelined" if pipelined else "two-launch"},
         "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel": dominant[0], "avg_launch_us": round(dominant[2] * 1e6, 2),
@@ -430,7 +460,9 @@ def main():
                           "achieved": round(algo_step / (elapsed / a.steps) / 1e9, 1),
                           "frac": round(algo_step / (elapsed / a.steps) / 1e9 / HBM_PEAK_GBS, 4),
                           "row_pass_us": round(t_row * 1e6, 2), "col_pass_us": round(t_col * 1e6, 2),
-                          "one_step_launch_us": round(t_fused * 1e6, 2), "fused": fused},
+                          "one_step_launch_us": round(t_fused * 1e6, 2), "fused": fused,
+                          "schedule": "pipelined" if pipelined else "two-launch",
+                          "pipelined_launch_us": round(t_pipe * 1e6, 2) if t_pipe else None},
     }
     if rank == 0 and world == 1:
         # PCIe-inclusive host-memory rate (ComputeExtendedDataSquare from host buffers)

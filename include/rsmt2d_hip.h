@@ -139,6 +139,10 @@ int rsm_sync(rsm_ctx* ctx);
  * column-pass call -- e.g. call i passes batch i+1's rows and batch i's columns. */
 int rsm_extend_pipeline_dev(rsm_ctx* ctx, void* d_rows_eds, void* d_cols_eds, uint32_t k, uint32_t share_size,
                             uint32_t count, void* stream);
+/* Event-timed back-to-back rsm_extend_pipeline_dev launches on the ctx stream:
+ * average milliseconds per launch over `reps`. */
+int rsm_time_pipeline(rsm_ctx* ctx, void* d_rows_eds, void* d_cols_eds, uint32_t k, uint32_t share_size,
+                      uint32_t count, uint32_t reps, float* ms);
 /* 1 when rsm_extend_squares_dev runs both passes of a (k, share_size) square
  * as ONE launch (GF(2^8), k = 128, fused form enabled), else 0. */
 int rsm_extend_fused(uint32_t k, uint32_t share_size);

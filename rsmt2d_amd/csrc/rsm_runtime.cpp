@@ -699,6 +699,26 @@ int rsm_extend_pipeline_dev(rsm_ctx* ctx, void* d_rows_eds, void* d_cols_eds, ui
     return RSM_OK;
 }
 
+int rsm_time_pipeline(rsm_ctx* ctx, void* d_rows_eds, void* d_cols_eds, uint32_t k, uint32_t share_size,
+                      uint32_t count, uint32_t reps, float* ms) {
+    if (!ctx || !ms || reps == 0) return fail(RSM_EINVAL, "rsm_time_pipeline: bad arguments");
+    hipEvent_t ev[2];
+    for (auto& x : ev)
+        if (hipEventCreate(&x) != hipSuccess) return fail(RSM_EDEVICE, "hipEventCreate");
+    int rc = RSM_OK;
+    (void)hipEventRecord(ev[0], ctx->stream);
+    for (uint32_t r = 0; r < reps && rc == RSM_OK; ++r)
+        rc = rsm_extend_pipeline_dev(ctx, d_rows_eds, d_cols_eds, k, share_size, count, nullptr);
+    (void)hipEventRecord(ev[1], ctx->stream);
+    if (hipEventSynchronize(ev[1]) != hipSuccess && rc == RSM_OK) rc = fail(RSM_EDEVICE, "hipEventSynchronize");
+    float t = 0;
+    (void)hipEventElapsedTime(&t, ev[0], ev[1]);
+    for (auto& x : ev) (void)hipEventDestroy(x);
+    if (rc) return rc;
+    *ms = t / reps;
+    return RSM_OK;
+}
+
 int rsm_set_fused(int on) {
     const int prev = fused_enabled() ? 1 : 0;
     g_fused.store(on ? 1 : 0, std::memory_order_relaxed);
