@@ -51,6 +51,8 @@ def parse():
                    help="initialise torch.distributed even at N=1 (rehearses the sharded c5 path on one GPU)")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--one-stream", action="store_true", help="GF(2^8): do not alternate steps over two streams")
+    p.add_argument("--streams", type=int, default=2, help="GF(2^8): streams the steps rotate over")
+    p.add_argument("--buffers", type=int, default=2, help="batches (EDS buffers) the steps rotate over")
     p.add_argument("--schedule", choices=["pipelined", "two-launch"], default="two-launch",
                    help="GF(2^8) M=128: 'pipelined' = one launch per step running the next batch's row pass "
                         "with this batch's column pass (rsm_extend_pipeline_dev; A/B, slower than two launches "
@@ -306,7 +308,7 @@ def main():
     # square's top-left quadrant is its ODS (the other quadrants are overwritten).
     # Two batches are used alternately, so a step never finds the previous step's
     # squares in the 256 MiB Infinity Cache (rotate > 512 MiB).
-    bufs = [R.DeviceBuffer(B * sq_bytes, local) for _ in range(2)]
+    bufs = [R.DeviceBuffer(B * sq_bytes, local) for _ in range(max(2, a.buffers))]
     for i, b in enumerate(bufs):
         b.fill_random(0x52534D543244 + 2 * rank + i)
     R._check(L.rsm_sync(ctx))
@@ -319,16 +321,17 @@ def main():
     import ctypes
     streams = [None]
     if k <= 128 and not a.one_stream:
-        s2 = ctypes.c_void_p()
-        R._check(L.rsm_stream_create(ctx, ctypes.byref(s2)))
-        streams.append(s2)
+        for _ in range(max(1, a.streams) - 1):
+            s2 = ctypes.c_void_p()
+            R._check(L.rsm_stream_create(ctx, ctypes.byref(s2)))
+            streams.append(s2)
 
     pipelined = a.schedule == "pipelined" and 64 < k <= 128
 
     def step():
         i = nstep[0]
         nstep[0] += 1
-        R._check(L.rsm_extend_squares_dev(ctx, bufs[i & 1].ptr, k, S, B, streams[i % len(streams)]))
+        R._check(L.rsm_extend_squares_dev(ctx, bufs[i % len(bufs)].ptr, k, S, B, streams[i % len(streams)]))
 
     def run(n):
         if not pipelined:
