@@ -23,7 +23,7 @@ if [[ $STEPS == *bench* ]]; then run bench 600 python3 bench.py ${BENCH_ARGS:-};
 if [[ $STEPS == *prof* ]]; then
   export TMPDIR=/tmp
   run rocprof 600 rocprofv3 --kernel-trace --stats -d "$PWD/$OUT/prof" -o run --output-format csv -- \
-      python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-}; ok $? || exit 6
+      python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ${PROF_ARGS:-} ${BENCH_ARGS:-}; ok $? || exit 6
 fi
 if [[ $STEPS == *pmc* ]]; then
   export TMPDIR=/tmp
