@@ -484,6 +484,38 @@ int fast_repair(rsm_eds* e, DevSquare& dev, const uint8_t* row_roots, const uint
     if ((r = launch_compare(dev.d_eds, dev.d_scratch, (uint64_t)W * W * S, dev.d_flags, dev.st)) != hipSuccess)
         return hip_fail(r, "compare");
     uint32_t mismatch = 0;
+    // ... and match every committed row and column root: on the device for the
+    // DefaultTree (kernels_sha.hip), through the host Tree plugin otherwise.  The
+    // device check runs before any copy back, so an accepted square lands straight
+    // in the EDS's own (already resident) buffer and a rejected one costs no D2H.
+    if (tree.is_default() && root_len == 32 && roots_dev_supported(W)) {
+        DevBuf& rb = dev.ctx->dev_buf(31);
+        if ((r = rb.ensure((size_t)2 * W * 32)) != hipSuccess) return hip_fail(r, "hipMalloc (roots)");
+        if (int rc = device_roots(dev.ctx, dev.d_eds, W, e->S, static_cast<uint8_t*>(rb.ptr), dev.st)) return rc;
+        std::vector<uint8_t> got((size_t)2 * W * 32);
+        if ((r = hipMemcpyAsync(&mismatch, dev.d_flags, 4, hipMemcpyDeviceToHost, dev.st)) != hipSuccess)
+            return hip_fail(r, "D2H flag");
+        if ((r = hipMemcpyAsync(got.data(), rb.ptr, got.size(), hipMemcpyDeviceToHost, dev.st)) != hipSuccess)
+            return hip_fail(r, "D2H roots");
+        if (int rc = dev.sync()) return rc;
+        if (mismatch) {
+            e->stats.fallback_reason = kFallbackEncoding;
+            return 1;
+        }
+        if (memcmp(got.data(), row_roots, (size_t)W * 32) != 0 ||
+            memcmp(got.data() + (size_t)W * 32, col_roots, (size_t)W * 32) != 0) {
+            e->stats.fallback_reason = kFallbackRoots;
+            return 1;
+        }
+        if (e->data.size() != (size_t)W * W * S) e->data.resize((size_t)W * W * S);
+        if ((r = hipMemcpyAsync(e->data.data(), dev.d_eds, e->data.size(), hipMemcpyDeviceToHost, dev.st)) !=
+            hipSuccess)
+            return hip_fail(r, "D2H square");
+        if (int rc = dev.sync()) return rc;
+        std::fill(e->present.begin(), e->present.end(), 1);
+        e->stats.fast_path = 1;
+        return RSM_OK;
+    }
     std::vector<uint8_t> repaired((size_t)W * W * S);
     if ((r = hipMemcpyAsync(&mismatch, dev.d_flags, 4, hipMemcpyDeviceToHost, dev.st)) != hipSuccess)
         return hip_fail(r, "D2H flag");
@@ -493,26 +525,6 @@ int fast_repair(rsm_eds* e, DevSquare& dev, const uint8_t* row_roots, const uint
     if (mismatch) {
         e->stats.fallback_reason = kFallbackEncoding;
         return 1;
-    }
-    // ... and match every committed row and column root: on the device for the
-    // DefaultTree (kernels_sha.hip), through the host Tree plugin otherwise.
-    if (tree.is_default() && root_len == 32 && roots_dev_supported(W)) {
-        DevBuf& rb = dev.ctx->dev_buf(31);
-        if ((r = rb.ensure((size_t)2 * W * 32)) != hipSuccess) return hip_fail(r, "hipMalloc (roots)");
-        if (int rc = device_roots(dev.ctx, dev.d_eds, W, e->S, static_cast<uint8_t*>(rb.ptr), dev.st)) return rc;
-        std::vector<uint8_t> got((size_t)2 * W * 32);
-        if ((r = hipMemcpyAsync(got.data(), rb.ptr, got.size(), hipMemcpyDeviceToHost, dev.st)) != hipSuccess)
-            return hip_fail(r, "D2H roots");
-        if (int rc = dev.sync()) return rc;
-        if (memcmp(got.data(), row_roots, (size_t)W * 32) != 0 ||
-            memcmp(got.data() + (size_t)W * 32, col_roots, (size_t)W * 32) != 0) {
-            e->stats.fallback_reason = kFallbackRoots;
-            return 1;
-        }
-        e->data.swap(repaired);
-        std::fill(e->present.begin(), e->present.end(), 1);
-        e->stats.fast_path = 1;
-        return RSM_OK;
     }
     std::vector<int> axes;
     std::vector<uint32_t> idxs;
