@@ -159,7 +159,8 @@ def bench_c3(local, L, R, repeats=5):
                       over a device-resident EDS + presence mask, HIP-synchronised);
       repair       -- (*ExtendedDataSquare).Repair end to end as BenchmarkRepair
                       times it (import untimed): upload, device sweeps, full
-                      re-extension check, host SHA-256 roots of every row/col.
+                      re-extension check, DefaultTree roots of every row/col
+                      (on the device), copy back.
     Replicas only: Repair is not sharded."""
     import ctypes
     import numpy as np
@@ -240,8 +241,8 @@ def bench_c3(local, L, R, repeats=5):
             "decode_sweep_frac": round(algo / t_sweep / 1e9 / HBM_PEAK_GBS, 4),
             "repair_ms": round(t_rep * 1e3, 3), "repair_samples": repeats,
             "repair_fast_path": int(stats.fast_path), "repair_sweeps": int(stats.sweeps),
-            "note": "repair = rsm_eds_repair end to end (H2D, device sweeps, re-extension check, "
-                    "host SHA-256 roots of all 512 vectors, D2H); median of samples"}
+            "note": "repair = rsm_eds_repair end to end (H2D, device sweeps, device re-extension check, "
+                    "device DefaultTree roots of all 512 vectors, D2H into the EDS buffer); median of samples"}
 
 
 def bench_roots(local, L, R, buf, k, S, B, steps):
