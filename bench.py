@@ -53,6 +53,9 @@ def parse():
     p.add_argument("--one-stream", action="store_true", help="GF(2^8): do not alternate steps over two streams")
     p.add_argument("--streams", type=int, default=2, help="GF(2^8): streams the steps rotate over")
     p.add_argument("--buffers", type=int, default=2, help="batches (EDS buffers) the steps rotate over")
+    p.add_argument("--row-grid", type=int, default=224,
+                   help="GF(2^8) M=128 with >1 stream: CUs of the row-pass persistent grid (0 = all); the "
+                        "remaining CUs run the other stream's column pass (profiles/r01h_grid_ab.txt)")
     p.add_argument("--schedule", choices=["pipelined", "two-launch"], default="two-launch",
                    help="GF(2^8) M=128: 'pipelined' = one launch per step running the next batch's row pass "
                         "with this batch's column pass (rsm_extend_pipeline_dev; A/B, slower than two launches "
@@ -329,6 +332,9 @@ def main():
 
     pipelined = a.schedule == "pipelined" and 64 < k <= 128
 
+    row_grid = a.row_grid if (len(streams) > 1 and 64 < k <= 128) else 0
+    L.rsm_set_pass_grid(0, row_grid)
+
     def step():
         i = nstep[0]
         nstep[0] += 1
@@ -455,7 +461,8 @@ def main():
         "config": {"workload": f"{a.workload}: {wl['desc']}", "k": k, "share_size": S,
                    "squares_per_step": B, "eds_bytes_per_step": B * sq_bytes,
                    "parallelism": f"independent squares per GPU x{world}",
-                   "schedule": "pipelined" if pipelined else "two-launch"},
+                   "schedule": "pipelined" if pipelined else "two-launch",
+                   "streams": len(streams), "row_pass_grid": row_grid or None},
         "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel": dominant[0], "avg_launch_us": round(dominant[2] * 1e6, 2),

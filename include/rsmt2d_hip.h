@@ -146,6 +146,10 @@ int rsm_time_pipeline(rsm_ctx* ctx, void* d_rows_eds, void* d_cols_eds, uint32_t
 /* 1 when rsm_extend_squares_dev runs both passes of a (k, share_size) square
  * as ONE launch (GF(2^8), k = 128, fused form enabled), else 0. */
 int rsm_extend_fused(uint32_t k, uint32_t share_size);
+/* Throughput tuning for several extensions in flight on different streams: cap
+ * the persistent grid (CUs) of the GF(2^8) M = 128 row pass (pass 0) or column
+ * pass (pass 1); 0 = all CUs (default).  Process-wide; returns the previous cap. */
+int rsm_set_pass_grid(int pass, int cus);
 /* Enable (1) or disable (0) the fused single-launch extension process-wide
  * (default: off, or RSM_FUSED=1); returns the previous setting. */
 int rsm_set_fused(int on);

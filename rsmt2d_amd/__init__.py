@@ -131,6 +131,7 @@ SIGNATURES = {
     "rsm_extend_pipeline_dev": (_I32, [_VP, _VP, _VP, _U32, _U32, _U32, _VP]),
     "rsm_time_pipeline": (_I32, [_VP, _VP, _VP, _U32, _U32, _U32, _U32, ctypes.POINTER(ctypes.c_float)]),
     "rsm_set_fused": (_I32, [ctypes.c_int]),
+    "rsm_set_pass_grid": (_I32, [ctypes.c_int, ctypes.c_int]),
     "rsm_fused_trace": (_I32, [_VP, ctypes.POINTER(ctypes.c_uint32), _U32, ctypes.POINTER(ctypes.c_uint32)]),
     "rsm_stream_create": (_I32, [_VP, ctypes.POINTER(_VP)]),
     "rsm_stream_destroy": (_I32, [_VP, _VP]),

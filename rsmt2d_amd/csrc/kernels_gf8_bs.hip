@@ -27,6 +27,7 @@
 // column pass, slices); callers with an index list use the byte-table kernel.
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <atomic>
 #include <cstdlib>
 #include "bs8.hpp"
 #include "rsm_kernels.hpp"
@@ -710,10 +711,34 @@ static uint32_t device_cus() {
     return n;
 }
 
+static std::atomic<int> g_pass_cap[2] = {-1, -1};
+uint32_t pass_grid_cap(int pass) {
+    int v = g_pass_cap[pass].load(std::memory_order_relaxed);
+    if (v < 0) {
+        const char* e = getenv(pass == 0 ? "RSM_BS_ROWGRID" : "RSM_BS_COLGRID");
+        v = e ? atoi(e) : 0;
+        if (v < 0) v = 0;
+        g_pass_cap[pass].store(v, std::memory_order_relaxed);
+    }
+    return (uint32_t)v;
+}
+int set_pass_grid_cap(int pass, int cus) {
+    const int prev = (int)pass_grid_cap(pass);
+    g_pass_cap[pass].store(cus > 0 ? cus : 0, std::memory_order_relaxed);
+    return prev;
+}
+
 hipError_t launch_encode_gf8_bs128(const CodewordSet& cs, hipStream_t st) {
     const uint64_t sets = ((uint64_t)cs.count * cs.S + kSetBytes - 1) / kSetBytes;
     if (sets == 0) return hipSuccess;
-    const uint32_t grid = (uint32_t)(sets < device_cus() ? sets : device_cus());
+    uint32_t grid = (uint32_t)(sets < device_cus() ? sets : device_cus());
+    // Persistent-grid caps (rsm_set_pass_grid; env RSM_BS_ROWGRID / RSM_BS_COLGRID):
+    // a row pass on fewer CUs leaves the rest to a column pass running on another
+    // stream (profiles/r01h_grid_ab.txt)
+    {
+        const uint32_t cap = pass_grid_cap(cs.elem_stride == cs.S ? 0 : 1);
+        if (cap > 0 && cap < grid) grid = cap;
+    }
     // RSM_BS_MODE: 40 production (addtid exchange + non-temporal loads: measured best,
     // profiles/r01e_bench_ab.txt); A/B: 0 ds_write_b32 exchange, 8 default-policy
     // loads, 24 nt stores, 56 nt loads + stores; diagnostics 2 = no arithmetic, 4 = no

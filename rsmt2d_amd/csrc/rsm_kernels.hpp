@@ -80,6 +80,9 @@ hipError_t launch_extend_gf8_bs128_fused(const FusedPlan& p, hipStream_t st);
 // bit-sliced M = 128 encode (kernels_gf8_bs.hip); launch_encode_gf8 picks it when applicable
 bool bs128_applicable(const CodewordSet& cs);
 hipError_t launch_encode_gf8_bs128(const CodewordSet& cs, hipStream_t st);
+// persistent-grid cap of the M = 128 row (pass 0) / column (pass 1) launches, 0 = all CUs
+uint32_t pass_grid_cap(int pass);
+int set_pass_grid_cap(int pass, int cus);
 hipError_t launch_decode_gf8(const DecodeSet& ds, hipStream_t st);
 struct Gf16Dev;
 hipError_t launch_encode_gf16(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st);

@@ -719,6 +719,11 @@ int rsm_time_pipeline(rsm_ctx* ctx, void* d_rows_eds, void* d_cols_eds, uint32_t
     return RSM_OK;
 }
 
+int rsm_set_pass_grid(int pass, int cus) {
+    if (pass != 0 && pass != 1) return fail(RSM_EINVAL, "rsm_set_pass_grid: pass must be 0 (rows) or 1 (columns)");
+    return set_pass_grid_cap(pass, cus);
+}
+
 int rsm_set_fused(int on) {
     const int prev = fused_enabled() ? 1 : 0;
     g_fused.store(on ? 1 : 0, std::memory_order_relaxed);
