@@ -17,8 +17,9 @@ exchange, so scaling is "weak".
 
 Extra JSON objects: "roofline" (dominant kernel, HIP-event timed on the launch
 stream), "step_roofline" (whole 2D encode vs SURVEY's algorithmic bytes 4k^2 S),
-"cpu_baseline" (the C oracle restatement -- kind "port" -- on this host's cores),
-"host_path" (PCIe-inclusive rate through rsm_extend_square; never `value`).
+"cpu_baseline" (AVX2 restatement of the reference path -- kind "port" -- on this host's cores),
+"host_path" (PCIe-inclusive rates, pinned+overlapped and pageable; never `value`),
+"codec" (per-codeword Encode latency and 64-thread concurrent rate).
 """
 import argparse
 import json
@@ -39,14 +40,15 @@ WORKLOADS = {
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     p.add_argument("--batch", type=int, default=0, help="squares per step (default: >= 512 MiB of EDS)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-c5", action="store_true", help="skip the config-5 (sharded 512x512 square) line")
     p.add_argument("--no-c3", action="store_true", help="skip the config-3 (Repair) timings")
     p.add_argument("--no-roots", action="store_true", help="skip the extension + Merkle roots timing")
+    p.add_argument("--no-extras", action="store_true", help="skip host-path and Codec-latency lines")
     p.add_argument("--dist", action="store_true",
                    help="initialise torch.distributed even at N=1 (rehearses the sharded c5 path on one GPU)")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -56,31 +58,148 @@ def parse():
     p.add_argument("--row-grid", type=int, default=224,
                    help="GF(2^8) M=128 with >1 stream: CUs of the row-pass persistent grid (0 = all); the "
                         "remaining CUs run the other stream's column pass (profiles/r01h_grid_ab.txt)")
-    p.add_argument("--schedule", choices=["pipelined", "two-launch"], default="two-launch",
-                   help="GF(2^8) M=128: 'pipelined' = one launch per step running the next batch's row pass "
-                        "with this batch's column pass (rsm_extend_pipeline_dev; A/B, slower than two launches "
-                        "alternating over two streams: profiles/r01g_pipeline_ab.txt)")
     return p.parse_args()
 
 
+def cpu_info():
+    model, cores = None, os.cpu_count()
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return model, cores
+
+
 def cpu_baseline(k, S, seconds):
-    """The oracle's C restatement of the reference path, multithreaded over codewords."""
+    """AVX2 restatement of the reference path (oracle/libleopard_simd.so: the C oracle
+    with klauspost's pshufb nibble-table GF(2^8) rows), multithreaded over codewords
+    with the reference's two-phase schedule.  Not the reference: its Go/klauspost
+    code cannot run here."""
     import numpy as np
     import oracle
     threads = min(16, os.cpu_count() or 1)
     ods = oracle.splitmix64_bytes(k * k * S).reshape(k, k, S)
-    oracle.extend_square(ods, nthreads=threads)  # warm
+    ext = oracle.extend_square_simd if k <= 128 else oracle.extend_square
+    ext(ods, nthreads=threads)  # warm
     n, t0 = 0, time.perf_counter()
     while True:
-        oracle.extend_square(ods, nthreads=threads)
+        ext(ods, nthreads=threads)
         n += 1
         dt = time.perf_counter() - t0
         if dt >= seconds:
             break
+    model, ncpu = cpu_info()
     return {"value": round(n * k * k * S / dt / 2**30, 4), "unit": "GiB/s", "cores": threads,
-            "kind": "port",
-            "sample": f"{n} squares k={k} S={S} through oracle/leopard_oracle.c (scalar C restatement of "
-                      f"klauspost leopard, {threads} threads over codewords); the Go reference cannot run here"}
+            "kind": "port", "cpu_model": model, "host_cpus": ncpu,
+            "sample": f"{n} squares k={k} S={S} ({dt:.1f} s) through oracle/leopard_oracle.c built with LEO_SIMD "
+                      f"(AVX2 pshufb nibble-table rows, restatement of klauspost leopard8, not the reference), "
+                      f"{threads} threads over codewords; the Go reference cannot run here"}
+
+
+def pct(xs, q):
+    xs = sorted(xs)
+    if not xs:
+        return None
+    i = min(len(xs) - 1, max(0, int(round(q * (len(xs) - 1)))))
+    return xs[i]
+
+
+def bench_codec(local, L, R, k=128, S=512, calls=400, threads=64):
+    """Per-codeword Encode (codec_test.go:15-35 BenchmarkEncoding, k=128, 512 B):
+    latency of one rsm_encode from host memory on an idle GPU, and aggregate rate
+    with `threads` host threads calling concurrently (rsmt2d's 2k goroutines)."""
+    import ctypes
+    import threading
+    import numpy as np
+    ctx = R.device_context(local)
+    rng = np.random.default_rng(7)
+
+    def mk():
+        data = rng.integers(0, 256, (k, S), dtype=np.uint8)
+        par = np.empty((k, S), np.uint8)
+        dp = (ctypes.c_void_p * k)(*[data.ctypes.data + i * S for i in range(k)])
+        pp = (ctypes.c_void_p * k)(*[par.ctypes.data + i * S for i in range(k)])
+        return data, par, dp, pp
+
+    d, p, dp, pp = mk()
+    for _ in range(20):
+        R._check(L.rsm_encode(ctx, dp, k, S, pp))
+    lat = []
+    for _ in range(calls):
+        t0 = time.perf_counter()
+        R._check(L.rsm_encode(ctx, dp, k, S, pp))
+        lat.append(time.perf_counter() - t0)
+    per = max(1, calls // 2)
+    bufs = [mk() for _ in range(threads)]
+    errs = []
+
+    def worker(i):
+        _, _, a, b = bufs[i]
+        for _ in range(per):
+            rc = L.rsm_encode(ctx, a, k, S, b)
+            if rc:
+                errs.append(rc)
+
+    ths = [threading.Thread(target=worker, args=(i,)) for i in range(threads)]
+    t0 = time.perf_counter()
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    dt = time.perf_counter() - t0
+    if errs:
+        raise SystemExit(f"bench codec: concurrent rsm_encode failed {errs[:3]}")
+    n = threads * per
+    return {"workload": f"per-codeword Encode k={k} S={S} from host memory (BenchmarkEncoding shape)",
+            "latency_us_p50": round(pct(lat, 0.5) * 1e6, 1), "latency_us_p10": round(pct(lat, 0.1) * 1e6, 1),
+            "latency_us_p90": round(pct(lat, 0.9) * 1e6, 1),
+            "concurrent_threads": threads, "concurrent_codewords_per_s": round(n / dt, 1),
+            "concurrent_GiB_s": round(n * k * S / dt / 2**30, 3)}
+
+
+def bench_host_path(local, L, R, k, S, squares=8, seconds=2.0):
+    """ComputeExtendedDataSquare from host memory (north_star: rate including
+    hipMemcpyAsync both ways).  pinned: rsm_extend_squares_host over `squares`
+    squares in pinned arenas (H2D / extension / D2H of different squares overlap on
+    three streams; only Q1..Q3 come back); pageable: rsm_extend_square one square
+    at a time from numpy memory."""
+    import ctypes
+    import numpy as np
+    ctx = R.device_context(local)
+    W = 2 * k
+    ob, eb = k * k * S, W * W * S
+    hp_o, hp_e = ctypes.c_void_p(), ctypes.c_void_p()
+    R._check(L.rsm_host_alloc(ctx, ob * squares, ctypes.byref(hp_o)))
+    R._check(L.rsm_host_alloc(ctx, eb * squares, ctypes.byref(hp_e)))
+    ods = np.ctypeslib.as_array((ctypes.c_uint8 * (ob * squares)).from_address(hp_o.value))
+    ods[:] = np.random.default_rng(3).integers(0, 256, ob * squares, dtype=np.uint8)
+    R._check(L.rsm_extend_squares_host(ctx, hp_o, k, S, squares, hp_e))
+    eds = np.ctypeslib.as_array((ctypes.c_uint8 * eb).from_address(hp_e.value)).reshape(W, W, S)
+    import oracle
+    if not np.array_equal(eds, oracle.extend_square(ods[:ob].reshape(k, k, S), nthreads=8)):
+        raise SystemExit("bench host path: pinned batch differs from the oracle")
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        R._check(L.rsm_extend_squares_host(ctx, hp_o, k, S, squares, hp_e))
+        n += 1
+    pinned = n * squares * ob / (time.perf_counter() - t0) / 2**30
+    R._check(L.rsm_host_free(ctx, hp_o))
+    R._check(L.rsm_host_free(ctx, hp_e))
+    o1 = np.random.default_rng(1).integers(0, 256, (k, k, S), dtype=np.uint8)
+    e1 = np.empty((W, W, S), np.uint8)
+    R._check(L.rsm_extend_square(ctx, o1.ctypes.data, k, S, e1.ctypes.data))
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds / 2:
+        R._check(L.rsm_extend_square(ctx, o1.ctypes.data, k, S, e1.ctypes.data))
+        n += 1
+    pageable = n * ob / (time.perf_counter() - t0) / 2**30
+    return {"pinned_GiB_s": round(pinned, 3), "pageable_GiB_s": round(pageable, 3), "unit": "GiB/s ODS",
+            "pcie_bytes_per_square": ob + 3 * ob,
+            "note": f"pinned = rsm_extend_squares_host over {squares} squares per call (3 streams: H2D, extension and "
+                    "D2H of different squares overlap; Q0 is not copied back); pageable = rsm_extend_square per square"}
 
 
 def bench_c5(world, rank, local, dist, steps, L, R):
@@ -104,6 +223,23 @@ def bench_c5(world, rank, local, dist, steps, L, R):
         R._check(L.rsm_sync(ctx))
         dt = (time.perf_counter() - t0) / steps
         buf.free()
+        # the C-ABI multi-GPU entry point (rsm_multi_extend_square) with a clique of one,
+        # host memory to host memory, both exchange schedules
+        import ctypes
+        import numpy as np
+        m = ctypes.c_void_p()
+        devs = (ctypes.c_int * 1)(local)
+        R._check(L.rsm_multi_create(devs, 1, ctypes.byref(m)))
+        ods = np.random.default_rng(5).integers(0, 256, (k, k, S), dtype=np.uint8)
+        eds = np.empty((W, W, S), np.uint8)
+        multi = {}
+        for name, sched in (("allgather", 0), ("alltoall", 1)):
+            R._check(L.rsm_multi_extend_square(m, ods.ctypes.data, k, S, eds.ctypes.data, sched))
+            t1 = time.perf_counter()
+            for _ in range(3):
+                R._check(L.rsm_multi_extend_square(m, ods.ctypes.data, k, S, eds.ctypes.data, sched))
+            multi[name + "_host_ms"] = round((time.perf_counter() - t1) / 3 * 1e3, 3)
+        L.rsm_multi_destroy(m)
     else:
         import torch
         from rsmt2d_amd.distributed import (RowShardedExtender, TransposeShardedExtender, hip_backend,
@@ -147,6 +283,8 @@ def bench_c5(world, rank, local, dist, steps, L, R):
                        + ("" if world == 1 else f", rows sharded over {world} GPUs + RCCL all-to-all of column slices"),
            "n_gpus": world, "ms_per_square": round(dt * 1e3, 4), "ods_GiB_s": round(k * k * S / dt / 2**30, 3),
            "scaling": "strong (one square)"}
+    if dist is None:
+        out["c_abi_multi_gpu_1"] = multi
     if dist is not None:
         out["received_bytes_per_gpu"] = (world - 1) * (k // world) * (W // world) * S
         out["allgather_ms_per_square"] = round(dt_ag * 1e3, 4)
@@ -283,6 +421,7 @@ def bench_roots(local, L, R, buf, k, S, B, steps):
 
 def main():
     a = parse()
+    import ctypes
     import numpy as np
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -310,54 +449,54 @@ def main():
 
     # synthetic ODS: seeded uniform bytes (SplitMix64) generated on the device; each
     # square's top-left quadrant is its ODS (the other quadrants are overwritten).
-    # Two batches are used alternately, so a step never finds the previous step's
-    # squares in the 256 MiB Infinity Cache (SURVEY §8(d): rotate > 512 MiB).
+    # Batches are used in rotation, so a step never finds the previous step's
+    # squares in the 256 MiB Infinity Cache (SURVEY section 8(d): rotate > 512 MiB).
     bufs = [R.DeviceBuffer(B * sq_bytes, local) for _ in range(max(2, a.buffers))]
     for i, b in enumerate(bufs):
         b.fill_random(0x52534D543244 + 2 * rank + i)
     R._check(L.rsm_sync(ctx))
     buf = bufs[0]
-    nstep = [0]
     # GF(2^8): consecutive steps alternate between two streams (each step's row and
     # column passes stay ordered on its own stream), so one step's column-pass tail
-    # overlaps the next step's row-pass prologue.  GF(2^16) shares the context's work
-    # arrays between launches: one stream.
-    import ctypes
+    # overlaps the next step's row-pass prologue.  (Every stream owns its scratch.)
     streams = [None]
-    if k <= 128 and not a.one_stream:
+    if not a.one_stream:
         for _ in range(max(1, a.streams) - 1):
             s2 = ctypes.c_void_p()
             R._check(L.rsm_stream_create(ctx, ctypes.byref(s2)))
             streams.append(s2)
-
-    pipelined = a.schedule == "pipelined" and 64 < k <= 128
-
     row_grid = a.row_grid if (len(streams) > 1 and 64 < k <= 128) else 0
-    L.rsm_set_pass_grid(0, row_grid)
+    prev_grid = ctypes.c_int()
+    R._check(L.rsm_ctx_set_pass_grid(ctx, 0, row_grid, ctypes.byref(prev_grid)))
 
-    def step():
+    def new_event():
+        e = ctypes.c_void_p()
+        R._check(L.rsm_event_create(ctx, ctypes.byref(e)))
+        return e
+
+    nstep = [0]
+
+    def step(ev=None):
         i = nstep[0]
         nstep[0] += 1
-        R._check(L.rsm_extend_squares_dev(ctx, bufs[i % len(bufs)].ptr, k, S, B, streams[i % len(streams)]))
-
-    def run(n):
-        if not pipelined:
-            for _ in range(n):
-                step()
+        st, b = streams[i % len(streams)], bufs[i % len(bufs)].ptr
+        if ev is None:
+            R._check(L.rsm_extend_squares_dev(ctx, b, k, S, B, st))
             return
-        # n complete extensions in n + 1 launches: launch i runs batch i+1's row pass
-        # and batch i's column pass (batches alternate between the two buffers)
-        R._check(L.rsm_extend_pipeline_dev(ctx, bufs[0].ptr, None, k, S, B, None))
-        for i in range(n):
-            rows = bufs[(i + 1) & 1].ptr if i + 1 < n else None
-            R._check(L.rsm_extend_pipeline_dev(ctx, rows, bufs[i & 1].ptr, k, S, B, None))
+        # the production step (two launches) with an event at each launch boundary
+        R._check(L.rsm_event_record(ctx, ev[0], st))
+        R._check(L.rsm_extend_squares_phase_dev(ctx, b, k, S, B, 1, st))
+        R._check(L.rsm_event_record(ctx, ev[1], st))
+        R._check(L.rsm_extend_squares_phase_dev(ctx, b, k, S, B, 2, st))
+        R._check(L.rsm_event_record(ctx, ev[2], st))
 
     def sync_all():
         R._check(L.rsm_sync(ctx))
         for st in streams[1:]:
             R._check(L.rsm_stream_sync(st))
 
-    run(max(1, a.warmup))
+    for _ in range(max(1, a.warmup)):
+        step()
     sync_all()
     # correctness gate on one square before timing (the oracle is the checker only)
     if rank == 0:
@@ -372,10 +511,12 @@ def main():
             dist.barrier()
             torch.cuda.synchronize()
 
+    events = [[new_event() for _ in range(3)] for _ in range(a.steps)]
     barrier()
     sync_all()
     t0 = time.perf_counter()
-    run(a.steps)
+    for i in range(a.steps):
+        step(events[i])
     sync_all()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -383,32 +524,30 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-
-    # per-kernel durations: HIP events on the launch stream (the context stream)
-    import ctypes
-    row_ms, col_ms, step_ms = ctypes.c_float(), ctypes.c_float(), ctypes.c_float()
-    rms, cms, sms = [], [], []
-    for r in range(max(6, min(a.steps, 20))):  # row, column, then one production step per call
-        R._check(L.rsm_time_extend(ctx, bufs[r & 1].ptr, k, S, B, 1, ctypes.byref(row_ms), ctypes.byref(col_ms),
-                                   ctypes.byref(step_ms)))
-        rms.append(row_ms.value)
-        cms.append(col_ms.value)
-        sms.append(step_ms.value)
-    t_row, t_col = sum(rms) / len(rms) / 1e3, sum(cms) / len(cms) / 1e3
-    t_fused = sum(sms) / len(sms) / 1e3
-    fused = bool(L.rsm_extend_fused(k, S))
-    t_pipe = None
-    if pipelined:
-        pms = ctypes.c_float()
-        R._check(L.rsm_time_pipeline(ctx, bufs[1].ptr, bufs[0].ptr, k, S, B, max(6, min(a.steps, 20)),
-                                     ctypes.byref(pms)))
-        t_pipe = pms.value / 1e3
+    # per-launch durations of THIS timed run (events on the launch streams)
+    rows, cols, spans = [], [], []
+    ms = ctypes.c_float()
+    for ev in events:
+        R._check(L.rsm_event_elapsed_ms(ev[0], ev[1], ctypes.byref(ms)))
+        rows.append(ms.value / 1e3)
+        R._check(L.rsm_event_elapsed_ms(ev[1], ev[2], ctypes.byref(ms)))
+        cols.append(ms.value / 1e3)
+        R._check(L.rsm_event_elapsed_ms(ev[0], ev[2], ctypes.byref(ms)))
+        spans.append(ms.value / 1e3)
+        for e in ev:
+            L.rsm_event_destroy(e)
+    t_row, t_col = sum(rows) / len(rows), sum(cols) / len(cols)
+    # the same launches alone on one stream (no overlap with another step)
+    r_ms, c_ms, s_ms = ctypes.c_float(), ctypes.c_float(), ctypes.c_float()
+    R._check(L.rsm_time_extend(ctx, bufs[0].ptr, k, S, B, 10, ctypes.byref(r_ms), ctypes.byref(c_ms),
+                               ctypes.byref(s_ms)))
+    R._check(L.rsm_ctx_set_pass_grid(ctx, 0, prev_grid.value, None))
 
     ods_bytes = k * k * S
     total = world * B * a.steps * ods_bytes
     value = total / elapsed / 2**30
     ms_per_step = elapsed / a.steps * 1e3
-    algo_step = 4 * ods_bytes * B  # SURVEY §8(d): read Q0 once, write Q1+Q2+Q3
+    algo_step = 4 * ods_bytes * B  # SURVEY section 8(d): read Q0 once, write Q1+Q2+Q3
     col_bytes = 4 * ods_bytes * B  # column pass: [Q0|Q1] in, [Q2|Q3] out
     row_bytes = 2 * ods_bytes * B  # row pass: Q0 in, Q1 out
     bitsliced = 64 < k <= 128
@@ -416,16 +555,6 @@ def main():
              else "enc16_a/b/c (GF(2^16) passes)")
     col_dom = t_col >= t_row
     dominant = ((kname + " column pass", col_bytes, t_col) if col_dom else (kname + " row pass", row_bytes, t_row))
-    if fused:
-        # opt-in: ONE launch per step runs both passes (encode_gf8_bs128f_kernel);
-        # its algorithmic bytes are the step's 4k^2 S
-        kname = "encode_gf8_bs128f_kernel"
-        dominant = (kname + " (fused row + column passes)", algo_step, t_fused)
-    if pipelined:
-        # one launch per step: batch i+1's row pass + batch i's column pass
-        # (encode_gf8_bs128p_kernel) -- one step's worth of algorithmic bytes, 4k^2 S B
-        kname = "encode_gf8_bs128p_kernel"
-        dominant = (kname + " (row pass of batch i+1 + column pass of batch i)", algo_step, t_pipe)
     ach = dominant[1] / dominant[2] / 1e9
     # HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC
     # passes (scripts/pmc_summary.py; FETCH_SIZE x2 gfx950 correction), matched by
@@ -434,17 +563,13 @@ def main():
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_latest.json")
     if bitsliced and os.path.exists(pmc_path):
-        # production template <MODE 40, PASS>; A/B modes (RSM_BS_MODE) launch PASS 1
-        want = "encode_gf8_bs128u_kernel<%s, %d>" % (os.environ.get("RSM_BS_MODE", "40"), 1 if col_dom else 0)
+        want = "encode_gf8_bs128u_kernel<40, %d>" % (1 if col_dom else 0)
         sets = (W if col_dom else k) * B * S // 2048
-        if fused:
-            want, sets = "encode_gf8_bs128f_kernel<40>", 3 * k * B * S // 2048
-        if pipelined:
-            want, sets = "encode_gf8_bs128p_kernel<40>", 3 * k * B * S // 2048
         grid_threads = min(sets, 256) * 512  # persistent grid: one 512-thread workgroup per CU
         for row in json.load(open(pmc_path)).get("launches", []):
             if want in row["kernel"] and row["grid_threads"] == grid_threads:
                 traffic = int(row["traffic_bytes"])
+    us = lambda x: round(x * 1e6, 2)
     out = {
         "metric": "GiB/s device-resident 2D RS encode, k=128 square, 512 B shares; % HBM peak",
         "value": round(value, 3),
@@ -459,33 +584,33 @@ def main():
         "dtype": "u8" if k <= 128 else "u16",
         "data": "synthetic (seeded SplitMix64 bytes, device-generated)",
         "config": {"workload": f"{a.workload}: {wl['desc']}", "k": k, "share_size": S,
-                   "squares_per_step": B, "eds_bytes_per_step": B * sq_bytes,
+                   "squares_per_step": B, "eds_bytes_per_step": B * sq_bytes, "buffers": len(bufs),
                    "parallelism": f"independent squares per GPU x{world}",
-                   "schedule": "pipelined" if pipelined else "two-launch",
-                   "streams": len(streams), "row_pass_grid": row_grid or None},
+                   "schedule": "two-launch", "streams": len(streams), "row_pass_grid": row_grid or None},
         "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": dominant[0], "avg_launch_us": round(dominant[2] * 1e6, 2),
-                     "bytes_per_launch": dominant[1]},
+                     "kernel": dominant[0], "avg_launch_us": us(dominant[2]),
+                     "bytes_per_launch": dominant[1],
+                     "source": f"HIP events around every launch of the {a.steps} timed steps"},
         "step_roofline": {"algorithmic_bytes": algo_step,
                           "achieved": round(algo_step / (elapsed / a.steps) / 1e9, 1),
                           "frac": round(algo_step / (elapsed / a.steps) / 1e9 / HBM_PEAK_GBS, 4),
-                          "row_pass_us": round(t_row * 1e6, 2), "col_pass_us": round(t_col * 1e6, 2),
-                          "one_step_launch_us": round(t_fused * 1e6, 2), "fused": fused,
-                          "schedule": "pipelined" if pipelined else "two-launch",
-                          "pipelined_launch_us": round(t_pipe * 1e6, 2) if t_pipe else None},
+                          "row_pass_us": {"mean": us(t_row), "p10": us(pct(rows, .1)), "p50": us(pct(rows, .5)),
+                                          "p90": us(pct(rows, .9))},
+                          "col_pass_us": {"mean": us(t_col), "p10": us(pct(cols, .1)), "p50": us(pct(cols, .5)),
+                                          "p90": us(pct(cols, .9))},
+                          "step_span_us": {"p10": us(pct(spans, .1)), "p50": us(pct(spans, .5)),
+                                           "p90": us(pct(spans, .9))},
+                          "isolated_one_stream_us": {"row": round(r_ms.value * 1e3, 2),
+                                                     "col": round(c_ms.value * 1e3, 2)}},
     }
     if rank == 0 and world == 1:
-        # PCIe-inclusive host-memory rate (ComputeExtendedDataSquare from host buffers)
-        ods = np.random.default_rng(1).integers(0, 256, (k, k, S), dtype=np.uint8)
-        eh = np.empty((W, W, S), np.uint8)
-        R._check(L.rsm_extend_square(ctx, ods.ctypes.data, k, S, eh.ctypes.data))
-        t1, n = time.perf_counter(), 0
-        while time.perf_counter() - t1 < 1.0:
-            R._check(L.rsm_extend_square(ctx, ods.ctypes.data, k, S, eh.ctypes.data))
-            n += 1
-        out["host_path"] = {"value": round(n * ods_bytes / (time.perf_counter() - t1) / 2**30, 3), "unit": "GiB/s",
-                            "note": "rsm_extend_square: pageable host ODS -> H2D -> extend -> D2H EDS, one square"}
+        model, ncpu = cpu_info()
+        out["host"] = {"cpu_model": model, "cpus": ncpu}
+        if not a.no_extras:
+            out["host_path"] = bench_host_path(local, L, R, k, S, squares=8 if k <= 128 else 2)
+            if k <= 128:
+                out["codec"] = bench_codec(local, L, R)
         out["cpu_baseline"] = None if a.no_cpu_baseline else cpu_baseline(k, S, a.cpu_seconds)
     if rank == 0 and world == 1 and not a.no_roots:
         out["with_roots"] = bench_roots(local, L, R, buf, k, S, B, a.steps)

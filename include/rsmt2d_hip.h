@@ -40,11 +40,20 @@ typedef struct rsm_ctx rsm_ctx;
 typedef struct rsm_eds rsm_eds;
 
 /* ---- context --------------------------------------------------------------- */
-/* One context per GPU (device ordinal).  Thread-safe: calls on one context are
- * serialised internally (rsmt2d calls the Codec from up to 2k goroutines,
- * extendeddatasquare.go:186-224). */
+/* One context per GPU (device ordinal).  Thread-safe: rsmt2d calls the Codec from
+ * up to 2k goroutines at once (extendeddatasquare.go:186-224); each Codec /
+ * host-memory call takes its own stream and staging buffers from the context's
+ * pool (up to 32 in flight, further callers wait), device scratch belongs to the
+ * stream it is used on, and every call selects the context's device on the
+ * calling thread (cgo moves goroutines between OS threads). */
 int rsm_ctx_create(int device, rsm_ctx** out);
 void rsm_ctx_destroy(rsm_ctx* ctx);
+int rsm_ctx_device(const rsm_ctx* ctx);
+/* Throughput tuning for several extensions in flight on different streams: cap the
+ * persistent grid (CUs) of this context's GF(2^8) M = 128 row pass (pass 0) or
+ * column pass (pass 1); 0 = all CUs (default).  *previous (may be NULL) receives
+ * the old cap.  Results never depend on it. */
+int rsm_ctx_set_pass_grid(rsm_ctx* ctx, int pass, int cus, int* previous);
 const char* rsm_last_error(void);
 const char* rsm_version(void);
 int rsm_device_count(void);
@@ -70,9 +79,22 @@ int rsm_decode(rsm_ctx* ctx, uint8_t* const* shares, const uint8_t* present, uin
                uint32_t share_size);
 
 /* ---- batched 2D extension (erasureExtendSquare, extendeddatasquare.go:154-227) -- */
-/* Host memory: ods = k*k shares row-major, eds = (2k)^2 shares row-major. */
+/* Host memory: ods = k*k shares row-major, eds = (2k)^2 shares row-major.  Only
+ * Q1, Q2, Q3 cross PCIe back; Q0 of eds is filled from ods on the host. */
 int rsm_extend_square(rsm_ctx* ctx, const uint8_t* ods, uint32_t k, uint32_t share_size,
                       uint8_t* eds);
+/* Host memory, in place: the top-left quadrant of eds already holds the ODS (the
+ * cgo shim gathers the [][]byte shares straight into a pinned EDS arena from
+ * rsm_host_alloc); Q1..Q3 are written around it. */
+int rsm_extend_square_inplace_host(rsm_ctx* ctx, uint8_t* eds, uint32_t k, uint32_t share_size);
+/* Host memory, `count` consecutive squares (ods: [count][k][k][S], eds:
+ * [count][2k][2k][S]): H2D, extension and D2H of different squares overlap on
+ * three streams.  Pinned buffers (rsm_host_alloc) make every copy an async DMA. */
+int rsm_extend_squares_host(rsm_ctx* ctx, const uint8_t* ods, uint32_t k, uint32_t share_size, uint32_t count,
+                            uint8_t* eds);
+/* Pinned (page-locked) host memory for the arenas above. */
+int rsm_host_alloc(rsm_ctx* ctx, uint64_t bytes, void** out);
+int rsm_host_free(rsm_ctx* ctx, void* p);
 /* Device-resident, in place: d_eds holds `count` consecutive [2k][2k][S] squares
  * whose top-left quadrant already holds the ODS (the EDS aliases the ODS, as in
  * ComputeExtendedDataSquare).  Enqueued on `stream` (a hipStream_t of this
@@ -117,6 +139,32 @@ int rsm_decode_vectors_dev(rsm_ctx* ctx, void* d_eds, const uint8_t* d_presence,
                            uint32_t share_size, int axis, const uint32_t* d_indices, uint32_t count,
                            void* stream);
 
+/* ---- one square over several GPUs of a node (config 5) --------------------------- */
+/* One process drives G GPUs: a context per device plus an RCCL clique
+ * (ncclCommInitAll).  GPU g owns Q0 rows [g k/G, (g+1) k/G): it row-encodes them,
+ * the top half is exchanged over xGMI, and GPU g column-encodes its 2k/G columns
+ * (SURVEY.md section 8(e)).  Kernels and collectives of a GPU are ordered on that
+ * GPU's context stream -- no host synchronisation between the steps. */
+typedef struct rsm_multi rsm_multi;
+#define RSM_SCHED_ALLGATHER 0 /* north_star: all-gather of the row-encoded top half */
+#define RSM_SCHED_ALLTOALL 1  /* grouped send/recv: each GPU receives only its column slice */
+int rsm_multi_create(const int* devices, int n, rsm_multi** out);
+void rsm_multi_destroy(rsm_multi* m);
+int rsm_multi_size(const rsm_multi* m);
+/* The per-GPU context (device memory, streams) of GPU i of the clique. */
+rsm_ctx* rsm_multi_context(rsm_multi* m, int i);
+/* ComputeExtendedDataSquare (extendeddatasquare.go:50-77) of ONE k x k square from
+ * host memory (ods k*k*S row-major -> eds (2k)^2*S row-major) over the clique;
+ * k must be a multiple of G.  Synchronous. */
+int rsm_multi_extend_square(rsm_multi* m, const uint8_t* ods, uint32_t k, uint32_t share_size, uint8_t* eds,
+                            int schedule);
+/* Device-resident form: d_eds[g] is a full [2k][2k][S] buffer on GPU g holding Q0
+ * rows of shard g; afterwards it holds shard g's rows of the top half and its
+ * column slice [g 2k/G, (g+1) 2k/G) of the whole square (all-gather: the whole top
+ * half as well).  Asynchronous on the context streams; rsm_multi_sync waits. */
+int rsm_multi_extend_dev(rsm_multi* m, void* const* d_eds, uint32_t k, uint32_t share_size, int schedule);
+int rsm_multi_sync(rsm_multi* m);
+
 /* ---- device memory / timing on the context's HIP runtime ---------------------- */
 /* The context's stream (hipStream_t); the *_dev calls above use it when their
  * stream argument is NULL. */
@@ -130,41 +178,20 @@ int rsm_dev_fill_random(rsm_ctx* ctx, void* d, uint64_t bytes, uint64_t seed);
 int rsm_sync(rsm_ctx* ctx);
 /* Extra HIP streams on the context's device, for callers that pipeline independent
  * batches (e.g. step n's column pass beside step n+1's row pass on another
- * stream).  GF(2^16) encodes share the context's work arrays: keep them on one
- * stream. */
-/* Software-pipelined batches: ONE launch runs the row pass (Q0 -> Q1) of `count`
- * squares at d_rows_eds AND the column pass ([Q0|Q1] -> [Q2|Q3]) of `count`
- * squares at d_cols_eds (either may be NULL; the two batches must not overlap).
- * A batch is fully extended by its row-pass call followed, in stream order, by its
- * column-pass call -- e.g. call i passes batch i+1's rows and batch i's columns. */
-int rsm_extend_pipeline_dev(rsm_ctx* ctx, void* d_rows_eds, void* d_cols_eds, uint32_t k, uint32_t share_size,
-                            uint32_t count, void* stream);
-/* Event-timed back-to-back rsm_extend_pipeline_dev launches on the ctx stream:
- * average milliseconds per launch over `reps`. */
-int rsm_time_pipeline(rsm_ctx* ctx, void* d_rows_eds, void* d_cols_eds, uint32_t k, uint32_t share_size,
-                      uint32_t count, uint32_t reps, float* ms);
-/* 1 when rsm_extend_squares_dev runs both passes of a (k, share_size) square
- * as ONE launch (GF(2^8), k = 128, fused form enabled), else 0. */
-int rsm_extend_fused(uint32_t k, uint32_t share_size);
-/* Throughput tuning for several extensions in flight on different streams: cap
- * the persistent grid (CUs) of the GF(2^8) M = 128 row pass (pass 0) or column
- * pass (pass 1); 0 = all CUs (default).  Process-wide; returns the previous cap. */
-int rsm_set_pass_grid(int pass, int cus);
-/* Enable (1) or disable (0) the fused single-launch extension process-wide
- * (default: off, or RSM_FUSED=1); returns the previous setting. */
-int rsm_set_fused(int on);
-/* Debug: with RSM_FUSED_TRACE set, the last fused launch on the ctx stream records
- * per item (queue order) workgroup << 8 | iteration << 2 | path (1 first item,
- * 2 prefetched, 3 loaded synchronously); copies min(n, items) words and the
- * stuck-wait flag.  Returns the number of words copied or a negative code. */
-int rsm_fused_trace(rsm_ctx* ctx, uint32_t* out, uint32_t n, uint32_t* err);
+ * stream).  Each stream owns its device scratch (GF(2^16) work arrays, leaf
+ * digests), released by rsm_stream_destroy. */
 int rsm_stream_create(rsm_ctx* ctx, void** out);
 int rsm_stream_destroy(rsm_ctx* ctx, void* stream);
 int rsm_stream_sync(void* stream);
+/* HIP events on the context's device, for timing launches inside a caller's loop
+ * (NULL stream = context stream).  rsm_event_elapsed_ms waits for `end`. */
+int rsm_event_create(rsm_ctx* ctx, void** out);
+int rsm_event_destroy(void* ev);
+int rsm_event_record(rsm_ctx* ctx, void* ev, void* stream);
+int rsm_event_elapsed_ms(void* start, void* end, float* ms);
 /* Event-timed extension of `count` in-place squares on the ctx stream, averaged
- * over `reps`: row pass and column pass as separate launches, and `step` = one
- * extension in the production form (the single fused launch where
- * rsm_extend_fused() says so, else the two launches), in milliseconds. */
+ * over `reps`: row pass and column pass (the two launches of one extension) and
+ * `step` = their sum, in milliseconds. */
 int rsm_time_extend(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size, uint32_t count,
                     uint32_t reps, float* row_ms, float* col_ms, float* step_ms);
 

@@ -1,0 +1,36 @@
+/*
+ * rsmt2d_hip_diag.h -- entry points of the DIAGNOSTIC library
+ * (rsmt2d_amd/librsmt2d_hip_diag.so, built by `make -C rsmt2d_amd/csrc diag` with
+ * -DRSM_DIAG).  Measurement tooling only: the product library
+ * (librsmt2d_hip.so, include/rsmt2d_hip.h) contains none of these kernels or
+ * switches, and no environment variable changes its results.
+ */
+#ifndef RSMT2D_HIP_DIAG_H
+#define RSMT2D_HIP_DIAG_H
+
+#include "rsmt2d_hip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Kernel variant of the bit-sliced GF(2^8) M = 128 encode, process-wide:
+ * 40 = production; 0 / 8 / 24 / 56 = A-B variants (exchange form, cache policy);
+ * 2 = no arithmetic, 4 = no global memory (both give WRONG output by design).
+ * rev_col: column pass in reverse set order; xcd: bit 0 rows / bit 1 columns in
+ * XCD-grouped set order. */
+int rsm_diag_set_bs_mode(int mode, int rev_col, int xcd);
+/* Both passes of `count` in-place k = 128 squares in ONE persistent launch
+ * (encode_gf8_bs128f_kernel).  Synchronous; fails if the kernel's bounded wait
+ * timed out (its output is then invalid). */
+int rsm_diag_extend_fused(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size, uint32_t count, uint32_t lag,
+                          void* stream);
+/* ONE launch running the row pass of the squares at d_rows_eds and the column pass
+ * of the squares at d_cols_eds (encode_gf8_bs128p_kernel); either may be NULL. */
+int rsm_diag_extend_pipeline_dev(rsm_ctx* ctx, void* d_rows_eds, void* d_cols_eds, uint32_t k, uint32_t share_size,
+                                 uint32_t count, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RSMT2D_HIP_DIAG_H */

@@ -115,6 +115,38 @@ def extend_square(ods: np.ndarray, nthreads: int = 1) -> np.ndarray:
     return eds
 
 
+_simd = None
+
+
+def simd_lib() -> ctypes.CDLL:
+    """libleopard_simd.so: the same restatement with AVX2 pshufb nibble-table rows
+    (LEO_SIMD) -- bench.py's cpu_baseline only, checked against the scalar oracle in
+    tests/test_oracle.py.  A restatement of klauspost's SIMD technique, not the
+    reference itself (which needs Go and the absent klauspost module)."""
+    global _simd
+    with _lock:
+        if _simd is None:
+            path = os.path.join(_HERE, "libleopard_simd.so")
+            if not os.path.exists(path):
+                build()
+            L = ctypes.CDLL(path)
+            L.leo_extend_square.argtypes = [ctypes.c_uint, ctypes.c_size_t, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_int]
+            L.leo_extend_square.restype = ctypes.c_int
+            _simd = L
+    return _simd
+
+
+def extend_square_simd(ods: np.ndarray, nthreads: int = 1) -> np.ndarray:
+    ods = np.ascontiguousarray(ods, dtype=np.uint8)
+    k, _, S = ods.shape
+    eds = np.empty((2 * k, 2 * k, S), dtype=np.uint8)
+    rc = simd_lib().leo_extend_square(k, S, ods.ctypes.data, eds.ctypes.data, int(nthreads))
+    if rc != 0:
+        raise ValueError(f"leo_extend_square (simd) failed rc={rc}")
+    return eds
+
+
 def tables8():
     e = np.zeros(256, np.uint8)
     lg = np.zeros(256, np.uint8)

@@ -41,6 +41,9 @@ static const unsigned kPoly8 = 0x11D;
 
 static uint8_t exp8[ORD8], log8[ORD8], skew8[MOD8], logwalsh8[ORD8];
 static uint8_t mul8[ORD8][ORD8]; /* mul8[logm][x] = mulLog8(x, logm) */
+#ifdef LEO_SIMD
+static uint8_t nib8[ORD8][2][16];
+#endif
 
 /* ------------------------------------------------------------------------- */
 /* GF(2^16): klauspost leopard.go / catid LeopardFF16.cpp                      */
@@ -202,7 +205,18 @@ static void init16(void) {
 }
 
 static pthread_once_t g_once = PTHREAD_ONCE_INIT;
+#ifdef LEO_SIMD
+static void init_nib8(void) {
+    for (unsigned lm = 0; lm < ORD8; ++lm)
+        for (unsigned v = 0; v < 16; ++v) {
+            nib8[lm][0][v] = mul8[lm][v];
+            nib8[lm][1][v] = mul8[lm][v << 4];
+        }
+}
+static void init_all(void) { init8(); init16(); init_nib8(); }
+#else
 static void init_all(void) { init8(); init16(); }
+#endif
 static void ensure_init(void) { pthread_once(&g_once, init_all); }
 
 /* ------------------------------------------------------------------------- */
@@ -210,6 +224,7 @@ static void ensure_init(void) { pthread_once(&g_once, init_all); }
 /* A GF16 work row is S bytes; per 64-byte block, symbol t (t<32) is          */
 /* lo = row[64b+t], hi = row[64b+32+t]  (klauspost refMulAdd layout, A.6).   */
 /* ------------------------------------------------------------------------- */
+#ifndef LEO_SIMD
 static inline void xor_row(uint8_t *restrict dst, const uint8_t *restrict src, size_t n) {
     for (size_t i = 0; i < n; ++i) dst[i] ^= src[i];
 }
@@ -222,6 +237,44 @@ static inline void mul8_row(uint8_t *restrict dst, const uint8_t *restrict src, 
     const uint8_t *t = mul8[lm];
     for (size_t i = 0; i < n; ++i) dst[i] = t[src[i]];
 }
+#else
+/* LEO_SIMD (libleopard_simd.so, the bench's cpu_baseline only): the same rows with
+ * AVX2, GF(2^8) multiply-by-constant as two 16-entry pshufb nibble tables -- the
+ * technique klauspost/reedsolomon's AVX2 leopard8 path uses (a restatement, not
+ * the reference, which cannot run here).  S % 64 == 0, so rows are whole 32-byte
+ * vectors. */
+#include <immintrin.h>
+/* nib8[logm][lo/hi][nibble] = mulLog8(nibble << 4*hi, logm): see init_nib8 */
+static inline void xor_row(uint8_t *restrict dst, const uint8_t *restrict src, size_t n) {
+    for (size_t i = 0; i < n; i += 32) {
+        __m256i d = _mm256_loadu_si256((const __m256i *)(dst + i));
+        __m256i s = _mm256_loadu_si256((const __m256i *)(src + i));
+        _mm256_storeu_si256((__m256i *)(dst + i), _mm256_xor_si256(d, s));
+    }
+}
+static inline __m256i mul8_v(__m256i x, __m256i tlo, __m256i thi, __m256i m) {
+    __m256i lo = _mm256_and_si256(x, m);
+    __m256i hi = _mm256_and_si256(_mm256_srli_epi64(x, 4), m);
+    return _mm256_xor_si256(_mm256_shuffle_epi8(tlo, lo), _mm256_shuffle_epi8(thi, hi));
+}
+static inline void muladd8(uint8_t *restrict dst, const uint8_t *restrict src, unsigned lm, size_t n) {
+    const __m256i tlo = _mm256_broadcastsi128_si256(_mm_loadu_si128((const __m128i *)nib8[lm][0]));
+    const __m256i thi = _mm256_broadcastsi128_si256(_mm_loadu_si128((const __m128i *)nib8[lm][1]));
+    const __m256i m = _mm256_set1_epi8(0x0F);
+    for (size_t i = 0; i < n; i += 32) {
+        __m256i x = _mm256_loadu_si256((const __m256i *)(src + i));
+        __m256i d = _mm256_loadu_si256((const __m256i *)(dst + i));
+        _mm256_storeu_si256((__m256i *)(dst + i), _mm256_xor_si256(d, mul8_v(x, tlo, thi, m)));
+    }
+}
+static inline void mul8_row(uint8_t *restrict dst, const uint8_t *restrict src, unsigned lm, size_t n) {
+    const __m256i tlo = _mm256_broadcastsi128_si256(_mm_loadu_si128((const __m128i *)nib8[lm][0]));
+    const __m256i thi = _mm256_broadcastsi128_si256(_mm_loadu_si128((const __m128i *)nib8[lm][1]));
+    const __m256i m = _mm256_set1_epi8(0x0F);
+    for (size_t i = 0; i < n; i += 32)
+        _mm256_storeu_si256((__m256i *)(dst + i), mul8_v(_mm256_loadu_si256((const __m256i *)(src + i)), tlo, thi, m));
+}
+#endif
 static inline void muladd16(uint8_t *restrict dst, const uint8_t *restrict src, unsigned lm, size_t n) {
     for (size_t b = 0; b < n; b += 64)
         for (unsigned t = 0; t < 32; ++t) {
@@ -359,16 +412,30 @@ int leo_encode(unsigned k, size_t S, const uint8_t *const *data, uint8_t *const 
     field_t f = {leo_field_bits(k) == 16, leo_field_bits(k) == 16 ? MOD16 : MOD8, S};
     unsigned m = ceil_pow2(k);
     unsigned mtrunc = k < m ? k : m;
-    uint8_t **work = (uint8_t **)malloc(sizeof(uint8_t *) * 2 * m);
-    uint8_t *buf = (uint8_t *)malloc(S * 2 * (size_t)m);
+    /* per-thread grow-only work rows: a fresh 2m*S allocation per codeword is an
+     * mmap/munmap pair (page faults, a process-wide lock) at k=128, S=512 */
+    static __thread uint8_t *tbuf = NULL;
+    static __thread size_t tcap = 0;
+    static __thread uint8_t **twork = NULL;
+    static __thread unsigned twcap = 0;
+    if (tcap < S * 2 * (size_t)m) {
+        free(tbuf);
+        tcap = S * 2 * (size_t)m;
+        tbuf = (uint8_t *)malloc(tcap);
+    }
+    if (twcap < 2 * m) {
+        free(twork);
+        twcap = 2 * m;
+        twork = (uint8_t **)malloc(sizeof(uint8_t *) * twcap);
+    }
+    uint8_t **work = twork;
+    uint8_t *buf = tbuf;
     for (unsigned i = 0; i < 2 * m; ++i) work[i] = buf + (size_t)i * S;
     ifft_dit_encoder(&f, (uint8_t *const *)data, mtrunc, work, m, (long)m - 1);
     /* k <= m always for square codes (parity count == data count), so the
      * "further blocks of m data" loop of the reference never runs. */
     fft_dit(&f, work, k, m);
     for (unsigned i = 0; i < k; ++i) memcpy(parity[i], work[i], S);
-    free(buf);
-    free(work);
     return 0;
 }
 
@@ -451,8 +518,9 @@ typedef struct {
 
 static void encode_vector(unsigned k, size_t S, uint8_t *eds, int is_col, unsigned idx) {
     size_t W = 2 * (size_t)k;
-    const uint8_t **in = (const uint8_t **)malloc(sizeof(uint8_t *) * k);
-    uint8_t **out = (uint8_t **)malloc(sizeof(uint8_t *) * k);
+    const uint8_t *in[32768];
+    uint8_t *out[32768];
+    if (k > 32768) return;
     for (unsigned i = 0; i < k; ++i) {
         if (is_col) {
             in[i] = eds + ((size_t)i * W + idx) * S;
@@ -463,8 +531,6 @@ static void encode_vector(unsigned k, size_t S, uint8_t *eds, int is_col, unsign
         }
     }
     leo_encode(k, S, in, out);
-    free(in);
-    free(out);
 }
 
 static void *ext_worker(void *arg) {

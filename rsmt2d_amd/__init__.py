@@ -82,7 +82,8 @@ class ErrByzantineData(RSMError):
 # library loading
 # ---------------------------------------------------------------------------
 _lib = None
-_lib_lock = threading.Lock()
+# re-entrant: a __del__ run by the garbage collector while the lock is held calls library()
+_lib_lock = threading.RLock()
 _TREE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32,
                             ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32, ctypes.c_uint32,
                             ctypes.POINTER(ctypes.c_uint8), ctypes.POINTER(ctypes.c_uint32))
@@ -103,6 +104,8 @@ _VP, _U8P, _U32, _I32, _I64, _U64 = (ctypes.c_void_p, ctypes.c_void_p, ctypes.c_
 SIGNATURES = {
     "rsm_ctx_create": (_I32, [_I32, ctypes.POINTER(_VP)]),
     "rsm_ctx_destroy": (None, [_VP]),
+    "rsm_ctx_device": (_I32, [_VP]),
+    "rsm_ctx_set_pass_grid": (_I32, [_VP, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     "rsm_last_error": (ctypes.c_char_p, []),
     "rsm_version": (ctypes.c_char_p, []),
     "rsm_device_count": (_I32, []),
@@ -113,6 +116,17 @@ SIGNATURES = {
     "rsm_encode": (_I32, [_VP, _VP, _U32, _U32, _VP]),
     "rsm_decode": (_I32, [_VP, _VP, _VP, _U32, _U32]),
     "rsm_extend_square": (_I32, [_VP, _VP, _U32, _U32, _VP]),
+    "rsm_extend_square_inplace_host": (_I32, [_VP, _VP, _U32, _U32]),
+    "rsm_extend_squares_host": (_I32, [_VP, _VP, _U32, _U32, _U32, _VP]),
+    "rsm_host_alloc": (_I32, [_VP, _U64, ctypes.POINTER(_VP)]),
+    "rsm_host_free": (_I32, [_VP, _VP]),
+    "rsm_multi_create": (_I32, [_VP, ctypes.c_int, ctypes.POINTER(_VP)]),
+    "rsm_multi_destroy": (None, [_VP]),
+    "rsm_multi_size": (_I32, [_VP]),
+    "rsm_multi_context": (_VP, [_VP, ctypes.c_int]),
+    "rsm_multi_extend_square": (_I32, [_VP, _VP, _U32, _U32, _VP, ctypes.c_int]),
+    "rsm_multi_extend_dev": (_I32, [_VP, _VP, _U32, _U32, ctypes.c_int]),
+    "rsm_multi_sync": (_I32, [_VP]),
     "rsm_extend_squares_dev": (_I32, [_VP, _VP, _U32, _U32, _U32, _VP]),
     "rsm_extend_squares_phase_dev": (_I32, [_VP, _VP, _U32, _U32, _U32, _I32, _VP]),
     "rsm_extend_rows_dev": (_I32, [_VP, _VP, _U32, _U32, _U32, _U32, _VP]),
@@ -127,12 +141,10 @@ SIGNATURES = {
     "rsm_memcpy": (_I32, [_VP, _VP, _VP, _U64, _I32]),
     "rsm_dev_fill_random": (_I32, [_VP, _VP, _U64, _U64]),
     "rsm_sync": (_I32, [_VP]),
-    "rsm_extend_fused": (_I32, [_U32, _U32]),
-    "rsm_extend_pipeline_dev": (_I32, [_VP, _VP, _VP, _U32, _U32, _U32, _VP]),
-    "rsm_time_pipeline": (_I32, [_VP, _VP, _VP, _U32, _U32, _U32, _U32, ctypes.POINTER(ctypes.c_float)]),
-    "rsm_set_fused": (_I32, [ctypes.c_int]),
-    "rsm_set_pass_grid": (_I32, [ctypes.c_int, ctypes.c_int]),
-    "rsm_fused_trace": (_I32, [_VP, ctypes.POINTER(ctypes.c_uint32), _U32, ctypes.POINTER(ctypes.c_uint32)]),
+    "rsm_event_create": (_I32, [_VP, ctypes.POINTER(_VP)]),
+    "rsm_event_destroy": (_I32, [_VP]),
+    "rsm_event_record": (_I32, [_VP, _VP, _VP]),
+    "rsm_event_elapsed_ms": (_I32, [_VP, _VP, ctypes.POINTER(ctypes.c_float)]),
     "rsm_stream_create": (_I32, [_VP, ctypes.POINTER(_VP)]),
     "rsm_stream_destroy": (_I32, [_VP, _VP]),
     "rsm_stream_sync": (_I32, [_VP]),
@@ -158,14 +170,49 @@ SIGNATURES = {
 }
 
 
-def build() -> str:
-    """Compile librsmt2d_hip.so for gfx950 (make in rsmt2d_amd/csrc)."""
+#: entry points of the diagnostic library only (include/rsmt2d_hip_diag.h)
+DIAG_SIGNATURES = {
+    "rsm_diag_set_bs_mode": (_I32, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "rsm_diag_extend_fused": (_I32, [_VP, _VP, _U32, _U32, _U32, _U32, _VP]),
+    "rsm_diag_extend_pipeline_dev": (_I32, [_VP, _VP, _VP, _U32, _U32, _U32, _VP]),
+}
+DIAG_LIB_PATH = os.path.join(_HERE, "librsmt2d_hip_diag.so")
+
+
+def build(diag: bool = True) -> str:
+    """Compile librsmt2d_hip.so for gfx950 (make in rsmt2d_amd/csrc); with ``diag``
+    also the measurement-only librsmt2d_hip_diag.so (-DRSM_DIAG)."""
     subprocess.run(["make", "-s", "-j8", "-C", os.path.join(_HERE, "csrc")], check=True)
+    if diag:
+        subprocess.run(["make", "-s", "-j8", "-C", os.path.join(_HERE, "csrc"), "diag"], check=True)
     return LIB_PATH
+
+
+_diag = None
+
+
+def diag_library() -> ctypes.CDLL:
+    """The DIAGNOSTIC library (A-B / no-arithmetic / fused kernels): measurement
+    tooling, never the product.  It carries its own HIP state: do not mix its
+    contexts with library()'s."""
+    global _diag
+    with _lib_lock:
+        if _diag is None:
+            if not os.path.exists(DIAG_LIB_PATH):
+                raise DeviceError(RSM_EDEVICE, f"{DIAG_LIB_PATH} is missing: run rsmt2d_amd.build()")
+            L = ctypes.CDLL(DIAG_LIB_PATH)
+            for name, (res, args) in list(SIGNATURES.items()) + list(DIAG_SIGNATURES.items()):
+                f = getattr(L, name)
+                f.restype = res
+                f.argtypes = args
+            _diag = L
+    return _diag
 
 
 def library() -> ctypes.CDLL:
     global _lib
+    if _lib is not None:
+        return _lib
     with _lib_lock:
         if _lib is None:
             if not os.path.exists(LIB_PATH):
@@ -190,6 +237,13 @@ def _err(rc: int) -> RSMError:
 def _check(rc: int) -> None:
     if rc != RSM_OK:
         raise _err(rc)
+
+
+def _check_with(L: ctypes.CDLL, rc: int) -> None:
+    """_check for a call into another copy of the ABI (the diagnostic library)."""
+    if rc != RSM_OK:
+        msg = (L.rsm_last_error() or b"").decode(errors="replace")
+        raise (DeviceError if rc == RSM_EDEVICE else RSMError)(rc, msg)
 
 
 _ctx = {}

@@ -22,12 +22,58 @@
 
 using namespace rsm;
 
+// Host bytes of a square: pinned (hipHostMalloc) whenever a HIP runtime is
+// usable, so Repair's square upload and download are direct DMA; plain memory on
+// a host without a GPU (Import/New are host-only operations).
+struct HostSquare {
+    uint8_t* p = nullptr;
+    size_t n = 0;
+    bool pinned = false;
+    HostSquare() = default;
+    HostSquare(const HostSquare&) = delete;
+    HostSquare& operator=(const HostSquare&) = delete;
+    ~HostSquare() { release(); }
+    void release() {
+        if (p) {
+            if (pinned) (void)hipHostFree(p);
+            else free(p);
+        }
+        p = nullptr;
+        n = 0;
+    }
+    bool assign(size_t bytes) {  // zero-filled
+        release();
+        if (bytes == 0) return true;
+        void* q = nullptr;
+        if (hipHostMalloc(&q, bytes, hipHostMallocDefault) == hipSuccess) {
+            pinned = true;
+        } else {
+            (void)hipGetLastError();
+            q = malloc(bytes);
+            pinned = false;
+            if (!q) return false;
+        }
+        p = static_cast<uint8_t*>(q);
+        n = bytes;
+        memset(p, 0, n);
+        return true;
+    }
+    uint8_t* data() { return p; }
+    const uint8_t* data() const { return p; }
+    size_t size() const { return n; }
+    void swap(HostSquare& o) {
+        std::swap(p, o.p);
+        std::swap(n, o.n);
+        std::swap(pinned, o.pinned);
+    }
+};
+
 struct rsm_eds {
     rsm_ctx* ctx = nullptr;
     uint32_t width = 0;
     uint32_t odw = 0;  // originalDataWidth
     uint32_t S = 0;    // shareSize
-    std::vector<uint8_t> data;     // width*width*S, row-major
+    HostSquare data;               // width*width*S, row-major
     std::vector<uint8_t> present;  // width*width
     std::vector<uint8_t> byz_data;
     std::vector<uint8_t> byz_present;
@@ -74,9 +120,12 @@ rsm_eds* alloc_eds(rsm_ctx* ctx, uint32_t width, uint32_t S) {
     e->width = width;
     e->S = S;
     try {
-        e->data.assign((size_t)width * width * S, 0);
         e->present.assign((size_t)width * width, 0);
     } catch (...) {
+        delete e;
+        return nullptr;
+    }
+    if (!e->data.assign((size_t)width * width * S)) {
         delete e;
         return nullptr;
     }
@@ -175,20 +224,21 @@ struct DevSquare {
     uint32_t* d_flags = nullptr;
     hipStream_t st;
 
+    // caller holds c->eds_mu (the buffers and the context stream are the EDS layer's)
     int init(rsm_ctx* c, uint32_t width, uint32_t share_size) {
         ctx = c;
         W = width;
         k = width / 2;
         S = share_size;
         st = c->stream;
-        hipError_t e = hipSetDevice(c->device);
-        if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+        if (int rc = use_device(c)) return rc;
+        hipError_t e;
         const size_t sq = (size_t)W * W * S;
-        DevBuf& a = c->dev_buf(10);
-        DevBuf& b = c->dev_buf(11);
-        DevBuf& p = c->dev_buf(12);
-        DevBuf& ix = c->dev_buf(13);
-        DevBuf& fl = c->dev_buf(14);
+        DevBuf& a = c->eds.eds;
+        DevBuf& b = c->eds.scratch;
+        DevBuf& p = c->eds.pres;
+        DevBuf& ix = c->eds.idx;
+        DevBuf& fl = c->eds.flags;
         if ((e = a.ensure(sq)) != hipSuccess || (e = b.ensure(sq)) != hipSuccess ||
             (e = p.ensure((size_t)W * W + 64)) != hipSuccess || (e = ix.ensure(sizeof(uint32_t) * (2 * W + 16))) != hipSuccess ||
             (e = fl.ensure(sizeof(uint32_t) * (2 * W + 16))) != hipSuccess)
@@ -489,7 +539,7 @@ int fast_repair(rsm_eds* e, DevSquare& dev, const uint8_t* row_roots, const uint
     // device check runs before any copy back, so an accepted square lands straight
     // in the EDS's own (already resident) buffer and a rejected one costs no D2H.
     if (tree.is_default() && root_len == 32 && roots_dev_supported(W)) {
-        DevBuf& rb = dev.ctx->dev_buf(31);
+        DevBuf& rb = dev.ctx->eds.roots;
         if ((r = rb.ensure((size_t)2 * W * 32)) != hipSuccess) return hip_fail(r, "hipMalloc (roots)");
         if (int rc = device_roots(dev.ctx, dev.d_eds, W, e->S, static_cast<uint8_t*>(rb.ptr), dev.st)) return rc;
         std::vector<uint8_t> got((size_t)2 * W * 32);
@@ -507,7 +557,6 @@ int fast_repair(rsm_eds* e, DevSquare& dev, const uint8_t* row_roots, const uint
             e->stats.fallback_reason = kFallbackRoots;
             return 1;
         }
-        if (e->data.size() != (size_t)W * W * S) e->data.resize((size_t)W * W * S);
         if ((r = hipMemcpyAsync(e->data.data(), dev.d_eds, e->data.size(), hipMemcpyDeviceToHost, dev.st)) !=
             hipSuccess)
             return hip_fail(r, "D2H square");
@@ -516,7 +565,8 @@ int fast_repair(rsm_eds* e, DevSquare& dev, const uint8_t* row_roots, const uint
         e->stats.fast_path = 1;
         return RSM_OK;
     }
-    std::vector<uint8_t> repaired((size_t)W * W * S);
+    HostSquare repaired;
+    if (!repaired.assign((size_t)W * W * S)) return fail(RSM_ENOMEM, "Repair: out of memory");
     if ((r = hipMemcpyAsync(&mismatch, dev.d_flags, 4, hipMemcpyDeviceToHost, dev.st)) != hipSuccess)
         return hip_fail(r, "D2H flag");
     if ((r = hipMemcpyAsync(repaired.data(), dev.d_eds, repaired.size(), hipMemcpyDeviceToHost, dev.st)) != hipSuccess)
@@ -573,9 +623,11 @@ int rsm_eds_compute(rsm_ctx* ctx, const uint8_t* const* data, const uint32_t* le
     if (!e) return fail(RSM_ENOMEM, "rsm_eds_compute: out of memory");
     e->odw = k;
     if (k > 0) {
-        std::vector<uint8_t> ods((size_t)k * k * S);
-        for (uint64_t i = 0; i < n; ++i) memcpy(ods.data() + i * S, data[i], S);
-        int rc = rsm_extend_square(ctx, ods.data(), k, S, e->data.data());
+        // gather the ODS straight into the (pinned) EDS's Q0 quadrant, then extend
+        // in place from there (rsm_extend_square leaves Q0 alone when ods == eds's Q0)
+        const size_t row = (size_t)2 * k * S;
+        for (uint64_t i = 0; i < n; ++i) memcpy(e->data.data() + (i / k) * row + (i % k) * S, data[i], S);
+        int rc = rsm_extend_square_inplace_host(ctx, e->data.data(), k, S);
         if (rc) {
             delete e;
             return rc;
@@ -675,12 +727,12 @@ int rsm_eds_roots(rsm_eds* e, int axis, rsm_tree_root_fn tree_fn, void* user, ui
         std::all_of(e->present.begin(), e->present.end(), [](uint8_t p) { return p != 0; })) {
         // complete square + DefaultTree: every leaf and node hash on the GPU
         const uint32_t W = e->width;
-        std::lock_guard<std::mutex> lk(e->ctx->mu);
+        std::lock_guard<std::mutex> lk(e->ctx->eds_mu);
         DevSquare dev{};
         if (int rc = dev.init(e->ctx, W, e->S)) return rc;
         hipError_t r = hipMemcpyAsync(dev.d_eds, e->data.data(), e->data.size(), hipMemcpyHostToDevice, dev.st);
         if (r != hipSuccess) return hip_fail(r, "H2D square");
-        DevBuf& rb = e->ctx->dev_buf(31);
+        DevBuf& rb = e->ctx->eds.roots;
         if ((r = rb.ensure((size_t)2 * W * 32)) != hipSuccess) return hip_fail(r, "hipMalloc (roots)");
         if (int rc = device_roots(e->ctx, dev.d_eds, W, e->S, static_cast<uint8_t*>(rb.ptr), dev.st)) return rc;
         std::vector<uint8_t> got((size_t)W * 32);
@@ -731,7 +783,7 @@ int rsm_eds_repair(rsm_eds* e, const uint8_t* row_roots, const uint8_t* col_root
     Tree tree{tree_fn, user};
     DevSquare dev{};
     {
-        std::lock_guard<std::mutex> lk(e->ctx->mu);
+        std::lock_guard<std::mutex> lk(e->ctx->eds_mu);
         if (int rc = dev.init(e->ctx, e->width, e->S)) return rc;
         if (int rc = pre_repair_sanity_check(e, dev, row_roots, col_roots, root_len, tree, byz)) return rc;
         bool complete = true;

@@ -537,14 +537,18 @@ inline uint32_t blocks_for(uint64_t tasks) { return (uint32_t)((tasks + 3) / 4);
 // stay in the Infinity Cache between the passes is SLOWER (175 vs 196 GiB/s, 0.90
 // vs 0.77 ms) than one launch triple over up to 1 GiB of work arrays -- the extra
 // launches cost more than the HBM round trips they save.  RSM_GF16_BATCH_MB
-// overrides (A/B measurements).
+// overrides it in the diagnostic build only (A/B measurements).
 static uint64_t gf16_batch_bytes() {
+#ifdef RSM_DIAG
     static const uint64_t b = [] {
         const char* v = getenv("RSM_GF16_BATCH_MB");
         const uint64_t mb = v ? strtoull(v, nullptr, 10) : 0;
         return (mb ? mb : 1024ull) << 20;
     }();
     return b;
+#else
+    return 1024ull << 20;
+#endif
 }
 
 template <int M>

@@ -428,13 +428,19 @@ static hipError_t launch_enc(const CodewordSet& cs, hipStream_t st) {
     return hipGetLastError();
 }
 
-// RSM_GF8_KERNEL=table forces the byte-table kernel for M = 128 (A/B measurements).
+// Diagnostic build only: RSM_GF8_KERNEL=table forces the byte-table kernel for
+// M = 128 (A/B measurements).  The product library always takes the bit-sliced
+// kernel where it applies.
 static bool bs128_enabled() {
+#ifdef RSM_DIAG
     static const bool on = [] {
         const char* v = getenv("RSM_GF8_KERNEL");
         return !(v && strcmp(v, "table") == 0);
     }();
     return on;
+#else
+    return true;
+#endif
 }
 
 hipError_t launch_encode_gf8(const CodewordSet& cs, hipStream_t st) {

@@ -28,7 +28,6 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <atomic>
-#include <cstdlib>
 #include "bs8.hpp"
 #include "rsm_kernels.hpp"
 
@@ -337,6 +336,7 @@ __global__ __launch_bounds__(512, 1) void encode_gf8_bs128u_kernel(CodewordSet c
 }
 
 
+#ifdef RSM_DIAG
 // ---------------------------------------------------------------------------
 // Fused two-pass extension (FusedPlan, rsm_kernels.hpp).  Items are handed out by
 // one device-scope queue head in this order: the row sets of squares 0..lag-1,
@@ -686,6 +686,8 @@ __global__ __launch_bounds__(512, 1) void encode_gf8_bs128p_kernel(DualPlan p) {
     bs_dual_wave<MODE>(p, (uint32_t)(uintptr_t)lds, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
 }
 
+#endif  // RSM_DIAG
+
 }  // namespace
 
 
@@ -700,82 +702,57 @@ bool bs128_applicable(const CodewordSet& cs) {
     return span + sym < kOobBs;
 }
 
-static uint32_t device_cus() {
-    static const uint32_t n = [] {
-        int dev = 0, cus = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-            cus = 256;
-        return (uint32_t)cus;
-    }();
-    return n;
+// Production launch: MODE 40 (ds_write_addtid_b32 exchange + non-temporal loads,
+// measured best: profiles/r01e_bench_ab.txt); the column pass walks its sets in
+// reverse order (its first reads are the squares the row pass wrote last).  The
+// persistent grid is the caller's (the context's CU count or per-pass cap).
+#ifdef RSM_DIAG
+static std::atomic<int> g_diag_mode{40};
+static std::atomic<int> g_diag_rev{1};
+static std::atomic<int> g_diag_xcd{0};
+void set_bs128_diag_mode(int mode, int rev_col, int xcd) {
+    g_diag_mode.store(mode);
+    g_diag_rev.store(rev_col);
+    g_diag_xcd.store(xcd);
 }
-
-static std::atomic<int> g_pass_cap[2] = {-1, -1};
-uint32_t pass_grid_cap(int pass) {
-    int v = g_pass_cap[pass].load(std::memory_order_relaxed);
-    if (v < 0) {
-        const char* e = getenv(pass == 0 ? "RSM_BS_ROWGRID" : "RSM_BS_COLGRID");
-        v = e ? atoi(e) : 0;
-        if (v < 0) v = 0;
-        g_pass_cap[pass].store(v, std::memory_order_relaxed);
-    }
-    return (uint32_t)v;
-}
-int set_pass_grid_cap(int pass, int cus) {
-    const int prev = (int)pass_grid_cap(pass);
-    g_pass_cap[pass].store(cus > 0 ? cus : 0, std::memory_order_relaxed);
-    return prev;
-}
+#endif
 
 hipError_t launch_encode_gf8_bs128(const CodewordSet& cs, hipStream_t st) {
     const uint64_t sets = ((uint64_t)cs.count * cs.S + kSetBytes - 1) / kSetBytes;
     if (sets == 0) return hipSuccess;
-    uint32_t grid = (uint32_t)(sets < device_cus() ? sets : device_cus());
-    // Persistent-grid caps (rsm_set_pass_grid; env RSM_BS_ROWGRID / RSM_BS_COLGRID):
-    // a row pass on fewer CUs leaves the rest to a column pass running on another
-    // stream (profiles/r01h_grid_ab.txt)
-    {
-        const uint32_t cap = pass_grid_cap(cs.elem_stride == cs.S ? 0 : 1);
-        if (cap > 0 && cap < grid) grid = cap;
-    }
-    // RSM_BS_MODE: 40 production (addtid exchange + non-temporal loads: measured best,
-    // profiles/r01e_bench_ab.txt); A/B: 0 ds_write_b32 exchange, 8 default-policy
-    // loads, 24 nt stores, 56 nt loads + stores; diagnostics 2 = no arithmetic, 4 = no
-    // global memory (wrong output)
-    // RSM_BS_REV=0: column pass in forward set order (A/B of the cache-reuse order)
-    static const int mode = [] {
-        const char* v = getenv("RSM_BS_MODE");
-        return v ? atoi(v) : 40;
-    }();
-    static const uint32_t rev_col = [] {
-        const char* v = getenv("RSM_BS_REV");
-        return v ? (uint32_t)(atoi(v) != 0) : 1u;
-    }();
-    const bool row = cs.elem_stride == cs.S;
-    // RSM_BS_XCD=1: XCD-grouped set order (A/B)
-    static const uint32_t xcd = [] {
-        const char* v = getenv("RSM_BS_XCD");
-        return v ? (uint32_t)(atoi(v) & 3) : 0u;
-    }();
-    const uint32_t rev = (row ? 0u : rev_col) | (((xcd >> (row ? 0 : 1)) & 1u) << 1);
+    const uint32_t cap = cs.grid ? cs.grid : 256u;
+    const uint32_t grid = (uint32_t)(sets < cap ? sets : cap);
+    const bool row = cs.pass == 0;
 #define RSM_BS_LAUNCH(m, p) \
     hipLaunchKernelGGL((encode_gf8_bs128u_kernel<m, p>), dim3(grid), dim3(512), 0, st, cs, (uint32_t)sets, rev)
-    switch (mode) {
-        case 2: RSM_BS_LAUNCH(10, 1); break;  // diagnostics (wrong output)
-        case 4: RSM_BS_LAUNCH(12, 1); break;
-        case 0: RSM_BS_LAUNCH(0, 1); break;   // A/B variants
-        case 8: RSM_BS_LAUNCH(8, 1); break;
-        case 24: RSM_BS_LAUNCH(24, 1); break;
-        case 56: RSM_BS_LAUNCH(56, 1); break;
-        default:
-            if (row) RSM_BS_LAUNCH(40, 0);
-            else RSM_BS_LAUNCH(40, 1);
+#ifdef RSM_DIAG
+    {
+        const int mode = g_diag_mode.load();
+        const uint32_t xcd = (uint32_t)g_diag_xcd.load();
+        const uint32_t rev = (row ? 0u : (uint32_t)g_diag_rev.load()) | (((xcd >> (row ? 0 : 1)) & 1u) << 1);
+        switch (mode) {
+            case 2: RSM_BS_LAUNCH(10, 1); return hipGetLastError();  // no arithmetic (wrong output)
+            case 4: RSM_BS_LAUNCH(12, 1); return hipGetLastError();  // no global memory (wrong output)
+            case 0: RSM_BS_LAUNCH(0, 1); return hipGetLastError();   // A/B variants
+            case 8: RSM_BS_LAUNCH(8, 1); return hipGetLastError();
+            case 24: RSM_BS_LAUNCH(24, 1); return hipGetLastError();
+            case 56: RSM_BS_LAUNCH(56, 1); return hipGetLastError();
+            default: break;
+        }
+        if (row) RSM_BS_LAUNCH(40, 0);
+        else RSM_BS_LAUNCH(40, 1);
+        return hipGetLastError();
     }
+#else
+    const uint32_t rev = row ? 0u : 1u;
+    if (row) RSM_BS_LAUNCH(40, 0);
+    else RSM_BS_LAUNCH(40, 1);
+#endif
 #undef RSM_BS_LAUNCH
     return hipGetLastError();
 }
 
+#ifdef RSM_DIAG
 // The fused launch needs whole sets per square in both passes (k * S a multiple of
 // 2 KiB: every k = 128 square) and the plain row/column CodewordSets to qualify.
 bool bs128_fused_applicable(const CodewordSet& rows, const CodewordSet& cols) {
@@ -785,7 +762,8 @@ bool bs128_fused_applicable(const CodewordSet& rows, const CodewordSet& cols) {
 
 hipError_t launch_extend_gf8_bs128_fused(const FusedPlan& p, hipStream_t st) {
     if (p.total == 0) return hipSuccess;
-    const uint32_t grid = p.total < device_cus() ? p.total : device_cus();
+    const uint32_t cap = p.rows.grid ? p.rows.grid : 256u;
+    const uint32_t grid = p.total < cap ? p.total : cap;
     hipLaunchKernelGGL((encode_gf8_bs128f_kernel<40>), dim3(grid), dim3(512), 0, st, p);
     return hipGetLastError();
 }
@@ -793,9 +771,11 @@ hipError_t launch_extend_gf8_bs128_fused(const FusedPlan& p, hipStream_t st) {
 hipError_t launch_encode_gf8_bs128_dual(const DualPlan& p, hipStream_t st) {
     const uint32_t sets = p.na + p.nb;
     if (sets == 0) return hipSuccess;
-    const uint32_t grid = sets < device_cus() ? sets : device_cus();
+    const uint32_t cap = p.a.grid ? p.a.grid : 256u;
+    const uint32_t grid = sets < cap ? sets : cap;
     hipLaunchKernelGGL((encode_gf8_bs128p_kernel<40>), dim3(grid), dim3(512), 0, st, p);
     return hipGetLastError();
 }
+#endif  // RSM_DIAG
 
 }  // namespace rsm

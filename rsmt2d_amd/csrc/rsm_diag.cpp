@@ -1,0 +1,120 @@
+// rsm_diag.cpp -- entry points of the DIAGNOSTIC library only (librsmt2d_hip_diag.so,
+// `make diag`, compiled with -DRSM_DIAG).  Nothing here is part of the product
+// library: the A/B kernel variants (no-arithmetic / no-memory modes give wrong
+// output by design), the fused single-launch extension and the software-pipelined
+// dual launch were measured no faster than the production two-launch schedule
+//  and stay available for measurements.
+#ifndef RSM_DIAG
+#error "rsm_diag.cpp belongs to the diagnostic build (-DRSM_DIAG)"
+#endif
+#include "../../include/rsmt2d_hip_diag.h"
+#include "rsm_internal.hpp"
+
+using namespace rsm;
+
+namespace {
+
+CodewordSet rows_of(uint8_t* d_eds, uint32_t k, uint32_t S, uint32_t count, uint32_t grid) {
+    const uint64_t W = 2ull * k;
+    CodewordSet rows{};
+    rows.base = rows.out_base = d_eds;
+    rows.square_stride = W * W * S;
+    rows.cw_stride = W * S;
+    rows.elem_stride = S;
+    rows.out_offset = (uint64_t)k * S;
+    rows.per_square = k;
+    rows.count = k * count;
+    rows.k = k;
+    rows.S = S;
+    rows.pass = 0;
+    rows.grid = grid;
+    return rows;
+}
+
+CodewordSet cols_of(uint8_t* d_eds, uint32_t k, uint32_t S, uint32_t count, uint32_t grid) {
+    CodewordSet cols = rows_of(d_eds, k, S, count, grid);
+    const uint64_t W = 2ull * k;
+    cols.cw_stride = S;
+    cols.elem_stride = W * S;
+    cols.out_offset = (uint64_t)k * W * S;
+    cols.per_square = (uint32_t)W;
+    cols.count = (uint32_t)W * count;
+    cols.pass = 1;
+    return cols;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rsm_diag_set_bs_mode(int mode, int rev_col, int xcd) {
+    set_bs128_diag_mode(mode, rev_col, xcd);
+    return RSM_OK;
+}
+
+// Both passes of `count` in-place k = 128 squares as ONE persistent launch (the
+// row sets of square s + lag interleaved with the column sets of square s).
+// Synchronous: reads back the kernel's stuck-wait flag and fails if it is set.
+int rsm_diag_extend_fused(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size, uint32_t count, uint32_t lag,
+                          void* stream) {
+    if (!ctx || !d_eds || k != 128 || validate_chunk_size(share_size) != RSM_OK ||
+        ((uint64_t)k * share_size) % 2048 != 0)
+        return fail(RSM_EINVAL, "rsm_diag_extend_fused: needs k = 128 and k * S a multiple of 2 KiB");
+    if (count == 0) return RSM_OK;
+    if (int rc = use_device(ctx)) return rc;
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    FusedPlan p{};
+    p.rows = rows_of(static_cast<uint8_t*>(d_eds), k, share_size, count, ctx->cus);
+    p.cols = cols_of(static_cast<uint8_t*>(d_eds), k, share_size, count, ctx->cus);
+    if (!bs128_fused_applicable(p.rows, p.cols)) return fail(RSM_EUNSUPPORTED, "fused extension not applicable");
+    p.count = count;
+    p.lag = lag < 1 ? 1 : (lag > count ? count : lag);
+    p.rn = (uint32_t)((uint64_t)k * share_size / 2048);
+    p.cn = 2 * p.rn;
+    p.total = count * (p.rn + p.cn);
+    StreamScratch& ss = stream_scratch(ctx, st);
+    std::lock_guard<std::mutex> lk(ss.mu);
+    const size_t words = (size_t)count + 3;
+    hipError_t e = hipStreamSynchronize(st);
+    if (e == hipSuccess) e = ss.leaf.ensure(words * 4);  // the stream's scratch doubles as the queue words
+    if (e == hipSuccess) e = hipMemsetAsync(ss.leaf.ptr, 0, words * 4, st);
+    if (e != hipSuccess) return hip_fail(e, "fused extension: queue words");
+    p.ctr = static_cast<uint32_t*>(ss.leaf.ptr);
+    if ((e = launch_extend_gf8_bs128_fused(p, st)) != hipSuccess) return hip_fail(e, "fused extension launch");
+    uint32_t stuck = 0;
+    if ((e = hipMemcpyAsync(&stuck, p.ctr + 2, 4, hipMemcpyDeviceToHost, st)) != hipSuccess ||
+        (e = hipStreamSynchronize(st)) != hipSuccess)
+        return hip_fail(e, "fused extension: error flag");
+    if (stuck) return fail(RSM_EDEVICE, "fused extension: a column set timed out waiting for its rows (output invalid)");
+    return RSM_OK;
+}
+
+// ONE launch running the row pass of the squares at d_rows_eds and the column pass
+// of the squares at d_cols_eds (either may be NULL; the batches must not overlap).
+int rsm_diag_extend_pipeline_dev(rsm_ctx* ctx, void* d_rows_eds, void* d_cols_eds, uint32_t k, uint32_t share_size,
+                                 uint32_t count, void* stream) {
+    if (!ctx || k == 0 || (!d_rows_eds && !d_cols_eds)) return fail(RSM_EINVAL, "rsm_diag_extend_pipeline_dev: bad arguments");
+    if (int rc = validate_chunk_size(share_size)) return rc;
+    if (count == 0) return RSM_OK;
+    if (int rc = use_device(ctx)) return rc;
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    const CodewordSet rows = rows_of(static_cast<uint8_t*>(d_rows_eds), k, share_size, count, ctx->cus);
+    const CodewordSet cols = cols_of(static_cast<uint8_t*>(d_cols_eds), k, share_size, count, ctx->cus);
+    const bool dual = field_bits(k) == 8 && d_rows_eds && d_cols_eds && bs128_applicable(rows) && bs128_applicable(cols);
+    if (!dual) {
+        if (d_rows_eds)
+            if (int rc = extend_squares(ctx, static_cast<uint8_t*>(d_rows_eds), k, share_size, count, st, 1)) return rc;
+        if (d_cols_eds)
+            if (int rc = extend_squares(ctx, static_cast<uint8_t*>(d_cols_eds), k, share_size, count, st, 2)) return rc;
+        return RSM_OK;
+    }
+    DualPlan p{};
+    p.a = rows;
+    p.b = cols;
+    p.na = (uint32_t)(((uint64_t)rows.count * share_size + 2047) / 2048);
+    p.nb = (uint32_t)(((uint64_t)cols.count * share_size + 2047) / 2048);
+    hipError_t e = launch_encode_gf8_bs128_dual(p, st);
+    return e == hipSuccess ? RSM_OK : hip_fail(e, "pipelined extension kernel launch");
+}
+
+}  // extern "C"

@@ -2,11 +2,14 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <condition_variable>
 #include <cstdint>
 #include <map>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "../../include/rsmt2d_hip.h"
 #include "gf16.hpp"
@@ -20,7 +23,9 @@ const char* last_error();
 int validate_chunk_size(int64_t share_size);
 int field_bits(uint32_t k);
 
-// Grow-only device / pinned-host scratch buffers owned by a context.
+// Grow-only device / pinned-host scratch buffers.  Not synchronised: every
+// instance below has exactly one owner (a lane, a stream's scratch under its own
+// mutex, or the EDS state under rsm_ctx::eds_mu).
 struct DevBuf {
     void* ptr = nullptr;
     size_t cap = 0;
@@ -40,51 +45,88 @@ struct HostBuf {
     hipError_t ensure(size_t n);
 };
 
+// Per-call resources of the Codec / host-memory entry points: rsmt2d calls
+// Encode/Decode from up to 2k goroutines at once (extendeddatasquare.go:186-224),
+// so each call takes a lane (own stream + pinned staging + device staging) from a
+// pool instead of serialising on one context lock.
+struct Lane {
+    hipStream_t stream = nullptr;
+    HostBuf host;
+    DevBuf dev, aux;
+};
+
+// Device scratch that belongs to one stream: kernels queued on different streams
+// never share it.  `mu` is held while the scratch is grown AND while the launches
+// that use it are enqueued.
+struct StreamScratch {
+    std::mutex mu;
+    DevBuf gf16_work, gf16_errs;  // GF(2^16) work arrays / error locators
+    DevBuf leaf;                  // DefaultTree leaf digests (device roots)
+};
+
+// Buffers of the ExtendedDataSquare layer (Repair, device roots of an EDS):
+// used only under rsm_ctx::eds_mu, on the context stream.
+struct EdsBufs {
+    DevBuf eds, scratch, pres, idx, flags, roots;
+    HostBuf staging;  // pinned: square upload / download
+};
+
 }  // namespace rsm
 
 struct rsm_ctx {
     int device = 0;
+    uint32_t cus = 256;          // compute units of `device` (persistent-grid size)
     hipStream_t stream = nullptr;
-    std::mutex mu;       // serialises API calls that use the context's staging buffers
-    std::mutex gf16_mu;  // guards gf16 table upload / scratch growth
-    std::map<int, std::unique_ptr<rsm::DevBuf>> bufs;
-    std::map<int, std::unique_ptr<rsm::HostBuf>> hbufs;
-    // queue/counter words of the fused extension kernel, one buffer per stream (two
-    // launches in flight on different streams must not share a queue)
-    std::mutex fused_mu;
-    std::map<void*, std::unique_ptr<rsm::DevBuf>> fused_ctr;
-    uint32_t fused_trace_n = 0;  // items of the last traced fused launch (RSM_FUSED_TRACE)
-    uint32_t* d_zero_index = nullptr;
-    rsm::Gf16Dev gf16{};
-    bool gf16_ready = false;
+    std::atomic<uint32_t> pass_grid[2] = {0, 0};  // rsm_ctx_set_pass_grid (0 = all CUs)
 
-    rsm::DevBuf& dev_buf(int slot) {
-        auto& p = bufs[slot];
-        if (!p) p = std::make_unique<rsm::DevBuf>();
-        return *p;
-    }
-    rsm::HostBuf& host_buf(int slot) {
-        auto& p = hbufs[slot];
-        if (!p) p = std::make_unique<rsm::HostBuf>();
-        return *p;
-    }
-    // Device array holding a single 0 (index list of a one-codeword decode).
-    const uint32_t* zero_index() {
-        if (!d_zero_index) {
-            rsm::DevBuf& b = dev_buf(-1);
-            if (b.ensure(64) != hipSuccess) return nullptr;
-            if (hipMemsetAsync(b.ptr, 0, 64, stream) != hipSuccess) return nullptr;
-            d_zero_index = static_cast<uint32_t*>(b.ptr);
-        }
-        return d_zero_index;
-    }
+    // lane pool (Codec calls, host-memory extension)
+    static constexpr size_t kMaxLanes = 32;
+    std::mutex lane_mu;
+    std::condition_variable lane_cv;
+    std::vector<std::unique_ptr<rsm::Lane>> lanes;
+    std::vector<rsm::Lane*> free_lanes;
+
+    // per-stream scratch
+    std::mutex scratch_mu;  // guards the map only
+    std::map<hipStream_t, std::unique_ptr<rsm::StreamScratch>> scratch;
+
+    // GF(2^16) tables, uploaded once
+    std::mutex gf16_mu;
+    bool gf16_ready = false;
+    rsm::DevBuf gf16_perm, gf16_skew, gf16_logwalsh;
+    rsm::Gf16Dev gf16{};  // table pointers only (scratch comes per stream)
+
+    rsm::DevBuf zero_index;  // one device u32 = 0 (index list of a single-codeword decode)
+
+    std::mutex eds_mu;
+    rsm::EdsBufs eds;
 };
 
 namespace rsm {
 
-// GF(2^16) tables on the context's device (uploaded once) + scratch sized for
-// `scratch_bytes` of work arrays.  Returns RSM_OK or an RSM_E* code.
-int ensure_gf16(rsm_ctx* ctx, uint64_t scratch_bytes, uint64_t errs_bytes);
+// Lane pool: blocks while all kMaxLanes lanes are busy.
+Lane* acquire_lane(rsm_ctx* ctx, int* rc);
+void release_lane(rsm_ctx* ctx, Lane* l);
+struct LaneGuard {
+    rsm_ctx* ctx;
+    Lane* lane;
+    int rc = RSM_OK;
+    explicit LaneGuard(rsm_ctx* c) : ctx(c), lane(acquire_lane(c, &rc)) {}
+    ~LaneGuard() {
+        if (lane) release_lane(ctx, lane);
+    }
+    LaneGuard(const LaneGuard&) = delete;
+    LaneGuard& operator=(const LaneGuard&) = delete;
+};
+
+StreamScratch& stream_scratch(rsm_ctx* ctx, hipStream_t st);
+
+// GF(2^16) tables on the context's device (uploaded once).  Returns RSM_OK or an RSM_E* code.
+int ensure_gf16_tables(rsm_ctx* ctx);
+
+// Selects the context's device on the calling thread (cgo moves goroutines
+// between OS threads; the HIP current device is per thread).
+int use_device(rsm_ctx* ctx);
 
 int launch_encode(rsm_ctx* ctx, const CodewordSet& cs, hipStream_t st);
 int launch_decode(rsm_ctx* ctx, const DecodeSet& ds, hipStream_t st);

@@ -31,6 +31,9 @@ struct CodewordSet {
     uint32_t k;
     uint32_t S;       // share size in bytes (multiple of 64)
     uint32_t chunks;  // ceil(S / bytes-per-wave)
+    uint32_t pass;    // 0 = row pass of a square, 1 = column pass / anything else (launch shape)
+    uint32_t grid;    // persistent-grid size (workgroups) of the bit-sliced launch: the
+                      // context's CU count or its per-pass cap (rsm_ctx_set_pass_grid)
 };
 
 // A list of row (axis 0) or column (axis 1) vectors of ONE [W][W][S] square to
@@ -46,6 +49,28 @@ struct DecodeSet {
     uint32_t chunks;
 };
 
+hipError_t launch_encode_gf8(const CodewordSet& cs, hipStream_t st);
+// bit-sliced M = 128 encode (kernels_gf8_bs.hip); launch_encode_gf8 picks it when applicable
+bool bs128_applicable(const CodewordSet& cs);
+hipError_t launch_encode_gf8_bs128(const CodewordSet& cs, hipStream_t st);
+hipError_t launch_decode_gf8(const DecodeSet& ds, hipStream_t st);
+struct Gf16Dev;
+hipError_t launch_encode_gf16(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st);
+hipError_t launch_decode_gf16(const DecodeSet& ds, const Gf16Dev& g, hipStream_t st);
+// Merkle roots (kernels_sha.hip): d_leaf scratch of squares*W*W*32 bytes
+bool roots_dev_supported(uint32_t W);
+hipError_t launch_roots(const uint8_t* d_eds, uint32_t W, uint32_t S, uint32_t squares, uint32_t* d_leaf,
+                        uint8_t* d_roots, hipStream_t st);
+hipError_t launch_fill_random(void* p, uint64_t bytes, uint64_t seed, hipStream_t st);
+hipError_t launch_compare(const uint8_t* a, const uint8_t* b, uint64_t n, uint32_t* mismatch, hipStream_t st);
+hipError_t launch_compare_parity(const uint8_t* a, const uint8_t* b, uint32_t k, uint32_t S, uint32_t axis,
+                                 const uint32_t* indices, uint32_t count, uint32_t* flags, hipStream_t st);
+
+#ifdef RSM_DIAG
+// ---------------------------------------------------------------------------
+// Diagnostic / A-B kernels: compiled only into librsmt2d_hip_diag.so (make diag),
+// never into the product library.
+// ---------------------------------------------------------------------------
 // One launch that runs both passes of the 2D extension over `count` squares
 // (kernels_gf8_bs.hip, encode_gf8_bs128f_kernel): the row sets of square s and
 // the column sets of square s - lag are handed out from one device-wide queue,
@@ -71,29 +96,14 @@ struct DualPlan {
     uint32_t na, nb;  // sets of a, of b
 };
 
-hipError_t launch_encode_gf8(const CodewordSet& cs, hipStream_t st);
-hipError_t launch_encode_gf8_bs128_dual(const DualPlan& p, hipStream_t st);
 // fused two-pass M = 128 extension; ctr must hold count + 3 zeroed words (the
-// kernel leaves them zeroed again, except the error flag)
+// kernel leaves them zeroed again, except the error flag ctr[2])
 bool bs128_fused_applicable(const CodewordSet& rows, const CodewordSet& cols);
 hipError_t launch_extend_gf8_bs128_fused(const FusedPlan& p, hipStream_t st);
-// bit-sliced M = 128 encode (kernels_gf8_bs.hip); launch_encode_gf8 picks it when applicable
-bool bs128_applicable(const CodewordSet& cs);
-hipError_t launch_encode_gf8_bs128(const CodewordSet& cs, hipStream_t st);
-// persistent-grid cap of the M = 128 row (pass 0) / column (pass 1) launches, 0 = all CUs
-uint32_t pass_grid_cap(int pass);
-int set_pass_grid_cap(int pass, int cus);
-hipError_t launch_decode_gf8(const DecodeSet& ds, hipStream_t st);
-struct Gf16Dev;
-hipError_t launch_encode_gf16(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st);
-hipError_t launch_decode_gf16(const DecodeSet& ds, const Gf16Dev& g, hipStream_t st);
-// Merkle roots (kernels_sha.hip): d_leaf scratch of squares*W*W*32 bytes
-bool roots_dev_supported(uint32_t W);
-hipError_t launch_roots(const uint8_t* d_eds, uint32_t W, uint32_t S, uint32_t squares, uint32_t* d_leaf,
-                        uint8_t* d_roots, hipStream_t st);
-hipError_t launch_fill_random(void* p, uint64_t bytes, uint64_t seed, hipStream_t st);
-hipError_t launch_compare(const uint8_t* a, const uint8_t* b, uint64_t n, uint32_t* mismatch, hipStream_t st);
-hipError_t launch_compare_parity(const uint8_t* a, const uint8_t* b, uint32_t k, uint32_t S, uint32_t axis,
-                                 const uint32_t* indices, uint32_t count, uint32_t* flags, hipStream_t st);
+hipError_t launch_encode_gf8_bs128_dual(const DualPlan& p, hipStream_t st);
+// A-B kernel variant of the bit-sliced encode: 40 production, 0/8/24/56 A-B
+// variants, 2 = no arithmetic, 4 = no global memory (wrong output by design)
+void set_bs128_diag_mode(int mode, int rev_col, int xcd);
+#endif
 
 }  // namespace rsm

@@ -1,0 +1,238 @@
+// rsm_multi.cpp -- one square over several GPUs of one node, behind the C ABI
+// (configuration 5: k = 512, S = 512, rows sharded over 8 MI355X).
+//
+// One process drives all GPUs (a cgo ComputeExtendedDataSquare call,
+// extendeddatasquare.go:50-77, is one goroutine): one rsm_ctx per device and an
+// RCCL clique from ncclCommInitAll.  GPU g owns Q0 rows [g k/G, (g+1) k/G):
+//   1. row pass of its rows (erasureExtendRow) -> its rows of the top half [Q0|Q1];
+//   2. exchange over xGMI:
+//        RSM_SCHED_ALLGATHER (north_star): in-place all-gather of the top half, every
+//          GPU receives (G-1) k/G x 2k shares;
+//        RSM_SCHED_ALLTOALL: grouped send/recv transpose, GPU g receives only its
+//          2k/G columns of every other GPU's rows (G-1 times fewer bytes);
+//   3. column pass of its 2k/G columns (erasureExtendCol; Q3 from Q1 columns equals
+//      the reference's Q3 from Q2 rows by linearity, extendeddatasquare.go:204-207).
+// Every step of a GPU is queued on that GPU's context stream, so the device orders
+// kernels and collectives itself: no host synchronisation between the steps.
+#include <rccl/rccl.h>
+
+#include <cstring>
+
+#include "rsm_internal.hpp"
+
+using namespace rsm;
+
+struct rsm_multi {
+    int n = 0;
+    std::vector<rsm_ctx*> ctx;
+    std::vector<ncclComm_t> comm;
+    std::vector<DevBuf> eds;       // per GPU: a full [2k][2k][S] square (host path)
+    std::vector<DevBuf> pack[2];   // per GPU: all-to-all send / receive staging
+    std::mutex mu;                 // one multi-GPU extension at a time
+};
+
+namespace {
+
+int nccl_fail(ncclResult_t r, const char* what) {
+    return fail(RSM_EDEVICE, "%s: %s", what, ncclGetErrorString(r));
+}
+
+// Steps 1-3 over device-resident squares d_eds[g] (each a full [2k][2k][S] buffer
+// on GPU g whose Q0 rows of shard g are valid).  Leaves on GPU g: its rows of the
+// top half and its column slice of the whole square (all-gather: the whole top
+// half too).
+int extend_sharded(rsm_multi* m, uint8_t* const* d_eds, uint32_t k, uint32_t S, int schedule) {
+    const int G = m->n;
+    const size_t W = 2ull * k, row = W * S;
+    const uint32_t rk = k / G, ck = (uint32_t)(W / G);
+    // 1. row pass
+    for (int g = 0; g < G; ++g) {
+        if (int rc = use_device(m->ctx[g])) return rc;
+        if (int rc = rsm_extend_rows_dev(m->ctx[g], d_eds[g], k, S, g * rk, rk, nullptr)) return rc;
+    }
+    // 2. exchange
+    ncclResult_t r;
+    if (schedule == RSM_SCHED_ALLGATHER) {
+        if ((r = ncclGroupStart()) != ncclSuccess) return nccl_fail(r, "ncclGroupStart");
+        for (int g = 0; g < G; ++g) {
+            uint8_t* top = d_eds[g];
+            r = ncclAllGather(top + (size_t)g * rk * row, top, (size_t)rk * row, ncclUint8, m->comm[g],
+                              m->ctx[g]->stream);
+            if (r != ncclSuccess) {
+                (void)ncclGroupEnd();
+                return nccl_fail(r, "ncclAllGather");
+            }
+        }
+        if ((r = ncclGroupEnd()) != ncclSuccess) return nccl_fail(r, "ncclGroupEnd");
+    } else {
+        // block (h rows) x (g columns): rk rows x ck*S bytes, packed contiguously
+        const size_t blk = (size_t)rk * ck * S;
+        hipError_t e;
+        for (int g = 0; g < G; ++g) {
+            if (int rc = use_device(m->ctx[g])) return rc;
+            if ((e = m->pack[0][g].ensure(blk * G)) != hipSuccess || (e = m->pack[1][g].ensure(blk * G)) != hipSuccess)
+                return hip_fail(e, "hipMalloc (all-to-all staging)");
+            uint8_t* snd = static_cast<uint8_t*>(m->pack[0][g].ptr);
+            const uint8_t* mine = d_eds[g] + (size_t)g * rk * row;
+            for (int h = 0; h < G; ++h)
+                if ((e = hipMemcpy2DAsync(snd + h * blk, (size_t)ck * S, mine + (size_t)h * ck * S, row, (size_t)ck * S, rk,
+                                          hipMemcpyDeviceToDevice, m->ctx[g]->stream)) != hipSuccess)
+                    return hip_fail(e, "all-to-all pack");
+        }
+        if ((r = ncclGroupStart()) != ncclSuccess) return nccl_fail(r, "ncclGroupStart");
+        for (int g = 0; g < G && r == ncclSuccess; ++g) {
+            uint8_t* snd = static_cast<uint8_t*>(m->pack[0][g].ptr);
+            uint8_t* rcv = static_cast<uint8_t*>(m->pack[1][g].ptr);
+            for (int h = 0; h < G && r == ncclSuccess; ++h) {
+                if (h == g) continue;
+                r = ncclSend(snd + h * blk, blk, ncclUint8, h, m->comm[g], m->ctx[g]->stream);
+                if (r == ncclSuccess) r = ncclRecv(rcv + h * blk, blk, ncclUint8, h, m->comm[g], m->ctx[g]->stream);
+            }
+        }
+        ncclResult_t r2 = ncclGroupEnd();
+        if (r != ncclSuccess) return nccl_fail(r, "ncclSend/ncclRecv");
+        if (r2 != ncclSuccess) return nccl_fail(r2, "ncclGroupEnd");
+        for (int g = 0; g < G; ++g) {
+            if (int rc = use_device(m->ctx[g])) return rc;
+            const uint8_t* rcv = static_cast<const uint8_t*>(m->pack[1][g].ptr);
+            for (int h = 0; h < G; ++h) {
+                if (h == g) continue;
+                uint8_t* dst = d_eds[g] + (size_t)h * rk * row + (size_t)g * ck * S;
+                if ((e = hipMemcpy2DAsync(dst, row, rcv + h * blk, (size_t)ck * S, (size_t)ck * S, rk,
+                                          hipMemcpyDeviceToDevice, m->ctx[g]->stream)) != hipSuccess)
+                    return hip_fail(e, "all-to-all unpack");
+            }
+        }
+    }
+    // 3. column pass of each GPU's column slice
+    for (int g = 0; g < G; ++g) {
+        if (int rc = use_device(m->ctx[g])) return rc;
+        if (int rc = rsm_extend_cols_dev(m->ctx[g], d_eds[g], k, S, g * ck, ck, nullptr)) return rc;
+    }
+    return RSM_OK;
+}
+
+int check_shape(const rsm_multi* m, uint32_t k, uint32_t S, int schedule) {
+    if (int rc = validate_chunk_size(S)) return rc;
+    if (k == 0 || k % m->n != 0) return fail(RSM_ESHAPE, "k=%u must be a positive multiple of the GPU count %d", k, m->n);
+    if (schedule != RSM_SCHED_ALLGATHER && schedule != RSM_SCHED_ALLTOALL)
+        return fail(RSM_EINVAL, "unknown multi-GPU schedule %d", schedule);
+    return RSM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rsm_multi_create(const int* devices, int n, rsm_multi** out) {
+    if (!devices || n <= 0 || !out) return fail(RSM_EINVAL, "rsm_multi_create: bad arguments");
+    *out = nullptr;
+    auto* m = new (std::nothrow) rsm_multi();
+    if (!m) return fail(RSM_ENOMEM, "rsm_multi_create: out of memory");
+    m->n = n;
+    m->ctx.assign(n, nullptr);
+    for (int g = 0; g < n; ++g)
+        if (int rc = rsm_ctx_create(devices[g], &m->ctx[g])) {
+            rsm_multi_destroy(m);
+            return rc;
+        }
+    m->comm.assign(n, nullptr);
+    ncclResult_t r = ncclCommInitAll(m->comm.data(), n, devices);
+    if (r != ncclSuccess) {
+        m->comm.clear();
+        rsm_multi_destroy(m);
+        return nccl_fail(r, "ncclCommInitAll");
+    }
+    m->eds = std::vector<DevBuf>(n);
+    m->pack[0] = std::vector<DevBuf>(n);
+    m->pack[1] = std::vector<DevBuf>(n);
+    *out = m;
+    return RSM_OK;
+}
+
+void rsm_multi_destroy(rsm_multi* m) {
+    if (!m) return;
+    for (auto* c : m->ctx)
+        if (c) {
+            (void)hipSetDevice(c->device);
+            (void)hipDeviceSynchronize();
+        }
+    for (auto& c : m->comm)
+        if (c) (void)ncclCommDestroy(c);
+    auto drop = [](DevBuf& b) {
+        if (b.ptr) (void)hipFree(b.ptr);
+        b.ptr = nullptr;
+        b.cap = 0;
+    };
+    for (size_t g = 0; g < m->eds.size(); ++g) {  // freed with their own device current
+        (void)hipSetDevice(m->ctx[g]->device);
+        drop(m->eds[g]);
+        drop(m->pack[0][g]);
+        drop(m->pack[1][g]);
+    }
+    for (auto* c : m->ctx)
+        if (c) rsm_ctx_destroy(c);
+    delete m;
+}
+
+int rsm_multi_size(const rsm_multi* m) { return m ? m->n : 0; }
+
+rsm_ctx* rsm_multi_context(rsm_multi* m, int i) { return (m && i >= 0 && i < m->n) ? m->ctx[i] : nullptr; }
+
+int rsm_multi_extend_dev(rsm_multi* m, void* const* d_eds, uint32_t k, uint32_t share_size, int schedule) {
+    if (!m || !d_eds) return fail(RSM_EINVAL, "rsm_multi_extend_dev: bad arguments");
+    if (int rc = check_shape(m, k, share_size, schedule)) return rc;
+    std::lock_guard<std::mutex> lk(m->mu);
+    std::vector<uint8_t*> p(m->n);
+    for (int g = 0; g < m->n; ++g) p[g] = static_cast<uint8_t*>(d_eds[g]);
+    return extend_sharded(m, p.data(), k, share_size, schedule);
+}
+
+int rsm_multi_sync(rsm_multi* m) {
+    if (!m) return fail(RSM_EINVAL, "rsm_multi_sync: NULL");
+    for (auto* c : m->ctx)
+        if (int rc = rsm_sync(c)) return rc;
+    return RSM_OK;
+}
+
+// ComputeExtendedDataSquare of one square from host memory over all GPUs: GPU g
+// uploads its Q0 rows, the sharded extension runs, and each GPU downloads its
+// rows of Q1 and its column slice of the bottom half [Q2|Q3]; Q0 is filled from
+// the host ODS.
+int rsm_multi_extend_square(rsm_multi* m, const uint8_t* ods, uint32_t k, uint32_t share_size, uint8_t* eds,
+                            int schedule) {
+    if (!m || !ods || !eds) return fail(RSM_EINVAL, "rsm_multi_extend_square: bad arguments");
+    if (int rc = check_shape(m, k, share_size, schedule)) return rc;
+    std::lock_guard<std::mutex> lk(m->mu);
+    const int G = m->n;
+    const size_t S = share_size, W = 2ull * k, row = W * S, half = (size_t)k * S;
+    const uint32_t rk = k / G, ck = (uint32_t)(W / G);
+    std::vector<uint8_t*> d(G);
+    hipError_t e;
+    for (int g = 0; g < G; ++g) {
+        if (int rc = use_device(m->ctx[g])) return rc;
+        if ((e = m->eds[g].ensure(W * W * S)) != hipSuccess) return hip_fail(e, "hipMalloc (sharded square)");
+        d[g] = static_cast<uint8_t*>(m->eds[g].ptr);
+        const size_t r0 = (size_t)g * rk;
+        if ((e = hipMemcpy2DAsync(d[g] + r0 * row, row, ods + r0 * half, half, half, rk, hipMemcpyHostToDevice,
+                                  m->ctx[g]->stream)) != hipSuccess)
+            return hip_fail(e, "H2D (Q0 rows)");
+    }
+    if (int rc = extend_sharded(m, d.data(), k, share_size, schedule)) return rc;
+    for (int g = 0; g < G; ++g) {
+        if (int rc = use_device(m->ctx[g])) return rc;
+        const size_t r0 = (size_t)g * rk;
+        hipStream_t st = m->ctx[g]->stream;
+        if ((e = hipMemcpy2DAsync(eds + r0 * row + half, row, d[g] + r0 * row + half, row, half, rk,
+                                  hipMemcpyDeviceToHost, st)) != hipSuccess)
+            return hip_fail(e, "D2H (Q1 rows)");
+        const size_t c0 = (size_t)g * ck * S;
+        if ((e = hipMemcpy2DAsync(eds + (size_t)k * row + c0, row, d[g] + (size_t)k * row + c0, row, (size_t)ck * S, k,
+                                  hipMemcpyDeviceToHost, st)) != hipSuccess)
+            return hip_fail(e, "D2H (bottom-half columns)");
+    }
+    for (uint32_t r = 0; r < k; ++r) memcpy(eds + r * row, ods + r * half, half);
+    return rsm_multi_sync(m);
+}
+
+}  // extern "C"

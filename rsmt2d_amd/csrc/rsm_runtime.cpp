@@ -3,12 +3,22 @@
 // The HIP kernels are the only compute path: every entry point that needs
 // arithmetic fails with RSM_EDEVICE when no GPU/HIP runtime is usable; there is
 // no CPU fallback anywhere in the product.
-#include <atomic>
+//
+// Threading (rsmt2d calls the Codec from up to 2k goroutines at once,
+// extendeddatasquare.go:186-224, extendeddatacrossword.go:372-425):
+//   * Codec and host-memory entry points take a Lane (own stream, pinned and
+//     device staging) from the context's pool -- concurrent calls run
+//     concurrently on the GPU;
+//   * scratch that kernels use (GF(2^16) work arrays, leaf digests) belongs to the
+//     stream the kernels are queued on, so launches on different streams never
+//     share it;
+//   * every entry point selects the context's device on the calling thread first.
 #include "rsm_internal.hpp"
 
+#include <algorithm>
+#include <cstdarg>
 #include <cstdio>
 #include <cstring>
-#include <cstdarg>
 
 namespace rsm {
 
@@ -68,6 +78,53 @@ int validate_chunk_size(int64_t share_size) {
 
 int field_bits(uint32_t k) { return 2ull * k > 256ull ? 16 : 8; }
 
+int use_device(rsm_ctx* ctx) {
+    hipError_t e = hipSetDevice(ctx->device);
+    return e == hipSuccess ? RSM_OK : hip_fail(e, "hipSetDevice");
+}
+
+// ---------------------------------------------------------------------------
+// Lanes and per-stream scratch
+// ---------------------------------------------------------------------------
+Lane* acquire_lane(rsm_ctx* ctx, int* rc) {
+    std::unique_lock<std::mutex> lk(ctx->lane_mu);
+    for (;;) {
+        if (!ctx->free_lanes.empty()) {
+            Lane* l = ctx->free_lanes.back();
+            ctx->free_lanes.pop_back();
+            *rc = RSM_OK;
+            return l;
+        }
+        if (ctx->lanes.size() < rsm_ctx::kMaxLanes) {
+            auto l = std::make_unique<Lane>();
+            hipError_t e = hipStreamCreateWithFlags(&l->stream, hipStreamNonBlocking);
+            if (e != hipSuccess) {
+                *rc = hip_fail(e, "hipStreamCreate (lane)");
+                return nullptr;
+            }
+            ctx->lanes.push_back(std::move(l));
+            *rc = RSM_OK;
+            return ctx->lanes.back().get();
+        }
+        ctx->lane_cv.wait(lk);
+    }
+}
+
+void release_lane(rsm_ctx* ctx, Lane* l) {
+    {
+        std::lock_guard<std::mutex> lk(ctx->lane_mu);
+        ctx->free_lanes.push_back(l);
+    }
+    ctx->lane_cv.notify_one();
+}
+
+StreamScratch& stream_scratch(rsm_ctx* ctx, hipStream_t st) {
+    std::lock_guard<std::mutex> lk(ctx->scratch_mu);
+    auto& p = ctx->scratch[st];
+    if (!p) p = std::make_unique<StreamScratch>();
+    return *p;
+}
+
 // ---------------------------------------------------------------------------
 // Launch helpers (device-resident, asynchronous on `st`)
 // ---------------------------------------------------------------------------
@@ -75,47 +132,48 @@ int field_bits(uint32_t k) { return 2ull * k > 256ull ? 16 : 8; }
 // every configuration in BASELINE.json); larger k returns RSM_EUNSUPPORTED.
 static bool gf16_supported(uint32_t k) { return k > 128 && k <= 512; }
 
-int ensure_gf16(rsm_ctx* ctx, uint64_t scratch_bytes, uint64_t errs_bytes) {
+int ensure_gf16_tables(rsm_ctx* ctx) {
     std::lock_guard<std::mutex> lk(ctx->gf16_mu);
-    hipError_t e = hipSetDevice(ctx->device);
-    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
-    if (!ctx->gf16_ready) {
-        const Gf16Host& t = gf16_host();
-        DevBuf& perm = ctx->dev_buf(20);
-        DevBuf& skew = ctx->dev_buf(21);
-        DevBuf& lw = ctx->dev_buf(22);
-        const size_t pb = t.perm.size() * sizeof(PermTab16), sb = t.skew.size() * 2, lb = t.logwalsh.size() * 2;
-        if ((e = perm.ensure(pb)) != hipSuccess || (e = skew.ensure(sb)) != hipSuccess || (e = lw.ensure(lb)) != hipSuccess)
-            return hip_fail(e, "hipMalloc (GF16 tables)");
-        if ((e = hipMemcpy(perm.ptr, t.perm.data(), pb, hipMemcpyHostToDevice)) != hipSuccess ||
-            (e = hipMemcpy(skew.ptr, t.skew.data(), sb, hipMemcpyHostToDevice)) != hipSuccess ||
-            (e = hipMemcpy(lw.ptr, t.logwalsh.data(), lb, hipMemcpyHostToDevice)) != hipSuccess)
-            return hip_fail(e, "upload GF16 tables");
-        ctx->gf16.perm = static_cast<const PermTab16*>(perm.ptr);
-        ctx->gf16.skew = static_cast<const uint16_t*>(skew.ptr);
-        ctx->gf16.logwalsh = static_cast<const uint16_t*>(lw.ptr);
-        ctx->gf16_ready = true;
-    }
-    if (scratch_bytes > ctx->gf16.scratch_bytes) {
-        // a kernel may still read the old scratch: drain the device before freeing it
-        if ((e = hipDeviceSynchronize()) != hipSuccess) return hip_fail(e, "hipDeviceSynchronize");
-        DevBuf& s = ctx->dev_buf(23);
-        if ((e = s.ensure(scratch_bytes)) != hipSuccess) return hip_fail(e, "hipMalloc (GF16 scratch)");
-        ctx->gf16.scratch = static_cast<uint8_t*>(s.ptr);
-        ctx->gf16.scratch_bytes = scratch_bytes;
-    }
-    if (errs_bytes > ctx->gf16.errs_bytes) {
-        if ((e = hipDeviceSynchronize()) != hipSuccess) return hip_fail(e, "hipDeviceSynchronize");
-        DevBuf& s = ctx->dev_buf(24);
-        if ((e = s.ensure(errs_bytes)) != hipSuccess) return hip_fail(e, "hipMalloc (GF16 error locators)");
-        ctx->gf16.errs = static_cast<uint16_t*>(s.ptr);
-        ctx->gf16.errs_bytes = errs_bytes;
-    }
+    if (ctx->gf16_ready) return RSM_OK;
+    const Gf16Host& t = gf16_host();
+    const size_t pb = t.perm.size() * sizeof(PermTab16), sb = t.skew.size() * 2, lb = t.logwalsh.size() * 2;
+    hipError_t e;
+    if ((e = ctx->gf16_perm.ensure(pb)) != hipSuccess || (e = ctx->gf16_skew.ensure(sb)) != hipSuccess ||
+        (e = ctx->gf16_logwalsh.ensure(lb)) != hipSuccess)
+        return hip_fail(e, "hipMalloc (GF16 tables)");
+    if ((e = hipMemcpy(ctx->gf16_perm.ptr, t.perm.data(), pb, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(ctx->gf16_skew.ptr, t.skew.data(), sb, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(ctx->gf16_logwalsh.ptr, t.logwalsh.data(), lb, hipMemcpyHostToDevice)) != hipSuccess)
+        return hip_fail(e, "upload GF16 tables");
+    ctx->gf16.perm = static_cast<const PermTab16*>(ctx->gf16_perm.ptr);
+    ctx->gf16.skew = static_cast<const uint16_t*>(ctx->gf16_skew.ptr);
+    ctx->gf16.logwalsh = static_cast<const uint16_t*>(ctx->gf16_logwalsh.ptr);
+    ctx->gf16_ready = true;
     return RSM_OK;
 }
 
-// Scratch budget for GF16 work arrays: all codewords of a launch when that fits
-// in 1 GiB, else 1 GiB worth per batch (the launcher loops).
+// GF(2^16) work arrays of stream `st` (caller holds ss.mu): grown after the
+// stream has drained, since a kernel queued earlier on it may still use them.
+static int gf16_for_stream(rsm_ctx* ctx, StreamScratch& ss, hipStream_t st, uint64_t work, uint64_t errs,
+                           Gf16Dev* out) {
+    if (int rc = ensure_gf16_tables(ctx)) return rc;
+    hipError_t e;
+    if (work > ss.gf16_work.cap || errs > ss.gf16_errs.cap) {
+        if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+        if ((e = ss.gf16_work.ensure(work)) != hipSuccess) return hip_fail(e, "hipMalloc (GF16 work arrays)");
+        if (errs && (e = ss.gf16_errs.ensure(errs)) != hipSuccess)
+            return hip_fail(e, "hipMalloc (GF16 error locators)");
+    }
+    *out = ctx->gf16;
+    out->scratch = static_cast<uint8_t*>(ss.gf16_work.ptr);
+    out->scratch_bytes = ss.gf16_work.cap;
+    out->errs = static_cast<uint16_t*>(ss.gf16_errs.ptr);
+    out->errs_bytes = ss.gf16_errs.cap;
+    return RSM_OK;
+}
+
+// Work arrays for GF(2^16): all codewords of a launch when that fits in 1 GiB,
+// else 1 GiB worth per batch (the launcher loops).
 static uint64_t gf16_budget(uint64_t per_cw, uint64_t count) {
     const uint64_t cap = 1ull << 30;
     const uint64_t want = per_cw * count;
@@ -128,12 +186,17 @@ int launch_encode(rsm_ctx* ctx, const CodewordSet& cs0, hipStream_t st) {
     hipError_t e;
     if (field_bits(cs.k) == 8) {
         cs.chunks = (cs.S + 255) / 256;
+        const uint32_t cap = ctx->pass_grid[cs.pass == 0 ? 0 : 1].load(std::memory_order_relaxed);
+        cs.grid = (cap > 0 && cap < ctx->cus) ? cap : ctx->cus;
         e = launch_encode_gf8(cs, st);
     } else {
         if (!gf16_supported(cs.k)) return fail(RSM_EUNSUPPORTED, "encode: k=%u (m > 512) not supported in this build", cs.k);
         const uint64_t per_cw = (uint64_t)ceil_pow2(cs.k) * cs.S;
-        if (int rc = ensure_gf16(ctx, gf16_budget(per_cw, cs.count), 0)) return rc;
-        e = launch_encode_gf16(cs, ctx->gf16, st);
+        StreamScratch& ss = stream_scratch(ctx, st);
+        std::lock_guard<std::mutex> lk(ss.mu);
+        Gf16Dev g;
+        if (int rc = gf16_for_stream(ctx, ss, st, gf16_budget(per_cw, cs.count), 0, &g)) return rc;
+        e = launch_encode_gf16(cs, g, st);
     }
     if (e != hipSuccess) return hip_fail(e, "encode kernel launch");
     return RSM_OK;
@@ -150,69 +213,13 @@ int launch_decode(rsm_ctx* ctx, const DecodeSet& ds0, hipStream_t st) {
         const uint64_t n = 2ull * ceil_pow2(ds.k);
         const uint64_t per_cw = 2ull * n * ds.S;
         const uint64_t budget = gf16_budget(per_cw, ds.count);
-        if (int rc = ensure_gf16(ctx, budget, (budget / per_cw) * n * sizeof(uint16_t))) return rc;
-        e = launch_decode_gf16(ds, ctx->gf16, st);
+        StreamScratch& ss = stream_scratch(ctx, st);
+        std::lock_guard<std::mutex> lk(ss.mu);
+        Gf16Dev g;
+        if (int rc = gf16_for_stream(ctx, ss, st, budget, (budget / per_cw) * n * sizeof(uint16_t), &g)) return rc;
+        e = launch_decode_gf16(ds, g, st);
     }
     if (e != hipSuccess) return hip_fail(e, "decode kernel launch");
-    return RSM_OK;
-}
-
-// The fused launch is opt-in (RSM_FUSED=1 or rsm_set_fused): measured no faster
-// than the two launches; RSM_FUSED_LAG sets FusedPlan::lag.
-std::atomic<int> g_fused{-1};
-bool fused_enabled() {
-    int v = g_fused.load(std::memory_order_relaxed);
-    if (v < 0) {
-        const char* e = getenv("RSM_FUSED");
-        v = (e != nullptr && atoi(e) != 0) ? 1 : 0;
-        g_fused.store(v, std::memory_order_relaxed);
-    }
-    return v != 0;
-}
-
-// Both passes in one launch (FusedPlan): the queue words live in a per-stream
-// buffer that the kernel leaves zeroed; a new or grown buffer is zeroed in stream
-// order before its first launch.
-int extend_fused(rsm_ctx* ctx, const CodewordSet& rows, const CodewordSet& cols, uint32_t count, hipStream_t st) {
-    static const uint32_t lag_env = [] {
-        const char* v = getenv("RSM_FUSED_LAG");
-        return v ? (uint32_t)atoi(v) : 4u;
-    }();
-    FusedPlan p{};
-    p.rows = rows;
-    p.cols = cols;
-    p.count = count;
-    p.lag = lag_env < 1 ? 1 : (lag_env > count ? count : lag_env);
-    p.rn = (uint32_t)((uint64_t)rows.k * rows.S / 2048);
-    p.cn = 2 * p.rn;
-    p.total = count * (p.rn + p.cn);
-    static const uint32_t flags_env = [] {
-        const char* v = getenv("RSM_FUSED_FLAGS");
-        return v ? (uint32_t)atoi(v) : 0u;
-    }();
-    p.flags = flags_env;
-    if (getenv("RSM_FUSED_TRACE")) {
-        DevBuf& tb = ctx->dev_buf(41);
-        if (tb.ensure((size_t)p.total * 4) != hipSuccess) return fail(RSM_EDEVICE, "fused trace buffer");
-        (void)hipMemsetAsync(tb.ptr, 0xFF, (size_t)p.total * 4, st);
-        p.trace = static_cast<uint32_t*>(tb.ptr);
-        ctx->fused_trace_n = p.total;
-    }
-    const size_t words = (size_t)count + 3;
-    {
-        std::lock_guard<std::mutex> g(ctx->fused_mu);
-        auto& b = ctx->fused_ctr[(void*)st];
-        if (!b) b = std::make_unique<DevBuf>();
-        if (b->cap < words * 4) {
-            hipError_t e = hipStreamSynchronize(st);  // an older, smaller buffer may still be in use
-            if (e == hipSuccess) e = b->ensure(((words * 4 + 4095) / 4096) * 4096);
-            if (e == hipSuccess) e = hipMemsetAsync(b->ptr, 0, b->cap, st);
-            if (e != hipSuccess) return hip_fail(e, "fused extension: queue buffer");
-        }
-        p.ctr = static_cast<uint32_t*>(b->ptr);
-    }
-    hipError_t e = launch_extend_gf8_bs128_fused(p, st);
-    if (e != hipSuccess) return hip_fail(e, "fused extension kernel launch");
     return RSM_OK;
 }
 
@@ -226,30 +233,19 @@ int extend_fused(rsm_ctx* ctx, const CodewordSet& rows, const CodewordSet& cols,
 int extend_squares(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, uint32_t count, hipStream_t st,
                    int phases) {
     const uint64_t W = 2ull * k;
-    CodewordSet rows{};
-    rows.base = d_eds;
-    rows.square_stride = W * W * S;
-    rows.cw_stride = W * S;
-    rows.elem_stride = S;
-    rows.out_offset = (uint64_t)k * S;
-    rows.per_square = k;
-    rows.count = k * count;
-    rows.k = k;
-    rows.S = S;
-    if (phases == 3 && fused_enabled() && field_bits(k) == 8) {
-        CodewordSet cols = rows;
-        cols.cw_stride = S;
-        cols.elem_stride = W * S;
-        cols.out_offset = (uint64_t)k * W * S;
-        cols.per_square = (uint32_t)W;
-        cols.count = (uint32_t)W * count;
-        rows.out_base = rows.base;
-        cols.out_base = cols.base;
-        if (bs128_fused_applicable(rows, cols)) return extend_fused(ctx, rows, cols, count, st);
-    }
     if (phases & 1) {
-        int rc = launch_encode(ctx, rows, st);
-        if (rc) return rc;
+        CodewordSet rows{};
+        rows.base = d_eds;
+        rows.square_stride = W * W * S;
+        rows.cw_stride = W * S;
+        rows.elem_stride = S;
+        rows.out_offset = (uint64_t)k * S;
+        rows.per_square = k;
+        rows.count = k * count;
+        rows.k = k;
+        rows.S = S;
+        rows.pass = 0;
+        if (int rc = launch_encode(ctx, rows, st)) return rc;
     }
     if (!(phases & 2)) return RSM_OK;
     CodewordSet cols{};
@@ -262,6 +258,7 @@ int extend_squares(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, uint32_
     cols.count = (uint32_t)W * count;
     cols.k = k;
     cols.S = S;
+    cols.pass = 1;
     return launch_encode(ctx, cols, st);
 }
 
@@ -270,12 +267,41 @@ int device_roots(rsm_ctx* ctx, const uint8_t* d_eds, uint32_t W, uint32_t S, uin
     if (!roots_dev_supported(W)) return fail(RSM_EUNSUPPORTED, "device roots: width %u not supported", W);
     if ((uint64_t)W * W * squares >= (1ull << 32) || squares > 65535)
         return fail(RSM_EINVAL, "device roots: %u squares of width %u exceed one launch", squares, W);
-    DevBuf& leaf = ctx->dev_buf(30);
-    hipError_t e = leaf.ensure((size_t)W * W * 32 * squares);
-    if (e != hipSuccess) return hip_fail(e, "hipMalloc (leaf digests)");
-    if ((e = launch_roots(d_eds, W, S, squares, static_cast<uint32_t*>(leaf.ptr), d_roots, st)) != hipSuccess)
+    StreamScratch& ss = stream_scratch(ctx, st);
+    std::lock_guard<std::mutex> lk(ss.mu);
+    const size_t need = (size_t)W * W * 32 * squares;
+    hipError_t e;
+    if (need > ss.leaf.cap) {
+        if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+        if ((e = ss.leaf.ensure(need)) != hipSuccess) return hip_fail(e, "hipMalloc (leaf digests)");
+    }
+    if ((e = launch_roots(d_eds, W, S, squares, static_cast<uint32_t*>(ss.leaf.ptr), d_roots, st)) != hipSuccess)
         return hip_fail(e, "roots kernel launch");
     return RSM_OK;
+}
+
+// One square host -> device -> host on `st`: the ODS goes straight into the EDS's
+// top-left quadrant (the EDS aliases the ODS); only Q1, Q2 and Q3 come back, the
+// caller's Q0 quadrant is filled from its own ODS on the host.
+static int host_square(rsm_ctx* ctx, const uint8_t* ods, size_t ods_pitch, uint8_t* eds, uint8_t* d, uint32_t k,
+                       uint32_t S, hipStream_t st) {
+    const size_t W = 2ull * k, row = W * S, half = (size_t)k * S;
+    hipError_t e;
+    if ((e = hipMemcpy2DAsync(d, row, ods, ods_pitch, half, k, hipMemcpyHostToDevice, st)) != hipSuccess)
+        return hip_fail(e, "hipMemcpy2DAsync H2D");
+    if (int rc = extend_squares(ctx, d, k, S, 1, st)) return rc;
+    if ((e = hipMemcpy2DAsync(eds + half, row, d + half, row, half, k, hipMemcpyDeviceToHost, st)) != hipSuccess)
+        return hip_fail(e, "hipMemcpy2DAsync D2H (Q1)");
+    if ((e = hipMemcpyAsync(eds + (size_t)k * row, d + (size_t)k * row, (size_t)k * row, hipMemcpyDeviceToHost, st)) !=
+        hipSuccess)
+        return hip_fail(e, "hipMemcpyAsync D2H (Q2|Q3)");
+    return RSM_OK;
+}
+
+static void fill_q0(const uint8_t* ods, uint8_t* eds, uint32_t k, uint32_t S) {
+    const size_t row = 2ull * k * S, half = (size_t)k * S;
+    if (eds == ods) return;
+    for (uint32_t r = 0; r < k; ++r) memcpy(eds + r * row, ods + r * half, half);
 }
 
 }  // namespace rsm
@@ -288,7 +314,7 @@ using namespace rsm;
 extern "C" {
 
 const char* rsm_last_error(void) { return last_error(); }
-const char* rsm_version(void) { return "rsmt2d-mi355x 0.1.0 (gfx950)"; }
+const char* rsm_version(void) { return "rsmt2d-mi355x 0.2.0 (gfx950)"; }
 
 int rsm_device_count(void) {
     int n = 0;
@@ -310,10 +336,16 @@ int rsm_ctx_create(int device, rsm_ctx** out) {
     auto* c = new (std::nothrow) rsm_ctx();
     if (!c) return fail(RSM_ENOMEM, "rsm_ctx_create: out of memory");
     c->device = device;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+        c->cus = (uint32_t)cus;
     e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = c->zero_index.ensure(64);
+    if (e == hipSuccess) e = hipMemset(c->zero_index.ptr, 0, 64);
     if (e != hipSuccess) {
+        if (c->stream) (void)hipStreamDestroy(c->stream);
         delete c;
-        return hip_fail(e, "hipStreamCreate");
+        return hip_fail(e, "rsm_ctx_create");
     }
     *out = c;
     return RSM_OK;
@@ -322,10 +354,21 @@ int rsm_ctx_create(int device, rsm_ctx** out) {
 void rsm_ctx_destroy(rsm_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
-    (void)hipStreamSynchronize(ctx->stream);
-    ctx->bufs.clear();
+    (void)hipDeviceSynchronize();
+    for (auto& l : ctx->lanes) (void)hipStreamDestroy(l->stream);
+    ctx->lanes.clear();
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
+}
+
+int rsm_ctx_device(const rsm_ctx* ctx) { return ctx ? ctx->device : -1; }
+
+int rsm_ctx_set_pass_grid(rsm_ctx* ctx, int pass, int cus, int* previous) {
+    if (!ctx || (pass != 0 && pass != 1) || cus < 0)
+        return fail(RSM_EINVAL, "rsm_ctx_set_pass_grid: pass must be 0 (rows) or 1 (columns), cus >= 0");
+    const uint32_t prev = ctx->pass_grid[pass].exchange((uint32_t)cus);
+    if (previous) *previous = (int)prev;
+    return RSM_OK;
 }
 
 // ---------------------------------------------------------------------------
@@ -344,34 +387,33 @@ int rsm_encode(rsm_ctx* ctx, const uint8_t* const* data, uint32_t k, uint32_t sh
     if (2ull * k > 65536ull) return fail(RSM_ESHAPE, "rsm_encode: %u shards exceed the Leopard limit", 2 * k);
     for (uint32_t i = 0; i < k; ++i)
         if (!data[i]) return fail(RSM_EINVAL, "rsm_encode: data[%u] is nil", i);
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    hipError_t e = hipSetDevice(ctx->device);
-    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    if (int rc = use_device(ctx)) return rc;
+    LaneGuard g(ctx);
+    if (!g.lane) return g.rc;
+    Lane& L = *g.lane;
     const size_t S = share_size;
     const size_t bytes = 2ull * k * S;
-    HostBuf& hb = ctx->host_buf(0);
-    DevBuf& db = ctx->dev_buf(0);
-    if ((e = hb.ensure(bytes)) != hipSuccess) return hip_fail(e, "hipHostMalloc");
-    if ((e = db.ensure(bytes)) != hipSuccess) return hip_fail(e, "hipMalloc");
-    uint8_t* h = static_cast<uint8_t*>(hb.ptr);
+    hipError_t e;
+    if ((e = L.host.ensure(bytes)) != hipSuccess) return hip_fail(e, "hipHostMalloc");
+    if ((e = L.dev.ensure(bytes)) != hipSuccess) return hip_fail(e, "hipMalloc");
+    uint8_t* h = static_cast<uint8_t*>(L.host.ptr);
     for (uint32_t i = 0; i < k; ++i) memcpy(h + i * S, data[i], S);
-    uint8_t* d = static_cast<uint8_t*>(db.ptr);
-    if ((e = hipMemcpyAsync(d, h, k * S, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess)
+    uint8_t* d = static_cast<uint8_t*>(L.dev.ptr);
+    if ((e = hipMemcpyAsync(d, h, k * S, hipMemcpyHostToDevice, L.stream)) != hipSuccess)
         return hip_fail(e, "hipMemcpyAsync H2D");
     CodewordSet cs{};
     cs.base = d;
-    cs.square_stride = 0;
-    cs.cw_stride = 0;
     cs.elem_stride = S;
     cs.out_offset = (uint64_t)k * S;
     cs.per_square = 1;
     cs.count = 1;
     cs.k = k;
     cs.S = share_size;
-    if (int rc = launch_encode(ctx, cs, ctx->stream)) return rc;
-    if ((e = hipMemcpyAsync(h + k * S, d + k * S, k * S, hipMemcpyDeviceToHost, ctx->stream)) != hipSuccess)
+    cs.pass = 1;
+    if (int rc = launch_encode(ctx, cs, L.stream)) return rc;
+    if ((e = hipMemcpyAsync(h + k * S, d + k * S, k * S, hipMemcpyDeviceToHost, L.stream)) != hipSuccess)
         return hip_fail(e, "hipMemcpyAsync D2H");
-    if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return hip_fail(e, "encode");
+    if ((e = hipStreamSynchronize(L.stream)) != hipSuccess) return hip_fail(e, "encode");
     for (uint32_t i = 0; i < k; ++i) memcpy(parity[i], h + (k + i) * S, S);
     return RSM_OK;
 }
@@ -388,45 +430,41 @@ int rsm_decode(rsm_ctx* ctx, uint8_t* const* shares, const uint8_t* present, uin
     }
     if (np == n) return RSM_OK;
     if (np < k) return fail(RSM_ETOOFEW, "too few shards given (%u of %u, need %u)", np, n, k);
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    hipError_t e = hipSetDevice(ctx->device);
-    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    if (int rc = use_device(ctx)) return rc;
+    LaneGuard g(ctx);
+    if (!g.lane) return g.rc;
+    Lane& L = *g.lane;
     const size_t S = share_size;
     const size_t bytes = (size_t)n * S;
-    HostBuf& hb = ctx->host_buf(0);
-    DevBuf& db = ctx->dev_buf(0);
-    DevBuf& dp = ctx->dev_buf(1);
-    if ((e = hb.ensure(bytes + n + 16)) != hipSuccess) return hip_fail(e, "hipHostMalloc");
-    if ((e = db.ensure(bytes)) != hipSuccess) return hip_fail(e, "hipMalloc");
-    if ((e = dp.ensure(n + 16)) != hipSuccess) return hip_fail(e, "hipMalloc");
-    uint8_t* h = static_cast<uint8_t*>(hb.ptr);
+    hipError_t e;
+    if ((e = L.host.ensure(bytes + n + 16)) != hipSuccess) return hip_fail(e, "hipHostMalloc");
+    if ((e = L.dev.ensure(bytes)) != hipSuccess) return hip_fail(e, "hipMalloc");
+    if ((e = L.aux.ensure(n + 16)) != hipSuccess) return hip_fail(e, "hipMalloc");
+    uint8_t* h = static_cast<uint8_t*>(L.host.ptr);
     for (uint32_t i = 0; i < n; ++i) {
         if (present[i]) memcpy(h + i * S, shares[i], S);
         else memset(h + i * S, 0, S);
     }
     uint8_t* hp = h + bytes;
     for (uint32_t i = 0; i < n; ++i) hp[i] = present[i] ? 1 : 0;
-    uint32_t* hidx = reinterpret_cast<uint32_t*>(hp + ((n + 3) & ~3u));
-    (void)hidx;
-    uint8_t* d = static_cast<uint8_t*>(db.ptr);
-    uint8_t* dpres = static_cast<uint8_t*>(dp.ptr);
-    if ((e = hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess)
+    uint8_t* d = static_cast<uint8_t*>(L.dev.ptr);
+    uint8_t* dpres = static_cast<uint8_t*>(L.aux.ptr);
+    if ((e = hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, L.stream)) != hipSuccess)
         return hip_fail(e, "hipMemcpyAsync H2D");
-    if ((e = hipMemcpyAsync(dpres, hp, n, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess)
+    if ((e = hipMemcpyAsync(dpres, hp, n, hipMemcpyHostToDevice, L.stream)) != hipSuccess)
         return hip_fail(e, "hipMemcpyAsync H2D");
     DecodeSet ds{};
     ds.base = d;
     ds.presence = dpres;
-    ds.indices = ctx->zero_index();
+    ds.indices = static_cast<const uint32_t*>(ctx->zero_index.ptr);
     ds.count = 1;
     ds.axis = 0;  // a single codeword is row 0 of a 1 x 2k "square"
     ds.k = k;
     ds.S = share_size;
-    if (!ds.indices) return fail(RSM_EDEVICE, "rsm_decode: index buffer allocation failed");
-    if (int rc = launch_decode(ctx, ds, ctx->stream)) return rc;
-    if ((e = hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, ctx->stream)) != hipSuccess)
+    if (int rc = launch_decode(ctx, ds, L.stream)) return rc;
+    if ((e = hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, L.stream)) != hipSuccess)
         return hip_fail(e, "hipMemcpyAsync D2H");
-    if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return hip_fail(e, "decode");
+    if ((e = hipStreamSynchronize(L.stream)) != hipSuccess) return hip_fail(e, "decode");
     for (uint32_t i = 0; i < n; ++i)
         if (!present[i]) memcpy(shares[i], h + i * S, S);
     return RSM_OK;
@@ -435,21 +473,88 @@ int rsm_decode(rsm_ctx* ctx, uint8_t* const* shares, const uint8_t* present, uin
 int rsm_extend_square(rsm_ctx* ctx, const uint8_t* ods, uint32_t k, uint32_t share_size, uint8_t* eds) {
     if (!ctx || !ods || !eds || k == 0) return fail(RSM_EINVAL, "rsm_extend_square: bad arguments");
     if (int rc = validate_chunk_size(share_size)) return rc;
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    hipError_t e = hipSetDevice(ctx->device);
-    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    if (int rc = use_device(ctx)) return rc;
+    LaneGuard g(ctx);
+    if (!g.lane) return g.rc;
     const size_t S = share_size, W = 2ull * k;
-    DevBuf& db = ctx->dev_buf(0);
-    if ((e = db.ensure(W * W * S)) != hipSuccess) return hip_fail(e, "hipMalloc");
-    uint8_t* d = static_cast<uint8_t*>(db.ptr);
-    // Q0 straight into the top-left quadrant: the EDS aliases the ODS.
-    if ((e = hipMemcpy2DAsync(d, W * S, ods, k * S, k * S, k, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess)
-        return hip_fail(e, "hipMemcpy2DAsync H2D");
-    if (int rc = extend_squares(ctx, d, k, share_size, 1, ctx->stream)) return rc;
-    if ((e = hipMemcpyAsync(eds, d, W * W * S, hipMemcpyDeviceToHost, ctx->stream)) != hipSuccess)
-        return hip_fail(e, "hipMemcpyAsync D2H");
-    if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return hip_fail(e, "extend");
+    hipError_t e;
+    if ((e = g.lane->dev.ensure(W * W * S)) != hipSuccess) return hip_fail(e, "hipMalloc");
+    if (int rc = host_square(ctx, ods, (size_t)k * S, eds, static_cast<uint8_t*>(g.lane->dev.ptr), k, share_size,
+                             g.lane->stream))
+        return rc;
+    fill_q0(ods, eds, k, share_size);
+    if ((e = hipStreamSynchronize(g.lane->stream)) != hipSuccess) return hip_fail(e, "extend");
     return RSM_OK;
+}
+
+// The EDS buffer's top-left quadrant already holds the ODS (the cgo shim gathers
+// the [][]byte shares straight into a pinned EDS arena): extend it in place.
+int rsm_extend_square_inplace_host(rsm_ctx* ctx, uint8_t* eds, uint32_t k, uint32_t share_size) {
+    if (!ctx || !eds || k == 0) return fail(RSM_EINVAL, "rsm_extend_square_inplace_host: bad arguments");
+    if (int rc = validate_chunk_size(share_size)) return rc;
+    if (int rc = use_device(ctx)) return rc;
+    LaneGuard g(ctx);
+    if (!g.lane) return g.rc;
+    const size_t S = share_size, W = 2ull * k;
+    hipError_t e;
+    if ((e = g.lane->dev.ensure(W * W * S)) != hipSuccess) return hip_fail(e, "hipMalloc");
+    if (int rc = host_square(ctx, eds, W * S, eds, static_cast<uint8_t*>(g.lane->dev.ptr), k, share_size,
+                             g.lane->stream))
+        return rc;
+    if ((e = hipStreamSynchronize(g.lane->stream)) != hipSuccess) return hip_fail(e, "extend");
+    return RSM_OK;
+}
+
+// Host-memory batch (ComputeExtendedDataSquare over many squares from host
+// buffers): square i uses lane i % n_lanes, so the H2D of one square, the
+// extension of another and the D2H of a third overlap on the copy engines and the
+// CUs.  With pinned buffers (rsm_host_alloc) every copy is an async DMA.
+int rsm_extend_squares_host(rsm_ctx* ctx, const uint8_t* ods, uint32_t k, uint32_t share_size, uint32_t count,
+                            uint8_t* eds) {
+    if (!ctx || !ods || !eds || k == 0) return fail(RSM_EINVAL, "rsm_extend_squares_host: bad arguments");
+    if (int rc = validate_chunk_size(share_size)) return rc;
+    if (count == 0) return RSM_OK;
+    if (int rc = use_device(ctx)) return rc;
+    constexpr int kLanes = 3;
+    const int nl = (int)std::min<uint32_t>(count, kLanes);
+    std::unique_ptr<LaneGuard> g[kLanes];
+    for (int i = 0; i < nl; ++i) {
+        g[i] = std::make_unique<LaneGuard>(ctx);
+        if (!g[i]->lane) return g[i]->rc;
+    }
+    const size_t S = share_size, W = 2ull * k, ods_b = (size_t)k * k * S, eds_b = W * W * S;
+    hipError_t e;
+    for (int i = 0; i < nl; ++i)
+        if ((e = g[i]->lane->dev.ensure(eds_b)) != hipSuccess) return hip_fail(e, "hipMalloc");
+    for (uint32_t i = 0; i < count; ++i) {
+        Lane& L = *g[i % nl]->lane;
+        if (int rc = host_square(ctx, ods + i * ods_b, (size_t)k * S, eds + i * eds_b, static_cast<uint8_t*>(L.dev.ptr),
+                                 k, share_size, L.stream))
+            return rc;
+        fill_q0(ods + i * ods_b, eds + i * eds_b, k, share_size);
+    }
+    for (int i = 0; i < nl; ++i)
+        if ((e = hipStreamSynchronize(g[i]->lane->stream)) != hipSuccess) return hip_fail(e, "extend (host batch)");
+    return RSM_OK;
+}
+
+int rsm_host_alloc(rsm_ctx* ctx, uint64_t bytes, void** out) {
+    if (!ctx || !out) return fail(RSM_EINVAL, "rsm_host_alloc: bad arguments");
+    *out = nullptr;
+    if (int rc = use_device(ctx)) return rc;
+    hipError_t e = hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault);
+    return e == hipSuccess ? RSM_OK : hip_fail(e, "hipHostMalloc");
+}
+
+int rsm_host_free(rsm_ctx* ctx, void* p) {
+    if (!ctx) return fail(RSM_EINVAL, "rsm_host_free: NULL ctx");
+    if (!p) return RSM_OK;
+    hipError_t e = hipHostFree(p);
+    return e == hipSuccess ? RSM_OK : hip_fail(e, "hipHostFree");
+}
+
+static hipStream_t pick(rsm_ctx* ctx, void* stream) {
+    return stream ? static_cast<hipStream_t>(stream) : ctx->stream;
 }
 
 int rsm_extend_squares_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size, uint32_t count,
@@ -457,8 +562,8 @@ int rsm_extend_squares_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share
     if (!ctx || !d_eds || k == 0) return fail(RSM_EINVAL, "rsm_extend_squares_dev: bad arguments");
     if (int rc = validate_chunk_size(share_size)) return rc;
     if (count == 0) return RSM_OK;
-    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-    return extend_squares(ctx, static_cast<uint8_t*>(d_eds), k, share_size, count, st);
+    if (int rc = use_device(ctx)) return rc;
+    return extend_squares(ctx, static_cast<uint8_t*>(d_eds), k, share_size, count, pick(ctx, stream));
 }
 
 int rsm_extend_squares_phase_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size, uint32_t count,
@@ -467,8 +572,8 @@ int rsm_extend_squares_phase_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t
         return fail(RSM_EINVAL, "rsm_extend_squares_phase_dev: bad arguments");
     if (int rc = validate_chunk_size(share_size)) return rc;
     if (count == 0) return RSM_OK;
-    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-    return extend_squares(ctx, static_cast<uint8_t*>(d_eds), k, share_size, count, st, phase);
+    if (int rc = use_device(ctx)) return rc;
+    return extend_squares(ctx, static_cast<uint8_t*>(d_eds), k, share_size, count, pick(ctx, stream), phase);
 }
 
 // Row / column slices of ONE in-place [2k][2k][S] square -- the per-GPU units of the
@@ -478,10 +583,10 @@ int rsm_extend_rows_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_si
     if (!ctx || !d_eds || k == 0 || row0 + nrows > 2 * k) return fail(RSM_EINVAL, "rsm_extend_rows_dev: bad arguments");
     if (int rc = validate_chunk_size(share_size)) return rc;
     if (nrows == 0) return RSM_OK;
+    if (int rc = use_device(ctx)) return rc;
     const uint64_t W = 2ull * k, S = share_size;
     CodewordSet cs{};
     cs.base = static_cast<uint8_t*>(d_eds) + row0 * W * S;
-    cs.square_stride = 0;
     cs.cw_stride = W * S;
     cs.elem_stride = S;
     cs.out_offset = k * S;
@@ -489,7 +594,8 @@ int rsm_extend_rows_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_si
     cs.count = nrows;
     cs.k = k;
     cs.S = share_size;
-    return launch_encode(ctx, cs, stream ? static_cast<hipStream_t>(stream) : ctx->stream);
+    cs.pass = 0;
+    return launch_encode(ctx, cs, pick(ctx, stream));
 }
 
 int rsm_extend_cols_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size, uint32_t col0, uint32_t ncols,
@@ -497,10 +603,10 @@ int rsm_extend_cols_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_si
     if (!ctx || !d_eds || k == 0 || col0 + ncols > 2 * k) return fail(RSM_EINVAL, "rsm_extend_cols_dev: bad arguments");
     if (int rc = validate_chunk_size(share_size)) return rc;
     if (ncols == 0) return RSM_OK;
+    if (int rc = use_device(ctx)) return rc;
     const uint64_t W = 2ull * k, S = share_size;
     CodewordSet cs{};
     cs.base = static_cast<uint8_t*>(d_eds) + col0 * S;
-    cs.square_stride = 0;
     cs.cw_stride = S;
     cs.elem_stride = W * S;
     cs.out_offset = k * W * S;
@@ -508,16 +614,17 @@ int rsm_extend_cols_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_si
     cs.count = ncols;
     cs.k = k;
     cs.S = share_size;
-    return launch_encode(ctx, cs, stream ? static_cast<hipStream_t>(stream) : ctx->stream);
+    cs.pass = 1;
+    return launch_encode(ctx, cs, pick(ctx, stream));
 }
 
 int rsm_roots_dev(rsm_ctx* ctx, const void* d_eds, uint32_t width, uint32_t share_size, void* d_roots,
                   void* stream) {
     if (!ctx || !d_eds || !d_roots || width == 0) return fail(RSM_EINVAL, "rsm_roots_dev: bad arguments");
     if (int rc = validate_chunk_size(share_size)) return rc;
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (int rc = use_device(ctx)) return rc;
     return device_roots(ctx, static_cast<const uint8_t*>(d_eds), width, share_size, static_cast<uint8_t*>(d_roots),
-                        stream ? static_cast<hipStream_t>(stream) : ctx->stream);
+                        pick(ctx, stream));
 }
 
 int rsm_roots_squares_dev(rsm_ctx* ctx, const void* d_eds, uint32_t width, uint32_t share_size, uint32_t count,
@@ -525,9 +632,9 @@ int rsm_roots_squares_dev(rsm_ctx* ctx, const void* d_eds, uint32_t width, uint3
     if (!ctx || !d_eds || !d_roots || width == 0) return fail(RSM_EINVAL, "rsm_roots_squares_dev: bad arguments");
     if (int rc = validate_chunk_size(share_size)) return rc;
     if (count == 0) return RSM_OK;
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (int rc = use_device(ctx)) return rc;
     return device_roots(ctx, static_cast<const uint8_t*>(d_eds), width, share_size, static_cast<uint8_t*>(d_roots),
-                        stream ? static_cast<hipStream_t>(stream) : ctx->stream, count);
+                        pick(ctx, stream), count);
 }
 
 int rsm_encode_batch_dev(rsm_ctx* ctx, const void* d_in, void* d_out, uint32_t k, uint32_t share_size,
@@ -536,10 +643,10 @@ int rsm_encode_batch_dev(rsm_ctx* ctx, const void* d_in, void* d_out, uint32_t k
         return fail(RSM_EINVAL, "rsm_encode_batch_dev: bad arguments");
     if (int rc = validate_chunk_size(share_size)) return rc;
     if (count == 0) return RSM_OK;
+    if (int rc = use_device(ctx)) return rc;
     CodewordSet cs{};
     cs.base = static_cast<uint8_t*>(const_cast<void*>(d_in));
     cs.out_base = static_cast<uint8_t*>(d_out);
-    cs.square_stride = 0;
     cs.cw_stride = cw_stride;
     cs.elem_stride = share_stride;
     cs.out_offset = 0;
@@ -547,7 +654,8 @@ int rsm_encode_batch_dev(rsm_ctx* ctx, const void* d_in, void* d_out, uint32_t k
     cs.count = count;
     cs.k = k;
     cs.S = share_size;
-    return launch_encode(ctx, cs, stream ? static_cast<hipStream_t>(stream) : ctx->stream);
+    cs.pass = 1;
+    return launch_encode(ctx, cs, pick(ctx, stream));
 }
 
 int rsm_decode_vectors_dev(rsm_ctx* ctx, void* d_eds, const uint8_t* d_presence, uint32_t k,
@@ -557,6 +665,7 @@ int rsm_decode_vectors_dev(rsm_ctx* ctx, void* d_eds, const uint8_t* d_presence,
         return fail(RSM_EINVAL, "rsm_decode_vectors_dev: bad arguments");
     if (int rc = validate_chunk_size(share_size)) return rc;
     if (count == 0) return RSM_OK;
+    if (int rc = use_device(ctx)) return rc;
     DecodeSet ds{};
     ds.base = static_cast<uint8_t*>(d_eds);
     ds.presence = d_presence;
@@ -565,16 +674,16 @@ int rsm_decode_vectors_dev(rsm_ctx* ctx, void* d_eds, const uint8_t* d_presence,
     ds.axis = (uint32_t)axis;
     ds.k = k;
     ds.S = share_size;
-    return launch_decode(ctx, ds, stream ? static_cast<hipStream_t>(stream) : ctx->stream);
+    return launch_decode(ctx, ds, pick(ctx, stream));
 }
 
 }  // extern "C"
 
 // ---------------------------------------------------------------------------
-// C ABI: device memory, synthetic inputs and event timing on the context's own
-// HIP runtime/stream.  (A host process embedding a second HIP runtime -- e.g.
-// PyTorch's bundled one -- must not hand its stream objects to this library;
-// device pointers are shared fine.)
+// C ABI: device memory, streams, events and synthetic inputs on the context's own
+// HIP runtime.  (A host process embedding a second HIP runtime -- e.g. PyTorch's
+// bundled one -- must not hand its stream objects to this library; device
+// pointers are shared fine.)
 // ---------------------------------------------------------------------------
 extern "C" {
 
@@ -582,16 +691,15 @@ void* rsm_ctx_stream(rsm_ctx* ctx) { return ctx ? static_cast<void*>(ctx->stream
 
 int rsm_dev_alloc(rsm_ctx* ctx, uint64_t bytes, void** out) {
     if (!ctx || !out) return fail(RSM_EINVAL, "rsm_dev_alloc: bad arguments");
-    hipError_t e = hipSetDevice(ctx->device);
-    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
-    if ((e = hipMalloc(out, bytes ? bytes : 1)) != hipSuccess) return hip_fail(e, "hipMalloc");
-    return RSM_OK;
+    if (int rc = use_device(ctx)) return rc;
+    hipError_t e = hipMalloc(out, bytes ? bytes : 1);
+    return e == hipSuccess ? RSM_OK : hip_fail(e, "hipMalloc");
 }
 
 int rsm_dev_free(rsm_ctx* ctx, void* p) {
     if (!ctx) return fail(RSM_EINVAL, "rsm_dev_free: NULL ctx");
     if (!p) return RSM_OK;
-    (void)hipSetDevice(ctx->device);
+    if (int rc = use_device(ctx)) return rc;
     hipError_t e = hipFree(p);
     return e == hipSuccess ? RSM_OK : hip_fail(e, "hipFree");
 }
@@ -599,8 +707,8 @@ int rsm_dev_free(rsm_ctx* ctx, void* p) {
 int rsm_memcpy(rsm_ctx* ctx, void* dst, const void* src, uint64_t bytes, int kind) {
     if (!ctx || !dst || !src || kind < 0 || kind > 2) return fail(RSM_EINVAL, "rsm_memcpy: bad arguments");
     const hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice : kind == 1 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
-    hipError_t e = hipSetDevice(ctx->device);
-    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    if (int rc = use_device(ctx)) return rc;
+    hipError_t e;
     if ((e = hipMemcpyAsync(dst, src, bytes, k, ctx->stream)) != hipSuccess) return hip_fail(e, "hipMemcpyAsync");
     if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
     return RSM_OK;
@@ -608,6 +716,7 @@ int rsm_memcpy(rsm_ctx* ctx, void* dst, const void* src, uint64_t bytes, int kin
 
 int rsm_dev_fill_random(rsm_ctx* ctx, void* d, uint64_t bytes, uint64_t seed) {
     if (!ctx || !d) return fail(RSM_EINVAL, "rsm_dev_fill_random: bad arguments");
+    if (int rc = use_device(ctx)) return rc;
     hipError_t e = launch_fill_random(d, bytes, seed, ctx->stream);
     return e == hipSuccess ? RSM_OK : hip_fail(e, "fill_random");
 }
@@ -615,17 +724,24 @@ int rsm_dev_fill_random(rsm_ctx* ctx, void* d, uint64_t bytes, uint64_t seed) {
 int rsm_stream_create(rsm_ctx* ctx, void** out) {
     if (!ctx || !out) return fail(RSM_EINVAL, "rsm_stream_create: bad arguments");
     *out = nullptr;
-    hipError_t e = hipSetDevice(ctx->device);
-    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    if (int rc = use_device(ctx)) return rc;
     hipStream_t st = nullptr;
-    if ((e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking)) != hipSuccess) return hip_fail(e, "hipStreamCreate");
+    hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+    if (e != hipSuccess) return hip_fail(e, "hipStreamCreate");
     *out = static_cast<void*>(st);
     return RSM_OK;
 }
 
 int rsm_stream_destroy(rsm_ctx* ctx, void* stream) {
     if (!ctx || !stream) return fail(RSM_EINVAL, "rsm_stream_destroy: bad arguments");
-    hipError_t e = hipStreamDestroy(static_cast<hipStream_t>(stream));
+    if (int rc = use_device(ctx)) return rc;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    (void)hipStreamSynchronize(st);
+    {
+        std::lock_guard<std::mutex> lk(ctx->scratch_mu);
+        ctx->scratch.erase(st);  // its scratch dies with it
+    }
+    hipError_t e = hipStreamDestroy(st);
     return e == hipSuccess ? RSM_OK : hip_fail(e, "hipStreamDestroy");
 }
 
@@ -637,107 +753,46 @@ int rsm_stream_sync(void* stream) {
 
 int rsm_sync(rsm_ctx* ctx) {
     if (!ctx) return fail(RSM_EINVAL, "rsm_sync: NULL ctx");
+    if (int rc = use_device(ctx)) return rc;
     hipError_t e = hipStreamSynchronize(ctx->stream);
     return e == hipSuccess ? RSM_OK : hip_fail(e, "hipStreamSynchronize");
 }
 
-int rsm_fused_trace(rsm_ctx* ctx, uint32_t* out, uint32_t n, uint32_t* err) {
-    if (!ctx || !out) return fail(RSM_EINVAL, "rsm_fused_trace: bad arguments");
-    if (hipStreamSynchronize(ctx->stream) != hipSuccess) return fail(RSM_EDEVICE, "hipStreamSynchronize");
-    const uint32_t m = n < ctx->fused_trace_n ? n : ctx->fused_trace_n;
-    if (m && hipMemcpy(out, ctx->dev_buf(41).ptr, (size_t)m * 4, hipMemcpyDeviceToHost) != hipSuccess)
-        return fail(RSM_EDEVICE, "rsm_fused_trace: copy");
-    if (err) {
-        *err = 0;
-        auto it = ctx->fused_ctr.find((void*)ctx->stream);
-        if (it != ctx->fused_ctr.end() && it->second->ptr &&
-            hipMemcpy(err, static_cast<uint32_t*>(it->second->ptr) + 2, 4, hipMemcpyDeviceToHost) != hipSuccess)
-            return fail(RSM_EDEVICE, "rsm_fused_trace: error flag");
-    }
-    return (int)m;
-}
-
-int rsm_extend_pipeline_dev(rsm_ctx* ctx, void* d_rows_eds, void* d_cols_eds, uint32_t k, uint32_t share_size,
-                            uint32_t count, void* stream) {
-    if (!ctx || k == 0 || (!d_rows_eds && !d_cols_eds)) return fail(RSM_EINVAL, "rsm_extend_pipeline_dev: bad arguments");
-    if (int rc = validate_chunk_size(share_size)) return rc;
-    if (count == 0) return RSM_OK;
-    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-    const uint64_t W = 2ull * k, S = share_size;
-    CodewordSet rows{}, cols{};
-    rows.base = rows.out_base = static_cast<uint8_t*>(d_rows_eds);
-    rows.square_stride = W * W * S;
-    rows.cw_stride = W * S;
-    rows.elem_stride = S;
-    rows.out_offset = (uint64_t)k * S;
-    rows.per_square = k;
-    rows.count = k * count;
-    rows.k = k;
-    rows.S = share_size;
-    cols = rows;
-    cols.base = cols.out_base = static_cast<uint8_t*>(d_cols_eds);
-    cols.cw_stride = S;
-    cols.elem_stride = W * S;
-    cols.out_offset = (uint64_t)k * W * S;
-    cols.per_square = (uint32_t)W;
-    cols.count = (uint32_t)W * count;
-    const bool dual = field_bits(k) == 8 && d_rows_eds && d_cols_eds && bs128_applicable(rows) && bs128_applicable(cols);
-    if (!dual) {  // separate launches (independent batches: order does not matter)
-        if (d_rows_eds)
-            if (int rc = extend_squares(ctx, static_cast<uint8_t*>(d_rows_eds), k, share_size, count, st, 1)) return rc;
-        if (d_cols_eds)
-            if (int rc = extend_squares(ctx, static_cast<uint8_t*>(d_cols_eds), k, share_size, count, st, 2)) return rc;
-        return RSM_OK;
-    }
-    DualPlan p{};
-    p.a = rows;
-    p.b = cols;
-    p.na = (uint32_t)(((uint64_t)rows.count * S + 2047) / 2048);
-    p.nb = (uint32_t)(((uint64_t)cols.count * S + 2047) / 2048);
-    hipError_t e = launch_encode_gf8_bs128_dual(p, st);
-    if (e != hipSuccess) return hip_fail(e, "pipelined extension kernel launch");
+// Events: in-loop timing of the production launches (bench.py records one per
+// phase boundary of every timed step).
+int rsm_event_create(rsm_ctx* ctx, void** out) {
+    if (!ctx || !out) return fail(RSM_EINVAL, "rsm_event_create: bad arguments");
+    if (int rc = use_device(ctx)) return rc;
+    hipEvent_t ev = nullptr;
+    hipError_t e = hipEventCreate(&ev);
+    if (e != hipSuccess) return hip_fail(e, "hipEventCreate");
+    *out = static_cast<void*>(ev);
     return RSM_OK;
 }
 
-int rsm_time_pipeline(rsm_ctx* ctx, void* d_rows_eds, void* d_cols_eds, uint32_t k, uint32_t share_size,
-                      uint32_t count, uint32_t reps, float* ms) {
-    if (!ctx || !ms || reps == 0) return fail(RSM_EINVAL, "rsm_time_pipeline: bad arguments");
-    hipEvent_t ev[2];
-    for (auto& x : ev)
-        if (hipEventCreate(&x) != hipSuccess) return fail(RSM_EDEVICE, "hipEventCreate");
-    int rc = RSM_OK;
-    (void)hipEventRecord(ev[0], ctx->stream);
-    for (uint32_t r = 0; r < reps && rc == RSM_OK; ++r)
-        rc = rsm_extend_pipeline_dev(ctx, d_rows_eds, d_cols_eds, k, share_size, count, nullptr);
-    (void)hipEventRecord(ev[1], ctx->stream);
-    if (hipEventSynchronize(ev[1]) != hipSuccess && rc == RSM_OK) rc = fail(RSM_EDEVICE, "hipEventSynchronize");
-    float t = 0;
-    (void)hipEventElapsedTime(&t, ev[0], ev[1]);
-    for (auto& x : ev) (void)hipEventDestroy(x);
-    if (rc) return rc;
-    *ms = t / reps;
-    return RSM_OK;
+int rsm_event_destroy(void* ev) {
+    if (!ev) return RSM_OK;
+    hipError_t e = hipEventDestroy(static_cast<hipEvent_t>(ev));
+    return e == hipSuccess ? RSM_OK : hip_fail(e, "hipEventDestroy");
 }
 
-int rsm_set_pass_grid(int pass, int cus) {
-    if (pass != 0 && pass != 1) return fail(RSM_EINVAL, "rsm_set_pass_grid: pass must be 0 (rows) or 1 (columns)");
-    return set_pass_grid_cap(pass, cus);
+int rsm_event_record(rsm_ctx* ctx, void* ev, void* stream) {
+    if (!ctx || !ev) return fail(RSM_EINVAL, "rsm_event_record: bad arguments");
+    hipError_t e = hipEventRecord(static_cast<hipEvent_t>(ev), pick(ctx, stream));
+    return e == hipSuccess ? RSM_OK : hip_fail(e, "hipEventRecord");
 }
 
-int rsm_set_fused(int on) {
-    const int prev = fused_enabled() ? 1 : 0;
-    g_fused.store(on ? 1 : 0, std::memory_order_relaxed);
-    return prev;
-}
-
-int rsm_extend_fused(uint32_t k, uint32_t share_size) {
-    if (!fused_enabled() || k != 128 || validate_chunk_size(share_size) != RSM_OK) return 0;
-    return ((uint64_t)k * share_size) % 2048 == 0 ? 1 : 0;
+int rsm_event_elapsed_ms(void* start, void* end, float* ms) {
+    if (!start || !end || !ms) return fail(RSM_EINVAL, "rsm_event_elapsed_ms: bad arguments");
+    hipError_t e = hipEventSynchronize(static_cast<hipEvent_t>(end));
+    if (e == hipSuccess) e = hipEventElapsedTime(ms, static_cast<hipEvent_t>(start), static_cast<hipEvent_t>(end));
+    return e == hipSuccess ? RSM_OK : hip_fail(e, "hipEventElapsedTime");
 }
 
 int rsm_time_extend(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size, uint32_t count, uint32_t reps,
                     float* row_ms, float* col_ms, float* step_ms) {
     if (!ctx || !d_eds || reps == 0) return fail(RSM_EINVAL, "rsm_time_extend: bad arguments");
+    if (int rc = use_device(ctx)) return rc;
     hipEvent_t ev[3];
     for (auto& x : ev)
         if (hipEventCreate(&x) != hipSuccess) return fail(RSM_EDEVICE, "hipEventCreate");
@@ -750,20 +805,12 @@ int rsm_time_extend(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size, 
         if (rc == RSM_OK) rc = extend_squares(ctx, static_cast<uint8_t*>(d_eds), k, share_size, count, ctx->stream, 2);
         (void)hipEventRecord(ev[2], ctx->stream);
         if (hipEventSynchronize(ev[2]) != hipSuccess) rc = fail(RSM_EDEVICE, "hipEventSynchronize");
-        float a = 0, b = 0, c = 0;
+        float a = 0, b = 0;
         (void)hipEventElapsedTime(&a, ev[0], ev[1]);
         (void)hipEventElapsedTime(&b, ev[1], ev[2]);
-        // step: the production form (one fused launch where it applies)
-        if (rc == RSM_OK) {
-            (void)hipEventRecord(ev[0], ctx->stream);
-            rc = extend_squares(ctx, static_cast<uint8_t*>(d_eds), k, share_size, count, ctx->stream, 3);
-            (void)hipEventRecord(ev[1], ctx->stream);
-            if (hipEventSynchronize(ev[1]) != hipSuccess) rc = fail(RSM_EDEVICE, "hipEventSynchronize");
-            (void)hipEventElapsedTime(&c, ev[0], ev[1]);
-        }
         acc[0] += a;
         acc[1] += b;
-        acc[2] += c;
+        acc[2] += a + b;
     }
     for (auto& x : ev) (void)hipEventDestroy(x);
     if (rc) return rc;

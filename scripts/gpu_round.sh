@@ -18,7 +18,7 @@ run() {
 }
 ok() { [ "$1" -le 1 ]; }
 if [[ $STEPS == *smoke* ]]; then run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"; ok $? || exit 3; fi
-if [[ $STEPS == *pytest* ]]; then run pytest_gpu 1200 python3 -m pytest tests -m gpu -q --maxfail=30 ${PYTEST_ARGS:-}; ok $? || exit 4; fi
+if [[ $STEPS == *pytest* ]]; then run pytest_gpu 1200 python3 -u -m pytest tests -m gpu -q --maxfail=30 --timeout 300 --timeout-method thread ${PYTEST_ARGS:-}; ok $? || exit 4; fi
 if [[ $STEPS == *bench* ]]; then run bench 600 python3 bench.py ${BENCH_ARGS:-}; ok $? || exit 5; fi
 if [[ $STEPS == *prof* ]]; then
   export TMPDIR=/tmp

@@ -1,0 +1,139 @@
+// hip_stub.cpp -- TEST INFRASTRUCTURE ONLY (tests/test_tsan_cpu.py): a host-memory
+// stand-in for the HIP runtime calls and kernel launchers that the product's host
+// code (rsm_runtime.cpp, eds.cpp) makes, so that code can be built with
+// -fsanitize=thread and hammered from many threads on a machine without a GPU.
+// "Kernels" here only touch the bytes a real launch would read and write (so the
+// sanitizer sees every buffer access); they compute nothing meaningful, and
+// nothing in the product links this file.
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cstdlib>
+#include <cstring>
+
+#include "../../rsmt2d_amd/csrc/gf16.hpp"
+#include "../../rsmt2d_amd/csrc/rsm_kernels.hpp"
+
+namespace {
+struct FakeStream {
+    int id;
+};
+std::atomic<int> g_streams{0};
+}  // namespace
+
+extern "C" {
+hipError_t hipGetDeviceCount(int* n) { *n = 1; return hipSuccess; }
+hipError_t hipSetDevice(int) { return hipSuccess; }
+hipError_t hipGetDevice(int* d) { *d = 0; return hipSuccess; }
+hipError_t hipDeviceGetAttribute(int* v, hipDeviceAttribute_t, int) { *v = 256; return hipSuccess; }
+hipError_t hipDeviceSynchronize(void) { return hipSuccess; }
+hipError_t hipGetLastError(void) { return hipSuccess; }
+hipError_t hipPeekAtLastError(void) { return hipSuccess; }
+const char* hipGetErrorString(hipError_t) { return "stub"; }
+hipError_t hipStreamCreateWithFlags(hipStream_t* s, unsigned int) {
+    *s = reinterpret_cast<hipStream_t>(new FakeStream{g_streams++});
+    return hipSuccess;
+}
+hipError_t hipStreamDestroy(hipStream_t s) {
+    delete reinterpret_cast<FakeStream*>(s);
+    return hipSuccess;
+}
+hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
+hipError_t hipMalloc(void** p, size_t n) {
+    *p = calloc(1, n ? n : 1);
+    return *p ? hipSuccess : hipErrorOutOfMemory;
+}
+hipError_t hipFree(void* p) { free(p); return hipSuccess; }
+hipError_t hipHostMalloc(void** p, size_t n, unsigned int) { return hipMalloc(p, n); }
+hipError_t hipHostFree(void* p) { free(p); return hipSuccess; }
+hipError_t hipMemcpy(void* d, const void* s, size_t n, hipMemcpyKind) { memcpy(d, s, n); return hipSuccess; }
+hipError_t hipMemcpyAsync(void* d, const void* s, size_t n, hipMemcpyKind, hipStream_t) {
+    memcpy(d, s, n);
+    return hipSuccess;
+}
+hipError_t hipMemcpy2DAsync(void* d, size_t dp, const void* s, size_t sp, size_t w, size_t h, hipMemcpyKind,
+                            hipStream_t) {
+    for (size_t r = 0; r < h; ++r) memcpy(static_cast<char*>(d) + r * dp, static_cast<const char*>(s) + r * sp, w);
+    return hipSuccess;
+}
+hipError_t hipMemset(void* d, int v, size_t n) { memset(d, v, n); return hipSuccess; }
+hipError_t hipMemsetAsync(void* d, int v, size_t n, hipStream_t) { memset(d, v, n); return hipSuccess; }
+hipError_t hipEventCreate(hipEvent_t* e) { *e = reinterpret_cast<hipEvent_t>(new int(0)); return hipSuccess; }
+hipError_t hipEventDestroy(hipEvent_t e) { delete reinterpret_cast<int*>(e); return hipSuccess; }
+hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipSuccess; }
+hipError_t hipEventSynchronize(hipEvent_t) { return hipSuccess; }
+hipError_t hipEventElapsedTime(float* ms, hipEvent_t, hipEvent_t) { *ms = 0.f; return hipSuccess; }
+}
+
+namespace rsm {
+
+// A launch reads every data symbol and writes every parity symbol of its codewords.
+static void touch_codewords(const CodewordSet& cs, bool gf16) {
+    (void)gf16;
+    for (uint32_t q = 0; q < cs.count; ++q) {
+        const uint64_t rel = cs.indices ? (uint64_t)cs.indices[q] * cs.cw_stride
+                                        : (uint64_t)(q / cs.per_square) * cs.square_stride +
+                                              (uint64_t)(q % cs.per_square) * cs.cw_stride;
+        uint8_t acc = 0;
+        for (uint32_t e = 0; e < cs.k; ++e) acc ^= cs.base[rel + (uint64_t)e * cs.elem_stride];
+        for (uint32_t e = 0; e < cs.k; ++e)
+            memset(cs.out_base + rel + cs.out_offset + (uint64_t)e * cs.elem_stride, acc, cs.S);
+    }
+}
+
+hipError_t launch_encode_gf8(const CodewordSet& cs, hipStream_t) {
+    touch_codewords(cs, false);
+    return hipSuccess;
+}
+hipError_t launch_encode_gf16(const CodewordSet& cs, const Gf16Dev& g, hipStream_t) {
+    if (g.scratch) memset(g.scratch, 0, g.scratch_bytes < 4096 ? g.scratch_bytes : 4096);
+    touch_codewords(cs, true);
+    return hipSuccess;
+}
+static void touch_decode(const DecodeSet& ds) {
+    const uint64_t W = 2ull * ds.k;
+    for (uint32_t i = 0; i < ds.count; ++i) {
+        const uint64_t vec = ds.indices[i];
+        for (uint64_t e = 0; e < W; ++e) {
+            const uint64_t cell = ds.axis == 0 ? vec * W + e : e * W + vec;
+            if (!ds.presence[cell]) memset(ds.base + cell * ds.S, 0, ds.S);
+        }
+    }
+}
+hipError_t launch_decode_gf8(const DecodeSet& ds, hipStream_t) {
+    touch_decode(ds);
+    return hipSuccess;
+}
+hipError_t launch_decode_gf16(const DecodeSet& ds, const Gf16Dev& g, hipStream_t) {
+    if (g.scratch) memset(g.scratch, 0, g.scratch_bytes < 4096 ? g.scratch_bytes : 4096);
+    if (g.errs) memset(g.errs, 0, g.errs_bytes < 4096 ? g.errs_bytes : 4096);
+    touch_decode(ds);
+    return hipSuccess;
+}
+bool bs128_applicable(const CodewordSet&) { return false; }
+hipError_t launch_encode_gf8_bs128(const CodewordSet& cs, hipStream_t st) { return launch_encode_gf8(cs, st); }
+bool roots_dev_supported(uint32_t W) { return W >= 1 && W <= 2048; }
+hipError_t launch_roots(const uint8_t* d_eds, uint32_t W, uint32_t S, uint32_t squares, uint32_t* d_leaf,
+                        uint8_t* d_roots, hipStream_t) {
+    for (uint32_t s = 0; s < squares; ++s) {
+        for (uint64_t c = 0; c < (uint64_t)W * W; ++c)
+            d_leaf[(s * (uint64_t)W * W + c) * 8] = d_eds[(s * (uint64_t)W * W + c) * S];
+        memset(d_roots + (uint64_t)s * 2 * W * 32, 0, (size_t)2 * W * 32);
+    }
+    return hipSuccess;
+}
+hipError_t launch_fill_random(void* p, uint64_t bytes, uint64_t seed, hipStream_t) {
+    memset(p, (int)(seed & 0xFF), bytes);
+    return hipSuccess;
+}
+hipError_t launch_compare(const uint8_t* a, const uint8_t* b, uint64_t n, uint32_t* mismatch, hipStream_t) {
+    *mismatch = memcmp(a, b, n) != 0;
+    return hipSuccess;
+}
+hipError_t launch_compare_parity(const uint8_t*, const uint8_t*, uint32_t, uint32_t, uint32_t, const uint32_t*,
+                                 uint32_t count, uint32_t* flags, hipStream_t) {
+    memset(flags, 0, count * 4);
+    return hipSuccess;
+}
+
+}  // namespace rsm

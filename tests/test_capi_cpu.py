@@ -128,3 +128,39 @@ def test_no_gpu_fails_loudly(lib):
         pytest.skip("a GPU is present")
     with pytest.raises(R.DeviceError):
         R.NewLeoRSCodec().Encode([b"\1" * 64] * 2)
+
+
+DIAG_HEADER = os.path.join(os.path.dirname(HEADER), "rsmt2d_hip_diag.h")
+
+
+def test_product_has_no_diagnostics(lib):
+    """The shipped library carries only the production kernels and no switch that
+    could change results: the A-B / no-arithmetic / no-memory / fused / pipelined
+    kernels and every environment knob live in librsmt2d_hip_diag.so only (VERDICT
+    round 1, item 7).  getenv needs the variable's name in the binary, so the absence
+    of every RSM_* name proves no environment variable can reach the product."""
+    blob = open(R.LIB_PATH, "rb").read()
+    for name in (b"RSM_BS_MODE", b"RSM_BS_REV", b"RSM_BS_XCD", b"RSM_BS_ROWGRID", b"RSM_BS_COLGRID", b"RSM_FUSED",
+                 b"RSM_GF8_KERNEL", b"RSM_GF16_BATCH_MB"):
+        assert name not in blob, name
+    assert not re.search(rb"RSM_[A-Z0-9_]{3,}\x00", blob), re.search(rb"RSM_[A-Z0-9_]{3,}\x00", blob)
+    # kernel symbols embedded in the gfx950 code object: only MODE 40 of the
+    # bit-sliced encode, no fused (bs128f) or dual (bs128p) kernel
+    modes = set(re.findall(rb"encode_gf8_bs128u_kernelILi(\d+)E", blob))
+    assert modes == {b"40"}, modes
+    assert b"encode_gf8_bs128f_kernel" not in blob and b"encode_gf8_bs128p_kernel" not in blob
+    txt = re.sub(r"/\*.*?\*/", "", open(DIAG_HEADER).read(), flags=re.S)
+    for s in set(re.findall(r"\b(rsm_diag_[a-z0-9_]+)\s*\(", txt)):
+        assert not hasattr(lib, s), s
+    for s in ("rsm_set_fused", "rsm_fused_trace", "rsm_extend_fused", "rsm_extend_pipeline_dev", "rsm_set_pass_grid"):
+        assert not hasattr(lib, s), s
+
+
+def test_diag_library_is_separate():
+    if not os.path.exists(R.DIAG_LIB_PATH):
+        pytest.skip("diagnostic library not built")
+    blob = open(R.DIAG_LIB_PATH, "rb").read()
+    assert b"encode_gf8_bs128f_kernel" in blob
+    dl = R.diag_library()
+    for s in R.DIAG_SIGNATURES:
+        assert hasattr(dl, s), s

@@ -1,0 +1,81 @@
+"""Diagnostic library (librsmt2d_hip_diag.so, -DRSM_DIAG): the A-B kernels kept for
+measurements -- the fused single-launch extension and the software-pipelined dual
+launch -- must still match the production two-launch form bit for bit.  The
+product library contains neither (tests/test_capi_cpu.py::test_product_has_no_diagnostics).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle
+import rsmt2d_amd as R
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dl():
+    return R.diag_library()
+
+
+def _ctx(dl):
+    h = ctypes.c_void_p()
+    R._check_with(dl, dl.rsm_ctx_create(0, ctypes.byref(h)))
+    return h.value
+
+
+def _buf(dl, ctx, n):
+    p = ctypes.c_void_p()
+    R._check_with(dl, dl.rsm_dev_alloc(ctx, n, ctypes.byref(p)))
+    return p.value
+
+
+def _down(dl, ctx, ptr, n):
+    out = np.empty(n, np.uint8)
+    R._check_with(dl, dl.rsm_memcpy(ctx, out.ctypes.data, ptr, n, 1))
+    return out
+
+
+@pytest.mark.parametrize("count,S,lag", [(1, 512, 1), (3, 512, 2), (4, 64, 4)])
+def test_fused_matches_two_launch(dl, count, S, lag):
+    k = 128
+    n = (2 * k) ** 2 * S * count
+    ctx = _ctx(dl)
+    a, b = _buf(dl, ctx, n), _buf(dl, ctx, n)
+    R._check_with(dl, dl.rsm_dev_fill_random(ctx, a, n, 91 + count))
+    R._check_with(dl, dl.rsm_sync(ctx))
+    R._check_with(dl, dl.rsm_memcpy(ctx, b, a, n, 2))
+    R._check_with(dl, dl.rsm_extend_squares_dev(ctx, a, k, S, count, None))
+    R._check_with(dl, dl.rsm_diag_extend_fused(ctx, b, k, S, count, lag, None))
+    R._check_with(dl, dl.rsm_sync(ctx))
+    ga, gb = _down(dl, ctx, a, n), _down(dl, ctx, b, n)
+    assert np.array_equal(ga, gb)
+    sq = ga[: (2 * k) ** 2 * S].reshape(2 * k, 2 * k, S)
+    assert np.array_equal(sq, oracle.extend_square(sq[:k, :k].copy(), nthreads=8))
+    for p in (a, b):
+        dl.rsm_dev_free(ctx, p)
+    dl.rsm_ctx_destroy(ctx)
+
+
+def test_pipeline_matches_two_launch(dl):
+    k, S, count = 128, 512, 2
+    n = (2 * k) ** 2 * S * count
+    ctx = _ctx(dl)
+    ref, x0, x1 = _buf(dl, ctx, n), _buf(dl, ctx, n), _buf(dl, ctx, n)
+    R._check_with(dl, dl.rsm_dev_fill_random(ctx, ref, n, 5))
+    R._check_with(dl, dl.rsm_sync(ctx))
+    for x in (x0, x1):
+        R._check_with(dl, dl.rsm_memcpy(ctx, x, ref, n, 2))
+    R._check_with(dl, dl.rsm_extend_squares_dev(ctx, ref, k, S, count, None))
+    # launch 0: rows of x0; launch 1: rows of x1 + columns of x0; launch 2: columns of x1
+    R._check_with(dl, dl.rsm_diag_extend_pipeline_dev(ctx, x0, None, k, S, count, None))
+    R._check_with(dl, dl.rsm_diag_extend_pipeline_dev(ctx, x1, x0, k, S, count, None))
+    R._check_with(dl, dl.rsm_diag_extend_pipeline_dev(ctx, None, x1, k, S, count, None))
+    R._check_with(dl, dl.rsm_sync(ctx))
+    want = _down(dl, ctx, ref, n)
+    assert np.array_equal(_down(dl, ctx, x0, n), want)
+    assert np.array_equal(_down(dl, ctx, x1, n), want)
+    for p in (ref, x0, x1):
+        dl.rsm_dev_free(ctx, p)
+    dl.rsm_ctx_destroy(ctx)

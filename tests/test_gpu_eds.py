@@ -165,10 +165,18 @@ def test_valid_fraud_proof(lib):  # extendeddatacrossword_test.go:116-163
     with pytest.raises(R.ErrByzantineData) as ei:
         corrupted.Repair(rr, cr)
     byz = ei.value
+    # PseudoFraudProof{0, byzData.Index, byzData.Shares}, verified exactly as the
+    # reference does (:144-162): decode the shares, compare the root of the rebuilt
+    # vector with getRowRoot(Index); only if they match must the re-encoded parity
+    # differ from the rebuilt parity half.
     rebuilt = codec.Decode(list(byz.Shares))
-    assert R._default_root(rebuilt) == rr[byz.Index] or True
-    parity = codec.Encode(rebuilt[:2])
-    assert parity != rebuilt[2:] or R._default_root(rebuilt) != rr[byz.Index]
+    assert all(s is not None for s in rebuilt)
+    root = R._default_root(rebuilt)           # computeSharesRoot(rebuilt, byzData.Axis, Index)
+    row_root = rr[byz.Index]                  # getRowRoot(fraudProof.Index)
+    if root == row_root:
+        odw = corrupted.originalDataWidth
+        parity = codec.Encode(rebuilt[:odw])
+        assert b"".join(parity) != b"".join(rebuilt[len(rebuilt) - odw:]), "invalid fraud proof"
 
 
 def test_random_byzantine_8x8_matches_oracle(lib, rng):

@@ -1,0 +1,213 @@
+"""GPU: the runtime around the kernels -- concurrent Codec callers, per-stream
+scratch, per-context grid caps, the pinned host-memory path and the multi-GPU C
+ABI (rsm_multi_*, RCCL from C++) -- each result checked bit-exact against the
+CPU oracle."""
+import ctypes
+import threading
+
+import numpy as np
+import pytest
+
+import oracle
+import rsmt2d_amd as R
+
+pytestmark = pytest.mark.gpu
+
+
+def _encode_args(data, parity):
+    k, S = data.shape
+    dp = (ctypes.c_void_p * k)(*[data.ctypes.data + i * S for i in range(k)])
+    pp = (ctypes.c_void_p * k)(*[parity.ctypes.data + i * S for i in range(k)])
+    return dp, pp
+
+
+def test_concurrent_codec_callers(lib):
+    """64 host threads call Encode and Decode at once on ONE context (rsmt2d calls
+    the Codec from up to 2k goroutines, extendeddatasquare.go:186-224); every result
+    equals the oracle's."""
+    ctx = R.device_context(0)
+    S = 512
+    rng = np.random.default_rng(64)
+    jobs = []
+    for t in range(64):
+        k = [128, 64, 100, 37, 128, 256][t % 6]  # GF(2^8) and GF(2^16) callers mixed
+        data = rng.integers(0, 256, (k, S), dtype=np.uint8)
+        want = np.frombuffer(b"".join(oracle.encode([bytes(r) for r in data])), np.uint8).reshape(k, S)
+        jobs.append((k, data, want))
+    errors = []
+
+    def worker(t):
+        k, data, want = jobs[t]
+        try:
+            for it in range(4):
+                par = np.zeros((k, S), np.uint8)
+                dp, pp = _encode_args(data, par)
+                rc = lib.rsm_encode(ctx, dp, k, S, pp)
+                if rc or not np.array_equal(par, want):
+                    errors.append(("encode", t, it, rc))
+                    return
+                full = np.concatenate([data, want])
+                pres = np.ones(2 * k, np.uint8)
+                lost = np.random.default_rng(1000 * t + it).choice(2 * k, size=k, replace=False)
+                pres[lost] = 0
+                work = full.copy()
+                work[lost] = 0
+                ptrs = (ctypes.c_void_p * (2 * k))(*[work.ctypes.data + i * S for i in range(2 * k)])
+                rc = lib.rsm_decode(ctx, ptrs, pres.ctypes.data, 2 * k, S)
+                if rc or not np.array_equal(work, full):
+                    errors.append(("decode", t, it, rc))
+                    return
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(("exception", t, repr(e)))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(64)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=100)
+    assert not any(x.is_alive() for x in th), "a Codec caller hung"
+    assert not errors, errors[:5]
+
+
+def test_streams_own_their_scratch(lib):
+    """Device roots and GF(2^16) extensions queued at once on different streams
+    (each with its own leaf / work-array scratch) match the one-stream results."""
+    ctx = R.device_context(0)
+    k, S, W = 256, 128, 512
+    n = W * W * S
+    bufs = [R.DeviceBuffer(n) for _ in range(2)]
+    for i, b in enumerate(bufs):
+        b.fill_random(300 + i)
+    R._check(lib.rsm_sync(ctx))
+    ods = [b.download(n).reshape(W, W, S)[:k, :k].copy() for b in bufs]
+    roots = [R.DeviceBuffer(2 * W * 32) for _ in range(2)]
+    st = [ctypes.c_void_p() for _ in range(2)]
+    for s in st:
+        R._check(lib.rsm_stream_create(ctx, ctypes.byref(s)))
+    for i in range(2):
+        R._check(lib.rsm_extend_squares_dev(ctx, bufs[i].ptr, k, S, 1, st[i]))
+        R._check(lib.rsm_roots_dev(ctx, bufs[i].ptr, W, S, roots[i].ptr, st[i]))
+    for s in st:
+        R._check(lib.rsm_stream_sync(s))
+    for i in range(2):
+        got = bufs[i].download(n).reshape(W, W, S)
+        assert np.array_equal(got, oracle.extend_square(ods[i], nthreads=8))
+        cells = [bytes(got[r, c]) for r in range(W) for c in range(W)]
+        e = R.ImportExtendedDataSquare(cells, R.NewLeoRSCodec(), R.NewDefaultTree)
+        rr = roots[i].download(2 * W * 32)
+        assert bytes(rr[: W * 32]) == b"".join(e.RowRoots())
+    for s in st:
+        R._check(lib.rsm_stream_destroy(ctx, s))
+
+
+@pytest.mark.parametrize("cap", [1, 7, 224])
+def test_pass_grid_caps_do_not_change_results(lib, cap):
+    """rsm_ctx_set_pass_grid only reshapes the persistent grid."""
+    ctx = R.device_context(0)
+    k, S, B = 128, 512, 2
+    n = (2 * k) ** 2 * S * B
+    b = R.DeviceBuffer(n)
+    b.fill_random(cap)
+    R._check(lib.rsm_sync(ctx))
+    prev = ctypes.c_int()
+    for p in (0, 1):
+        R._check(lib.rsm_ctx_set_pass_grid(ctx, p, cap, ctypes.byref(prev) if p == 0 else None))
+    try:
+        R._check(lib.rsm_extend_squares_dev(ctx, b.ptr, k, S, B, None))
+        R._check(lib.rsm_sync(ctx))
+    finally:
+        for p in (0, 1):
+            R._check(lib.rsm_ctx_set_pass_grid(ctx, p, 0, None))
+    got = b.download(n).reshape(B, 2 * k, 2 * k, S)
+    for i in range(B):
+        assert np.array_equal(got[i], oracle.extend_square(got[i, :k, :k].copy(), nthreads=8))
+    assert lib.rsm_ctx_set_pass_grid(ctx, 2, 0, None) == R.RSM_EINVAL
+
+
+@pytest.mark.parametrize("k,S,count", [(128, 512, 5), (16, 64, 3), (256, 128, 2)])
+def test_pinned_host_batch(lib, k, S, count):
+    """rsm_extend_squares_host over pinned arenas: three lanes overlap H2D,
+    extension and D2H; Q0 is filled on the host."""
+    ctx = R.device_context(0)
+    W = 2 * k
+    ob, eb = k * k * S, W * W * S
+    ho, he = ctypes.c_void_p(), ctypes.c_void_p()
+    R._check(lib.rsm_host_alloc(ctx, ob * count, ctypes.byref(ho)))
+    R._check(lib.rsm_host_alloc(ctx, eb * count, ctypes.byref(he)))
+    try:
+        ods = np.ctypeslib.as_array((ctypes.c_uint8 * (ob * count)).from_address(ho.value))
+        ods[:] = np.random.default_rng(k + count).integers(0, 256, ob * count, dtype=np.uint8)
+        R._check(lib.rsm_extend_squares_host(ctx, ho, k, S, count, he))
+        eds = np.ctypeslib.as_array((ctypes.c_uint8 * (eb * count)).from_address(he.value))
+        for i in range(count):
+            want = oracle.extend_square(ods[i * ob:(i + 1) * ob].reshape(k, k, S), nthreads=8)
+            assert np.array_equal(eds[i * eb:(i + 1) * eb].reshape(W, W, S), want), i
+    finally:
+        R._check(lib.rsm_host_free(ctx, ho))
+        R._check(lib.rsm_host_free(ctx, he))
+
+
+def test_inplace_host_and_pageable(lib):
+    ctx = R.device_context(0)
+    k, S = 128, 256
+    W = 2 * k
+    rng = np.random.default_rng(9)
+    ods = rng.integers(0, 256, (k, k, S), dtype=np.uint8)
+    want = oracle.extend_square(ods, nthreads=8)
+    eds = np.full((W, W, S), 0xAB, np.uint8)
+    R._check(lib.rsm_extend_square(ctx, ods.ctypes.data, k, S, eds.ctypes.data))
+    assert np.array_equal(eds, want)
+    eds2 = np.full((W, W, S), 0xCD, np.uint8)
+    eds2[:k, :k] = ods
+    R._check(lib.rsm_extend_square_inplace_host(ctx, eds2.ctypes.data, k, S))
+    assert np.array_equal(eds2, want)
+
+
+@pytest.fixture(scope="module")
+def multi(lib):
+    m = ctypes.c_void_p()
+    devs = (ctypes.c_int * 1)(0)
+    R._check(lib.rsm_multi_create(devs, 1, ctypes.byref(m)))
+    yield m
+    lib.rsm_multi_destroy(m)
+
+
+@pytest.mark.parametrize("sched", [0, 1])
+def test_multi_gpu_c_abi_config5_world1(lib, multi, sched):
+    """Config 5 through the C ABI (rsm_multi_extend_square: RCCL clique driven from
+    C++, all-gather and all-to-all schedules) at k = 512, S = 512 on the one GPU of
+    this box, bit-exact against the oracle."""
+    k, S = 512, 512
+    W = 2 * k
+    assert lib.rsm_multi_size(multi) == 1
+    ods = oracle.splitmix64_bytes(k * k * S, seed=0xC5 + sched).reshape(k, k, S)
+    eds = np.zeros((W, W, S), np.uint8)
+    R._check(lib.rsm_multi_extend_square(multi, ods.ctypes.data, k, S, eds.ctypes.data, sched))
+    assert np.array_equal(eds, oracle.extend_square(ods, nthreads=8))
+
+
+@pytest.mark.parametrize("k,S", [(128, 512), (64, 192)])
+def test_multi_gpu_dev_world1(lib, multi, k, S):
+    W = 2 * k
+    ctx = lib.rsm_multi_context(multi, 0)
+    p = ctypes.c_void_p()
+    R._check(lib.rsm_dev_alloc(ctx, W * W * S, ctypes.byref(p)))
+    try:
+        ods = np.random.default_rng(k).integers(0, 256, (k, k, S), dtype=np.uint8)
+        full = np.zeros((W, W, S), np.uint8)
+        full[:k, :k] = ods
+        R._check(lib.rsm_memcpy(ctx, p, full.ctypes.data, full.nbytes, 0))
+        arr = (ctypes.c_void_p * 1)(p.value)
+        R._check(lib.rsm_multi_extend_dev(multi, arr, k, S, 1))
+        R._check(lib.rsm_multi_sync(multi))
+        out = np.empty_like(full)
+        R._check(lib.rsm_memcpy(ctx, out.ctypes.data, p, out.nbytes, 1))
+        assert np.array_equal(out, oracle.extend_square(ods, nthreads=8))
+    finally:
+        lib.rsm_dev_free(ctx, p)
+
+
+def test_multi_gpu_shape_errors(lib, multi):
+    eds = np.zeros(16, np.uint8)
+    assert lib.rsm_multi_extend_square(multi, eds.ctypes.data, 4, 100, eds.ctypes.data, 0) == R.RSM_ESHARESIZE
+    assert lib.rsm_multi_extend_square(multi, eds.ctypes.data, 4, 64, eds.ctypes.data, 7) == R.RSM_EINVAL

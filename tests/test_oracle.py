@@ -137,3 +137,10 @@ def test_crossword_row_byzantine_preserves_nils():  # extendeddatacrossword_test
         crossword.repair(f, rr, cr)
     assert (ei.value.axis, ei.value.index) == (crossword.Row, 0)
     assert ei.value.shares[2] is None and ei.value.shares[3] is None
+
+
+@pytest.mark.parametrize("k,S", [(2, 64), (8, 128), (33, 64), (128, 512)])
+def test_simd_restatement_matches_scalar(k, S):
+    """The AVX2 build (cpu_baseline) computes exactly what the scalar oracle does."""
+    ods = oracle.splitmix64_bytes(k * k * S, seed=0x51D + k).reshape(k, k, S)
+    assert np.array_equal(oracle.extend_square_simd(ods, nthreads=4), oracle.extend_square(ods, nthreads=4))
