@@ -299,9 +299,10 @@ def bench_c3(local, L, R, repeats=5):
       decode_sweep -- the device decode of all 2k rows alone (rsm_decode_vectors_dev
                       over a device-resident EDS + presence mask, HIP-synchronised);
       repair       -- (*ExtendedDataSquare).Repair end to end as BenchmarkRepair
-                      times it (import untimed): upload, device sweeps, full
-                      re-extension check, DefaultTree roots of every row/col
-                      (on the device), copy back.
+                      times it (import untimed): zero-copy decode sweeps over
+                      PCIe (present cells up, rebuilt cells back), column
+                      re-encode check, DefaultTree roots of every row/col (on
+                      the device).
     Replicas only: Repair is not sharded."""
     import ctypes
     import numpy as np
@@ -382,8 +383,9 @@ def bench_c3(local, L, R, repeats=5):
             "decode_sweep_frac": round(algo / t_sweep / 1e9 / HBM_PEAK_GBS, 4),
             "repair_ms": round(t_rep * 1e3, 3), "repair_samples": repeats,
             "repair_fast_path": int(stats.fast_path), "repair_sweeps": int(stats.sweeps),
-            "note": "repair = rsm_eds_repair end to end (H2D, device sweeps, device re-extension check, "
-                    "device DefaultTree roots of all 512 vectors, D2H into the EDS buffer); median of samples"}
+            "note": "repair = rsm_eds_repair end to end on a host EDS (zero-copy decode sweeps: present cells "
+                    "read over PCIe, rebuilt cells written back; device column re-encode check; device "
+                    "DefaultTree roots of all 512 vectors); median of samples"}
 
 
 def bench_roots(local, L, R, buf, k, S, B, steps):

@@ -489,9 +489,170 @@ int pre_repair_sanity_check(rsm_eds* e, DevSquare& dev, const uint8_t* row_roots
 // Device fast path.  Returns RSM_OK with the square repaired, 1 to request the
 // exact sequential path (e is untouched in that case), or an RSM_E* error.
 enum { kFallbackStuck = 1, kFallbackEncoding = 2, kFallbackRoots = 3 };
+
+// Zero-copy form of the common first sweep (BenchmarkRepair's shape: every
+// incomplete row has >= k shares, so one row sweep completes the square).  The
+// EDS's host square is pinned and mapped: the decode kernel reads the present
+// cells straight from it over PCIe, stores them into the device square, and writes
+// every rebuilt cell both into the device square and straight back into the host
+// square -- half the bytes of an upload + download of the whole square, no copy
+// engine.  Writing the rebuilt bytes into cells that are still nil is harmless:
+// nothing reads a cell whose presence byte is 0 (the exact solver, snapshots and
+// Flattened go by presence), and presence flips only after the device verification
+// passes.  Returns RSM_OK (repaired), 1 (fall back) or an RSM_E* error.
+int fast_repair_rows_zero_copy(rsm_eds* e, DevSquare& dev, const std::vector<uint32_t>& todo,
+                               const uint8_t* row_roots, const uint8_t* col_roots) {
+    const uint32_t W = e->width, k = W / 2;
+    const size_t S = e->S, row = (size_t)W * S;
+    if (!e->data.pinned || ceil_pow2(k) != 128) return 1;
+    void* hmap = nullptr;
+    hipError_t r = hipHostGetDevicePointer(&hmap, e->data.data(), 0);
+    if (r != hipSuccess || !hmap) {
+        (void)hipGetLastError();
+        return 1;
+    }
+    // Zero-copy transport (profiles/r02c_zcprobe.jsonl: GPU reads of mapped host
+    // memory reach the copy engine's ~57 GB/s, and reads plus writes together ~73
+    // GB/s, more than the copy engine's duplex): only the present cells go up and
+    // only the rebuilt cells come back.  The decoder runs on a capped grid so its
+    // stores of one task drain while the loads of its next task arrive.  Two sweeps
+    // (top half, bottom half) on st; the verification stream sv starts on the top
+    // half while the bottom half is still crossing PCIe:
+    //   the columns of the top half are re-encoded and compared with the bottom half
+    //   (every row is a codeword by construction, so this makes the square a valid 2D
+    //   codeword: the reference's verifyEncoding of each completed column,
+    //   extendeddatacrossword.go:184), then the DefaultTree roots of all 2W vectors
+    //   (verifyAgainstRowRoots / ColRoots, :153, :173).
+    hipStream_t st = dev.st;
+    LaneGuard gv(dev.ctx);
+    if (!gv.lane) return gv.rc;
+    hipStream_t sv = gv.lane->stream;
+    StreamScratch& ss = stream_scratch(dev.ctx, sv);
+    std::lock_guard<std::mutex> lk(ss.mu);
+    if ((r = hipStreamSynchronize(sv)) != hipSuccess) return hip_fail(r, "hipStreamSynchronize");
+    if ((r = ss.leaf.ensure((size_t)W * W * 32)) != hipSuccess) return hip_fail(r, "hipMalloc (leaf digests)");
+    uint32_t* leaf = static_cast<uint32_t*>(ss.leaf.ptr);
+    DevBuf& rb = dev.ctx->eds.roots;
+    if ((r = rb.ensure((size_t)2 * W * 32)) != hipSuccess) return hip_fail(r, "hipMalloc (roots)");
+    uint8_t* d_roots = static_cast<uint8_t*>(rb.ptr);
+    hipEvent_t ev[2];
+    for (auto& x : ev) (void)hipEventCreateWithFlags(&x, hipEventDisableTiming);
+    struct EvGuard {
+        hipEvent_t* e;
+        ~EvGuard() {
+            for (int c = 0; c < 2; ++c) (void)hipEventDestroy(e[c]);
+        }
+    } evg{ev};
+    hipEvent_t &ev_top = ev[0], &ev_bot = ev[1];
+    if ((r = hipMemcpyAsync(dev.d_pres, e->present.data(), e->present.size(), hipMemcpyHostToDevice, st)) != hipSuccess)
+        return hip_fail(r, "H2D presence");
+    if ((r = hipMemcpyAsync(dev.d_idx, todo.data(), todo.size() * 4, hipMemcpyHostToDevice, st)) != hipSuccess)
+        return hip_fail(r, "H2D indices");
+    // a quarter of the CUs (A/B on MI355X, profiles/r02c_repair_ab.txt: 64 workgroups
+    // 0.87 ms, 128 0.89 ms, one per task 0.91 ms)
+    const uint32_t zc_grid = dev.ctx->cus / 4 ? dev.ctx->cus / 4 : 1;
+    auto sweep = [&](size_t t0, size_t t1) -> int {
+        if (t1 <= t0) return RSM_OK;
+        DecodeSet ds{};
+        ds.base = dev.d_eds;
+        ds.presence = dev.d_pres;
+        ds.indices = dev.d_idx + t0;
+        ds.count = (uint32_t)(t1 - t0);
+        ds.axis = RSM_AXIS_ROW;
+        ds.k = k;
+        ds.S = e->S;
+        ds.in_base = static_cast<const uint8_t*>(hmap);
+        ds.mirror = static_cast<uint8_t*>(hmap);
+        ds.grid = zc_grid;
+        return launch_decode(dev.ctx, ds, st);
+    };
+    // complete rows (not decoded) go up as they are, top half first
+    auto upload_complete = [&](uint32_t lo, uint32_t hi, size_t t) -> int {
+        for (uint32_t i = lo; i < hi;) {
+            if (t < todo.size() && todo[t] == i) {
+                ++i, ++t;
+                continue;
+            }
+            uint32_t j = i;
+            while (j < hi && !(t < todo.size() && todo[t] == j)) ++j;
+            if ((r = hipMemcpyAsync(dev.d_eds + i * row, e->data.data() + i * row, (j - i) * row,
+                                    hipMemcpyHostToDevice, st)) != hipSuccess)
+                return hip_fail(r, "H2D complete rows");
+            i = j;
+        }
+        return RSM_OK;
+    };
+    size_t split = 0;
+    while (split < todo.size() && todo[split] < k) ++split;
+    if (int rc = upload_complete(0, k, 0)) return rc;
+    if (int rc = sweep(0, split)) return rc;
+    (void)hipEventRecord(ev_top, st);
+    if (int rc = upload_complete(k, W, split)) return rc;
+    if (int rc = sweep(split, todo.size())) return rc;
+    (void)hipEventRecord(ev_bot, st);
+    // verification
+    (void)hipStreamWaitEvent(sv, ev_top, 0);
+    CodewordSet cols{};
+    cols.base = dev.d_eds;
+    cols.out_base = dev.d_scratch;
+    cols.square_stride = (uint64_t)W * row;
+    cols.cw_stride = S;
+    cols.elem_stride = row;
+    cols.out_offset = (uint64_t)k * row;
+    cols.per_square = W;
+    cols.count = W;
+    cols.k = k;
+    cols.S = e->S;
+    cols.pass = 1;
+    if (int rc = launch_encode(dev.ctx, cols, sv)) return rc;
+    if ((r = launch_leaf_hashes(dev.d_eds, k * W, e->S, leaf, sv)) != hipSuccess) return hip_fail(r, "leaf hashes");
+    (void)hipStreamWaitEvent(sv, ev_bot, 0);
+    e->stats.sweeps++;
+    e->stats.decoded_vectors += (uint32_t)todo.size();
+    uint32_t mismatch = 1;
+    std::vector<uint8_t> got((size_t)2 * W * 32);
+    if ((r = launch_leaf_hashes(dev.d_eds + (size_t)k * row, k * W, e->S, leaf + (size_t)k * W * 8, sv)) != hipSuccess ||
+        (r = hipMemsetAsync(dev.d_flags, 0, 4, sv)) != hipSuccess ||
+        (r = launch_compare(dev.d_eds + (size_t)k * row, dev.d_scratch + (size_t)k * row, (uint64_t)k * row,
+                            dev.d_flags, sv)) != hipSuccess ||
+        (r = launch_tree_roots(leaf, W, 0, 2 * W, d_roots, sv)) != hipSuccess ||  // latency-bound: one launch
+        (r = hipMemcpyAsync(&mismatch, dev.d_flags, 4, hipMemcpyDeviceToHost, sv)) != hipSuccess ||
+        (r = hipMemcpyAsync(got.data(), d_roots, got.size(), hipMemcpyDeviceToHost, sv)) != hipSuccess ||
+        (r = hipStreamSynchronize(sv)) != hipSuccess)
+        return hip_fail(r, "verify");
+    const bool enc_ok = mismatch == 0;
+    const bool roots_ok = memcmp(got.data(), row_roots, (size_t)W * 32) == 0 &&
+                          memcmp(got.data() + (size_t)W * 32, col_roots, (size_t)W * 32) == 0;
+    if (!enc_ok || !roots_ok) {
+        e->stats.fallback_reason = enc_ok ? kFallbackRoots : kFallbackEncoding;
+        return 1;
+    }
+    std::fill(e->present.begin(), e->present.end(), 1);
+    e->stats.fast_path = 1;
+    return RSM_OK;
+}
+
 int fast_repair(rsm_eds* e, DevSquare& dev, const uint8_t* row_roots, const uint8_t* col_roots,
                 uint32_t root_len, const Tree& tree) {
     const uint32_t W = e->width, k = W / 2;
+    if (tree.is_default() && root_len == 32 && roots_dev_supported(W)) {
+        // one row sweep completes the square?  then the pipelined form
+        std::vector<uint32_t> todo;
+        bool rows_only = true;
+        for (uint32_t i = 0; i < W && rows_only; ++i) {
+            const uint8_t* pr = e->present.data() + (size_t)i * W;
+            uint32_t have = 0;
+            for (uint32_t p = 0; p < W; ++p) have += pr[p] ? 1u : 0u;
+            if (have < W) {
+                if (have >= k) todo.push_back(i);
+                else rows_only = false;
+            }
+        }
+        if (rows_only && !todo.empty()) {
+            int rc = fast_repair_rows_zero_copy(e, dev, todo, row_roots, col_roots);
+            if (rc <= 0 || e->stats.fallback_reason) return rc;  // repaired / error / byzantine evidence
+        }
+    }
     std::vector<uint8_t> pres = e->present;
     auto missing_in = [&](int axis, uint32_t idx, uint32_t* have) {
         uint32_t h = 0;

@@ -417,6 +417,222 @@ __global__ __launch_bounds__(64) void decode_gf8_kernel(DecodeSet ds) {
 }
 
 // ---------------------------------------------------------------------------
+// Split decoder for M = 128 (65 <= k <= 128, n = 256 points): one 4-wave
+// workgroup per (codeword, 256-byte chunk), 2048 waves for a 256-row sweep
+// instead of 512 single waves (2 per CU, VALU issue-bound at one wave per SIMD).
+//   S layout: wave w holds points e = 64w + j (j = 0..63): decoder IFFT layers
+//             d = 1..32 and FFT layers 32..1 (twiddles depend on w: one
+//             compile-time variant per wave, selected by a wave-uniform branch);
+//   L layout: wave w holds e = 4h + w (h = 0..63): IFFT layers 64, 128, the
+//             formal derivative and FFT layers 128, 64 (twiddles independent of w).
+// The derivative (closed form out[e] = in[e] ^ XOR_{t: e_t = 0} in[e + 2^t], see
+// derivative_half) needs, in L, the partners across bits 0 and 1 from the other
+// waves: all waves publish their post-IFFT points to LDS once, then each adds the
+// (original) partner values.  LDS: [256 points][64 lanes] dwords = 64 KiB, so two
+// workgroups share a CU.
+// ---------------------------------------------------------------------------
+template <int W>
+__device__ __forceinline__ void split_ifft_low(uint32_t (&v)[64]) { ifft_layers<64, 64 * W - 1>(v); }
+template <int W>
+__device__ __forceinline__ void split_fft_low(uint32_t (&v)[64]) { fft_layers<64, 64 * W - 1>(v); }
+
+// L layout: points 4h + w: the layer joining e and e + 64 pairs h and h + 16 (block
+// start b = 128 * (h >> 5)), the layer joining e and e + 128 pairs h and h + 32.
+__device__ __forceinline__ void split_ifft_high(uint32_t (&v)[64]) {
+    constexpr unsigned L64a = kGf8.skew[0 + 64 - 1], L64b = kGf8.skew[128 + 64 - 1], L128 = kGf8.skew[128 - 1];
+    static_for<16>([&](auto H) {
+        constexpr int h = decltype(H)::value;
+        ifft2<L64a>(v[h], v[h + 16]);
+        ifft2<L64b>(v[h + 32], v[h + 48]);
+    });
+    static_for<32>([&](auto H) { ifft2<L128>(v[decltype(H)::value], v[decltype(H)::value + 32]); });
+}
+__device__ __forceinline__ void split_fft_high(uint32_t (&v)[64]) {
+    constexpr unsigned L64a = kGf8.skew[0 + 64 - 1], L64b = kGf8.skew[128 + 64 - 1], L128 = kGf8.skew[128 - 1];
+    static_for<32>([&](auto H) { fft2<L128>(v[decltype(H)::value], v[decltype(H)::value + 32]); });
+    static_for<16>([&](auto H) {
+        constexpr int h = decltype(H)::value;
+        fft2<L64a>(v[h], v[h + 16]);
+        fft2<L64b>(v[h + 32], v[h + 48]);
+    });
+}
+
+// y * exp(L) with the table in registers (VGPR operands: read from LDS)
+__device__ __forceinline__ uint32_t gf8_mul_tab(uint32_t y, const PermTab& t) {
+    const uint32_t sa = y & 0x07070707u;
+    const uint32_t sb = (y >> 3) & 0x07070707u;
+    const uint32_t sc = (y >> 6) & 0x03030303u;
+    return xor3(__builtin_amdgcn_perm(t.a_hi, t.a_lo, sa), __builtin_amdgcn_perm(t.b_hi, t.b_lo, sb),
+                __builtin_amdgcn_perm(t.c, t.c, sc));
+}
+
+// per-point multiply tables of one codeword: [0] scale by err[e] (all-zero for an
+// absent point, so its bytes -- whatever the buffer holds -- enter as 0), [1]
+// reveal by 255 - err[e].  Written once by wave 0; every wave reads them with
+// uniform LDS broadcasts instead of a dependent scalar table load per point.
+template <bool ZC>
+__device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t task, uint32_t (&xch)[256][64],
+                                                  PermTab (&ptab)[2][256]) {
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t chunks = ds.chunks;
+    const uint32_t qi = task / chunks;
+    const uint32_t chunk = task - qi * chunks;
+    const uint32_t k = ds.k;
+    const uint32_t Wd = 2u * k;
+    const uint32_t vec = __builtin_amdgcn_readfirstlane(ds.indices[qi]);
+    const uint64_t cell0 = ds.axis == 0 ? (uint64_t)vec * Wd : (uint64_t)vec;
+    const uint64_t cell_step = ds.axis == 0 ? 1u : (uint64_t)Wd;
+
+    // This wave's points e = 64w + j are 64 consecutive cell positions: recovery
+    // (parity) i = e for w < 2, original (data) i = e - 128 for w >= 2; point j is
+    // valid when i < k.  From HBM their loads go out first (independent of the
+    // presence mask and the error locator, whose latency they overlap; an absent
+    // point's bytes are multiplied by zero).  Zero-copy (ZC: inputs from host-mapped
+    // memory over PCIe), only the present points are read: the presence mask comes
+    // first, and the PCIe bytes halve.
+    const uint32_t off0 = chunk * 256u + lane * 4u;
+    const uint32_t off = off0 < ds.S ? off0 : kOob;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(ds.base);
+    const bool mirror = ds.mirror != nullptr;  // rebuilt cells also written there
+    const __amdgpu_buffer_rsrc_t ri = make_rsrc(ZC ? ds.in_base : ds.base);
+    const uint32_t ib = (w & 1u) * 64u;
+    const uint32_t p0 = (w < 2u ? k : 0u) + ib;
+    const uint32_t nvalid = ib >= k ? 0u : (k - ib >= 64u ? 64u : k - ib);
+    const uint32_t pbase = (uint32_t)((cell0 + (uint64_t)p0 * cell_step) * ds.S);
+    const uint32_t pstep = (uint32_t)(cell_step * ds.S);
+    const uint64_t valid = nvalid == 64u ? ~0ull : ((1ull << nvalid) - 1ull);
+    uint32_t v[64];
+    auto load_points = [&](uint64_t mask) {
+        static_for<64>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            const uint32_t so = ((mask >> j) & 1ull) ? pbase + (uint32_t)j * pstep : kOob;
+            v[j] = __builtin_amdgcn_raw_buffer_load_b32(ri, off, so, 0);
+        });
+    };
+    if constexpr (!ZC) load_points(valid);
+
+    uint64_t pres[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const uint32_t e = g * 64u + lane;
+        const bool p = e < Wd && ds.presence[cell0 + e * cell_step] != 0;
+        pres[g] = __ballot(p);
+    }
+    auto present = [&](uint32_t e) -> bool { return (pres[e >> 6] >> (e & 63u)) & 1u; };
+    const uint64_t have = w < 2u ? (pres[(k + ib) >> 6] >> ((k + ib) & 63u)) | (((k + ib) & 63u) ? pres[((k + ib) >> 6) + 1] << (64u - ((k + ib) & 63u)) : 0ull)
+                                 : pres[ib >> 6];
+    if constexpr (ZC) load_points(valid & have);
+
+    // error locator (log domain), as decode_gf8_kernel: entries 4 lane .. 4 lane + 3
+    uint32_t er[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t i = lane * 4u + j;
+        uint32_t x = 0;
+        if (i < k) x = present(k + i) ? 0u : 1u;
+        else if (i < 128u) x = 1u;
+        else if (i < 128u + k) x = present(i - 128u) ? 0u : 1u;
+        er[j] = x;
+    }
+    fwht256(er, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) er[j] = (er[j] * d_gf8.logwalsh[lane * 4u + j]) % 255u;
+    fwht256(er, lane);
+    if (w == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t e = lane * 4u + j;  // point e: a present, valid input?
+            const uint32_t i = e < 128u ? e : e - 128u;
+            const bool in = i < k && present(e < 128u ? k + e : i);
+            ptab[0][e] = in ? d_perm8.t[er[j]] : PermTab{0, 0, 0, 0, 0};
+            ptab[1][e] = d_perm8.t[255u - er[j]];
+        }
+    }
+    if constexpr (ZC) {  // the present cells also land in the device square
+        const uint64_t keep = valid & have;
+        static_for<64>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            const uint32_t so = ((keep >> j) & 1ull) ? pbase + (uint32_t)j * pstep : kOob;
+            __builtin_amdgcn_raw_buffer_store_b32(v[j], rs, off, so, 0);
+        });
+    }
+    __syncthreads();
+
+    // 1. S layout: scale every point by the error locator (absent -> 0)
+    static_for<64>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        v[j] = gf8_mul_tab(v[j], ptab[0][64u * w + j]);
+    });
+    // 2. IFFT layers 1..32 (per-wave twiddles)
+    if (w == 0) split_ifft_low<0>(v);
+    else if (w == 1) split_ifft_low<1>(v);
+    else if (w == 2) split_ifft_low<2>(v);
+    else split_ifft_low<3>(v);
+    // 3. S -> L
+    static_for<64>([&](auto J) { xch[64u * w + decltype(J)::value][lane] = v[decltype(J)::value]; });
+    __syncthreads();
+    static_for<64>([&](auto H) { v[decltype(H)::value] = xch[4u * decltype(H)::value + w][lane]; });
+    __syncthreads();
+    // 4. IFFT layers 64, 128; formal derivative
+    split_ifft_high(v);
+    static_for<64>([&](auto H) { xch[4u * decltype(H)::value + w][lane] = v[decltype(H)::value]; });
+    __syncthreads();
+    static_for<64>([&](auto H) {  // partners across bits 2..7: same wave, registers h + 2^s
+        constexpr int h = decltype(H)::value;
+        static_for<6>([&](auto T) {
+            constexpr int t = decltype(T)::value;
+            if constexpr (((h >> t) & 1) == 0) v[h] ^= v[h + (1 << t)];
+        });
+    });
+    if ((w & 1u) == 0)  // bit 0 of the point is 0: add point e + 1 (wave w + 1)
+        static_for<64>([&](auto H) { v[decltype(H)::value] ^= xch[4u * decltype(H)::value + w + 1][lane]; });
+    if ((w & 2u) == 0)  // bit 1 is 0: add point e + 2 (wave w + 2)
+        static_for<64>([&](auto H) { v[decltype(H)::value] ^= xch[4u * decltype(H)::value + w + 2][lane]; });
+    // 5. FFT layers 128, 64; L -> S
+    split_fft_high(v);
+    __syncthreads();
+    static_for<64>([&](auto H) { xch[4u * decltype(H)::value + w][lane] = v[decltype(H)::value]; });
+    __syncthreads();
+    static_for<64>([&](auto J) { v[decltype(J)::value] = xch[64u * w + decltype(J)::value][lane]; });
+    // 6. FFT layers 32..1; reveal the missing points of this wave
+    if (w == 0) split_fft_low<0>(v);
+    else if (w == 1) split_fft_low<1>(v);
+    else if (w == 2) split_fft_low<2>(v);
+    else split_fft_low<3>(v);
+    const uint64_t reveal = valid & ~have;
+    const __amdgpu_buffer_rsrc_t rm = make_rsrc(mirror ? ds.mirror : ds.base);
+    uint32_t sbase = pbase, sstep = pstep;
+    asm volatile("" : "+s"(sbase), "+s"(sstep));
+    static_for<64>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        const uint32_t e = 64u * w + j;
+        const uint32_t so = ((reveal >> j) & 1ull) ? sbase + (uint32_t)j * sstep : kOob;
+        const uint32_t x = gf8_mul_tab(v[j], ptab[1][e]);
+        __builtin_amdgcn_raw_buffer_store_b32(x, rs, off, so, 0);
+        if (mirror) __builtin_amdgcn_raw_buffer_store_b32(x, rm, off, so, 0);
+    });
+}
+
+// one workgroup per task (device-resident square)
+__global__ __launch_bounds__(256, 2) void decode_gf8_split_kernel(DecodeSet ds) {
+    __shared__ uint32_t xch[256][64];
+    __shared__ PermTab ptab[2][256];
+    decode_split_task<false>(ds, blockIdx.x, xch, ptab);
+}
+
+// zero-copy form: a capped grid loops over the tasks
+__global__ __launch_bounds__(256, 2) void decode_gf8_split_zc_kernel(DecodeSet ds) {
+    __shared__ uint32_t xch[256][64];
+    __shared__ PermTab ptab[2][256];
+    const uint32_t tasks = ds.count * ds.chunks;
+    for (uint32_t task = blockIdx.x; task < tasks; task += gridDim.x) {
+        decode_split_task<true>(ds, __builtin_amdgcn_readfirstlane(task), xch, ptab);
+        __syncthreads();  // LDS (xch, ptab) is reused by the next task
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Host launchers
 // ---------------------------------------------------------------------------
 template <int M>
@@ -467,6 +683,17 @@ static hipError_t launch_dec(const DecodeSet& ds, hipStream_t st) {
 }
 
 hipError_t launch_decode_gf8(const DecodeSet& ds, hipStream_t st) {
+    if (ceil_pow2(ds.k) == 128) {  // split form: 4 waves per (codeword, 256 B chunk)
+        const uint64_t tasks = (uint64_t)ds.count * ds.chunks;
+        if (tasks == 0) return hipSuccess;
+        if (ds.in_base) {
+            const uint32_t grid = ds.grid && ds.grid < tasks ? ds.grid : (uint32_t)tasks;
+            hipLaunchKernelGGL(decode_gf8_split_zc_kernel, dim3(grid), dim3(256), 0, st, ds);
+        } else {
+            hipLaunchKernelGGL(decode_gf8_split_kernel, dim3((uint32_t)tasks), dim3(256), 0, st, ds);
+        }
+        return hipGetLastError();
+    }
     switch (ceil_pow2(ds.k)) {
         case 1: return launch_dec<1>(ds, st);
         case 2: return launch_dec<2>(ds, st);

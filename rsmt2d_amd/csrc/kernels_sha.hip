@@ -42,20 +42,25 @@ __device__ __forceinline__ uint32_t shift8(uint32_t prev, uint32_t cur) {
     return __builtin_amdgcn_alignbit(prev, cur, 8);
 }
 
+// three-input XOR in one VALU op (gfx950 v_bitop3_b32, truth table 0x96)
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
 __device__ __forceinline__ void sha_block(uint32_t (&h)[8], uint32_t (&w)[16]) {
     uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
 #pragma unroll
     for (int i = 0; i < 64; ++i) {
         if (i >= 16) {
             const uint32_t x = w[(i + 1) & 15], y = w[(i + 14) & 15];
-            const uint32_t s0 = rotr(x, 7) ^ rotr(x, 18) ^ (x >> 3);
-            const uint32_t s1 = rotr(y, 17) ^ rotr(y, 19) ^ (y >> 10);
+            const uint32_t s0 = xor3(rotr(x, 7), rotr(x, 18), x >> 3);
+            const uint32_t s1 = xor3(rotr(y, 17), rotr(y, 19), y >> 10);
             w[i & 15] += s0 + w[(i + 9) & 15] + s1;
         }
-        const uint32_t S1 = rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25);
+        const uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
         const uint32_t ch = (e & f) ^ (~e & g);
         const uint32_t t1 = hh + S1 + ch + kK[i] + w[i & 15];
-        const uint32_t S0 = rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22);
+        const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
         const uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
         hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
     }
@@ -125,17 +130,18 @@ constexpr uint32_t kMaxLevel1 = 1024;  // W <= 2048
 // blockIdx.y = square of a batch.  roots: [squares][2][W][32] bytes (big-endian
 // digest bytes, as Tree.Root() returns them).
 __global__ __launch_bounds__(256) void tree_root_kernel(const uint32_t* __restrict__ leaf, uint32_t W,
-                                                        uint8_t* __restrict__ roots) {
+                                                        uint8_t* __restrict__ roots, uint32_t first) {
     leaf += (uint64_t)blockIdx.y * W * W * 8u;
     roots += (uint64_t)blockIdx.y * 2u * W * 32u;
+    const uint32_t tree = blockIdx.x + first;  // < W: row tree, else column tree
     // two ping-pong levels of W/2 digests, sized at launch (dynamic LDS): 8 KiB for
     // W = 256 instead of a fixed 64 KiB, so 8 trees share a CU instead of 2
     extern __shared__ uint32_t lvl_raw[];
     const uint32_t half = W / 2;
     auto lvl = [&](uint32_t buf, uint32_t j) -> uint32_t* { return lvl_raw + ((size_t)buf * half + j) * 8u; };
     __shared__ uint32_t sub[16][8];
-    const uint32_t axis = blockIdx.x >= W ? 1u : 0u;
-    const uint32_t idx = blockIdx.x - axis * W;
+    const uint32_t axis = tree >= W ? 1u : 0u;
+    const uint32_t idx = tree - axis * W;
     const uint32_t n = W;
     auto leaf_at = [&](uint32_t pos, uint32_t (&d)[8]) {
         const uint64_t cell = axis == 0 ? (uint64_t)idx * W + pos : (uint64_t)pos * W + idx;
@@ -209,7 +215,24 @@ hipError_t launch_roots(const uint8_t* d_eds, uint32_t W, uint32_t S, uint32_t s
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(tree_root_kernel, dim3(2 * W, squares), dim3(256), (size_t)2 * (W / 2) * 32, st, d_leaf, W,
-                       d_roots);
+                       d_roots, 0u);
+    return hipGetLastError();
+}
+
+// Pieces of launch_roots for one square, so a caller can hash rows as they become
+// final: leaf digests of `cells` consecutive cells (d_cells -> d_leaf, both already
+// offset to the first cell), and the trees [first, first + count) (row trees 0..W-1,
+// column trees W..2W-1) over a complete leaf array.
+hipError_t launch_leaf_hashes(const uint8_t* d_cells, uint32_t cells, uint32_t S, uint32_t* d_leaf, hipStream_t st) {
+    if (cells == 0) return hipSuccess;
+    hipLaunchKernelGGL(leaf_hash_kernel, dim3((cells + 255) / 256), dim3(256), 0, st, d_cells, cells, S, d_leaf);
+    return hipGetLastError();
+}
+hipError_t launch_tree_roots(const uint32_t* d_leaf, uint32_t W, uint32_t first, uint32_t count, uint8_t* d_roots,
+                             hipStream_t st) {
+    if (count == 0) return hipSuccess;
+    hipLaunchKernelGGL(tree_root_kernel, dim3(count, 1), dim3(256), (size_t)2 * (W / 2) * 32, st, d_leaf, W, d_roots,
+                       first);
     return hipGetLastError();
 }
 

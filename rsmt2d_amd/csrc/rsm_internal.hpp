@@ -68,7 +68,6 @@ struct StreamScratch {
 // used only under rsm_ctx::eds_mu, on the context stream.
 struct EdsBufs {
     DevBuf eds, scratch, pres, idx, flags, roots;
-    HostBuf staging;  // pinned: square upload / download
 };
 
 }  // namespace rsm

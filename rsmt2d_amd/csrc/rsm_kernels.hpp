@@ -47,6 +47,17 @@ struct DecodeSet {
     uint32_t k;
     uint32_t S;
     uint32_t chunks;
+    // Zero-copy forms (M = 128 split decoder only; both nullable): `in_base` (a
+    // host-mapped copy of the square): read the present cells from there instead of
+    // `base` and store them into `base` as well; `mirror`: write every rebuilt cell
+    // there too.
+    const uint8_t* in_base;
+    uint8_t* mirror;
+    // Workgroups of the M = 128 split decoder (0: one per task).  A smaller grid
+    // loops over the tasks, so the zero-copy form streams: a workgroup's stores
+    // drain over PCIe while its next loads arrive, instead of every workgroup
+    // loading, then computing, then storing in lockstep.
+    uint32_t grid;
 };
 
 hipError_t launch_encode_gf8(const CodewordSet& cs, hipStream_t st);
@@ -61,6 +72,9 @@ hipError_t launch_decode_gf16(const DecodeSet& ds, const Gf16Dev& g, hipStream_t
 bool roots_dev_supported(uint32_t W);
 hipError_t launch_roots(const uint8_t* d_eds, uint32_t W, uint32_t S, uint32_t squares, uint32_t* d_leaf,
                         uint8_t* d_roots, hipStream_t st);
+hipError_t launch_leaf_hashes(const uint8_t* d_cells, uint32_t cells, uint32_t S, uint32_t* d_leaf, hipStream_t st);
+hipError_t launch_tree_roots(const uint32_t* d_leaf, uint32_t W, uint32_t first, uint32_t count, uint8_t* d_roots,
+                             hipStream_t st);
 hipError_t launch_fill_random(void* p, uint64_t bytes, uint64_t seed, hipStream_t st);
 hipError_t launch_compare(const uint8_t* a, const uint8_t* b, uint64_t n, uint32_t* mismatch, hipStream_t st);
 hipError_t launch_compare_parity(const uint8_t* a, const uint8_t* b, uint32_t k, uint32_t S, uint32_t axis,

@@ -46,6 +46,7 @@ hipError_t hipMalloc(void** p, size_t n) {
 hipError_t hipFree(void* p) { free(p); return hipSuccess; }
 hipError_t hipHostMalloc(void** p, size_t n, unsigned int) { return hipMalloc(p, n); }
 hipError_t hipHostFree(void* p) { free(p); return hipSuccess; }
+hipError_t hipHostGetDevicePointer(void** d, void* h, unsigned int) { *d = h; return hipSuccess; }
 hipError_t hipMemcpy(void* d, const void* s, size_t n, hipMemcpyKind) { memcpy(d, s, n); return hipSuccess; }
 hipError_t hipMemcpyAsync(void* d, const void* s, size_t n, hipMemcpyKind, hipStream_t) {
     memcpy(d, s, n);
@@ -63,6 +64,8 @@ hipError_t hipEventDestroy(hipEvent_t e) { delete reinterpret_cast<int*>(e); ret
 hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipSuccess; }
 hipError_t hipEventSynchronize(hipEvent_t) { return hipSuccess; }
 hipError_t hipEventElapsedTime(float* ms, hipEvent_t, hipEvent_t) { *ms = 0.f; return hipSuccess; }
+hipError_t hipEventCreateWithFlags(hipEvent_t* e, unsigned) { return hipEventCreate(e); }
+hipError_t hipStreamWaitEvent(hipStream_t, hipEvent_t, unsigned int) { return hipSuccess; }
 }
 
 namespace rsm {
@@ -120,6 +123,16 @@ hipError_t launch_roots(const uint8_t* d_eds, uint32_t W, uint32_t S, uint32_t s
             d_leaf[(s * (uint64_t)W * W + c) * 8] = d_eds[(s * (uint64_t)W * W + c) * S];
         memset(d_roots + (uint64_t)s * 2 * W * 32, 0, (size_t)2 * W * 32);
     }
+    return hipSuccess;
+}
+hipError_t launch_leaf_hashes(const uint8_t* d_cells, uint32_t cells, uint32_t S, uint32_t* d_leaf, hipStream_t) {
+    for (uint32_t c = 0; c < cells; ++c) d_leaf[(uint64_t)c * 8] = d_cells[(uint64_t)c * S];
+    return hipSuccess;
+}
+hipError_t launch_tree_roots(const uint32_t* d_leaf, uint32_t W, uint32_t first, uint32_t count, uint8_t* d_roots,
+                             hipStream_t) {
+    for (uint32_t t = first; t < first + count; ++t) d_roots[(uint64_t)t * 32] = (uint8_t)d_leaf[0];
+    (void)W;
     return hipSuccess;
 }
 hipError_t launch_fill_random(void* p, uint64_t bytes, uint64_t seed, hipStream_t) {

@@ -110,3 +110,33 @@ def test_affine_digest_k128(lib):
     got = np.empty((256, 256, 512), np.uint8)
     R._check(lib.rsm_extend_square(R.device_context(), ods.ctypes.data, 128, 512, got.ctypes.data))
     assert hashlib.sha256(got.tobytes()).hexdigest() == want
+
+
+@pytest.mark.parametrize("k", [65, 100, 127, 128])
+@pytest.mark.parametrize("axis", [0, 1])
+@pytest.mark.parametrize("S", [192, 512, 1024])
+def test_decode_sweep_matches_oracle(lib, k, axis, S):
+    """Batched device decode of every row (or column) of a square, each with its own
+    random erasure pattern (the C3 sweep; split M = 128 decoder), bit-exact."""
+    rng = np.random.default_rng(k * 7 + axis * 3 + S)
+    W = 2 * k
+    ods = rng.integers(0, 256, (k, k, S), dtype=np.uint8)
+    full = oracle.extend_square(ods, nthreads=8)
+    pres = np.ones((W, W), np.uint8)
+    for v in range(W):
+        lost = rng.choice(W, size=int(rng.integers(1, k + 1)), replace=False)
+        if axis == 0:
+            pres[v, lost] = 0
+        else:
+            pres[lost, v] = 0
+    dmg = full * pres[:, :, None]
+    buf = R.DeviceBuffer(full.nbytes)
+    buf.upload(dmg)
+    pd = R.DeviceBuffer(W * W)
+    pd.upload(pres)
+    idx = R.DeviceBuffer(4 * W)
+    idx.upload(np.arange(W, dtype=np.uint32))
+    ctx = R.device_context(0)
+    R._check(lib.rsm_decode_vectors_dev(ctx, buf.ptr, pd.ptr, k, S, axis, idx.ptr, W, None))
+    R._check(lib.rsm_sync(ctx))
+    assert np.array_equal(buf.download(full.nbytes).reshape(W, W, S), full)

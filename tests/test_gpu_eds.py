@@ -229,3 +229,37 @@ def test_repair_half_of_each_row(lib, rng, k):
     eds.Repair(rr, cr)
     assert eds.Equals(original)
     assert eds.repair_stats().fast_path == 1
+
+
+def test_repair_half_of_each_row_byzantine_k128(lib, rng):
+    """The zero-copy row sweep (k = 128, every row decodable) with one corrupted
+    present share: the device verification rejects it, the EDS is left as it was
+    (rebuilt bytes only ever land in nil cells), and the exact sequential solver
+    reports the same ErrByzantineData as the oracle crossword."""
+    k, S_ = 128, 64
+    ods = [rng.integers(0, 256, S_, dtype=np.uint8).tobytes() for _ in range(k * k)]
+    original = R.ComputeExtendedDataSquare(ods, R.NewLeoRSCodec(), R.NewDefaultTree)
+    rr, cr = _roots(original)
+    flat = original.Flattened()
+    w = 2 * k
+    for r in range(w):
+        for c in rng.choice(w, size=k, replace=False):
+            flat[r * w + c] = None
+    present = [i for i, s in enumerate(flat) if s is not None]
+    bad = present[len(present) // 3]
+    flat[bad] = bytes(b ^ 0x5A for b in flat[bad])
+    eds = R.ImportExtendedDataSquare(flat, R.NewLeoRSCodec(), R.NewDefaultTree)
+    before = eds.Flattened()
+    try:
+        crossword.repair(list(flat), rr, cr)
+        want = None
+    except crossword.Byzantine as b:
+        want = (b.axis, b.index, b.shares)
+    with pytest.raises(R.ErrByzantineData) as ei:
+        eds.Repair(rr, cr)
+    assert (ei.value.Axis, ei.value.Index, ei.value.Shares) == want
+    assert eds.repair_stats().fast_path == 0
+    # nil cells stay nil and present cells unchanged up to the exact solver's own
+    # progress (it inserts verified rows before meeting the byzantine one)
+    after = eds.Flattened()
+    assert all(a == b for a, b in zip(before, after) if a is not None)
