@@ -208,6 +208,31 @@ int rsm_default_tree_root(void* user, int axis, uint32_t index, const uint8_t* c
                           uint32_t n_leaves, uint32_t leaf_size, uint8_t* root_out,
                           uint32_t* root_len);
 
+/* Namespaced Merkle tree (celestiaorg/nmt v0.24.3) as rsmt2d's erasured-NMT
+ * wrappers push it (nmtwrapper_test.go:94-120; the buffered pool tree
+ * nmtbuffered_tree_test.go:118-152 pushes identically): leaf i of row/column
+ * `index` is pushed as ns || share with ns = share[:namespace_size] when
+ * i < square_size and index < square_size (quadrant 0), else the parity namespace
+ * 0xFF..; root = minNs || maxNs || SHA-256 digest (2*namespace_size + 32 bytes).
+ * Tree errors (push order, too short, past the square) return RSM_ETREE. */
+typedef struct {
+    uint32_t namespace_size;       /* nmt.NamespaceIDSize (Celestia: 29) */
+    uint32_t ignore_max_namespace; /* nmt.IgnoreMaxNamespace (the wrappers force 1) */
+    uint32_t square_size;          /* ODS width k the wrapper was built for */
+} rsm_nmt_params;
+/* Tree plugin form: pass rsm_nmt_tree_root with user = (rsm_nmt_params*) as the
+ * tree_fn of rsm_eds_roots / rsm_eds_repair: complete squares then take the
+ * device path (kernels_nmt.hip), anything else the host restatement. */
+int rsm_nmt_tree_root(void* user, int axis, uint32_t index, const uint8_t* const* leaves, uint32_t n_leaves,
+                      uint32_t leaf_size, uint8_t* root_out, uint32_t* root_len);
+/* Device NMT roots of a complete device-resident [width][width][share_size]
+ * square: d_roots receives 2*width roots of 2*namespace_size + 32 bytes (rows,
+ * then columns); d_status (device, may be NULL) 2*width uint32, non-zero where
+ * that tree fails (push order).  namespace_size <= 32, width <= 1024.
+ * Asynchronous on `stream`. */
+int rsm_nmt_roots_dev(rsm_ctx* ctx, const void* d_eds, uint32_t width, uint32_t share_size,
+                      const rsm_nmt_params* params, void* d_roots, void* d_status, void* stream);
+
 /* ---- ExtendedDataSquare (extendeddatasquare.go, datasquare.go) ------------------ */
 /* ComputeExtendedDataSquare(data, codec, tree) (:50-77): n shares (lens[i] bytes). */
 int rsm_eds_compute(rsm_ctx* ctx, const uint8_t* const* data, const uint32_t* lens, uint64_t n,

@@ -19,6 +19,7 @@ from __future__ import annotations
 import base64
 import ctypes
 import json
+import math
 import os
 import subprocess
 import threading
@@ -28,6 +29,9 @@ __all__ = [
     "Leopard", "Row", "Col", "Axis", "Codec", "LeoRSCodec", "NewLeoRSCodec",
     "ExtendedDataSquare", "ComputeExtendedDataSquare", "ImportExtendedDataSquare",
     "NewExtendedDataSquare", "NewDefaultTree", "Tree", "ErrByzantineData",
+    "ComputeExtendedDataSquareWithBuffer", "BufferedTreeConstructor", "NmtParams",
+    "ErasuredNamespacedMerkleTreeConstructor", "newErasuredNamespacedMerkleTreeConstructor",
+    "TreePool", "newTreePool",
     "ErrUnrepairableDataSquare", "ErrUnevenChunks", "RSMError", "DeviceError",
     "library", "build", "device_context",
 ]
@@ -93,6 +97,12 @@ class _Byz(ctypes.Structure):
     _fields_ = [("axis", ctypes.c_int32), ("index", ctypes.c_uint32)]
 
 
+class NmtParams(ctypes.Structure):
+    """rsm_nmt_params (include/rsmt2d_hip.h)."""
+    _fields_ = [("namespace_size", ctypes.c_uint32), ("ignore_max_namespace", ctypes.c_uint32),
+                ("square_size", ctypes.c_uint32)]
+
+
 class RepairStats(ctypes.Structure):
     _fields_ = [("fast_path", ctypes.c_int32), ("sweeps", ctypes.c_uint32),
                 ("decoded_vectors", ctypes.c_uint32), ("fallback_reason", ctypes.c_uint32)]
@@ -151,6 +161,8 @@ SIGNATURES = {
     "rsm_time_extend": (_I32, [_VP, _VP, _U32, _U32, _U32, _U32, ctypes.POINTER(ctypes.c_float),
                                ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
     "rsm_default_tree_root": (_I32, [_VP, _I32, _U32, _VP, _U32, _U32, _VP, _VP]),
+    "rsm_nmt_tree_root": (_I32, [_VP, _I32, _U32, _VP, _U32, _U32, _VP, _VP]),
+    "rsm_nmt_roots_dev": (_I32, [_VP, _VP, _U32, _U32, ctypes.POINTER(NmtParams), _VP, _VP, _VP]),
     "rsm_eds_compute": (_I32, [_VP, _VP, _VP, _U64, ctypes.POINTER(_VP)]),
     "rsm_eds_import": (_I32, [_VP, _VP, _VP, _U64, ctypes.POINTER(_VP)]),
     "rsm_eds_new": (_I32, [_VP, _U32, _U32, ctypes.POINTER(_VP)]),
@@ -407,10 +419,93 @@ def NewDefaultTree(axis: int = Row, index: int = 0):
     return None
 
 
+class _NmtTree(Tree):
+    """Host Tree of the erasured NMT (Push collects, Root hashes via rsm_nmt_tree_root)."""
+
+    def __init__(self, params: "NmtParams", axis: int, index: int):
+        self._p, self._axis, self._index, self._leaves = params, axis, index, []
+
+    def Push(self, data: bytes):
+        self._leaves.append(bytes(data))
+
+    def Root(self) -> bytes:
+        keep, ptrs, _ = _bufs(self._leaves) if self._leaves else ([], None, None)
+        cap = 2 * self._p.namespace_size + 32
+        out = (ctypes.c_uint8 * cap)()
+        ln = ctypes.c_uint32(cap)
+        size = len(self._leaves[0]) if self._leaves else 0
+        if any(len(x) != size for x in self._leaves):
+            raise ValueError("NMT leaves of unequal size")
+        rc = library().rsm_nmt_tree_root(ctypes.byref(self._p), self._axis, self._index, ptrs, len(self._leaves),
+                                         size, out, ctypes.byref(ln))
+        if rc:
+            raise _err(rc)
+        return bytes(out[:ln.value])
+
+
+class ErasuredNamespacedMerkleTreeConstructor:
+    """TreeConstructorFn of rsmt2d's erasured namespaced Merkle tree
+    (nmtwrapper_test.go:75-92: celestiaorg/nmt with the parity namespace 0xFF.. for
+    every cell outside quadrant 0, IgnoreMaxNamespace).  Recognised by the EDS
+    layer, which computes these roots on the GPU (kernels_nmt.hip) for complete
+    squares; calling it returns a host Tree like the reference's NewTree."""
+
+    def __init__(self, squareSize: int, namespaceSize: int = 29, ignoreMaxNamespace: bool = True):
+        if squareSize == 0:
+            raise ValueError("cannot create a erasuredNamespacedMerkleTree of squareSize == 0")
+        self.params = NmtParams(namespaceSize, 1 if ignoreMaxNamespace else 0, squareSize)
+
+    def __call__(self, axis: int = Row, index: int = 0) -> Tree:
+        return _NmtTree(self.params, axis, index)
+
+
+def newErasuredNamespacedMerkleTreeConstructor(squareSize: int, namespaceSize: int = 29,
+                                               ignoreMaxNamespace: bool = True):
+    return ErasuredNamespacedMerkleTreeConstructor(squareSize, namespaceSize, ignoreMaxNamespace)
+
+
+class BufferedTreeConstructor:
+    """tree.go:13-16: NewConstructor(squareSize) -> TreeConstructorFn; TreeCount()."""
+
+    def NewConstructor(self, squareSize: int):  # pragma: no cover - interface
+        raise NotImplementedError
+
+    def TreeCount(self) -> int:  # pragma: no cover - interface
+        raise NotImplementedError
+
+
+class TreePool(BufferedTreeConstructor):
+    """The pooled NMT of nmtbuffered_tree_test.go:10-58 (newTreePool): a fixed number
+    of trees reused across squares of any size.  Its trees push exactly as the
+    erasured wrapper does, so here the pool hands out the device-computed NMT
+    constructor; TreeCount bounds the host-side root parallelism as setParallelOps
+    does (extendeddatasquare.go:90)."""
+
+    def __init__(self, initSquareSize: int, poolSize: int, namespaceSize: int = 29, ignoreMaxNamespace: bool = True):
+        if initSquareSize == 0:
+            raise ValueError("cannot create a resizeableBufferTree of maxSquareSize == 0")
+        self.poolSize, self.namespaceSize, self.ignoreMaxNamespace = poolSize, namespaceSize, ignoreMaxNamespace
+
+    def NewConstructor(self, squareSize: int):
+        return ErasuredNamespacedMerkleTreeConstructor(squareSize, self.namespaceSize, self.ignoreMaxNamespace)
+
+    def TreeCount(self) -> int:
+        return self.poolSize
+
+
+def newTreePool(initSquareSize: int, poolSize: int, namespaceSize: int = 29, ignoreMaxNamespace: bool = True):
+    return TreePool(initSquareSize, poolSize, namespaceSize, ignoreMaxNamespace)
+
+
 def _tree_callback(tree_fn):
-    """ctypes callback for a Python TreeConstructorFn, or NULL for NewDefaultTree."""
+    """(keep-alive, tree_fn pointer, user pointer) for the C ABI: NULL for
+    NewDefaultTree, the library's rsm_nmt_tree_root for the NMT constructor (so the
+    GPU computes it), a ctypes callback for any other Python TreeConstructorFn."""
     if tree_fn is None or tree_fn is NewDefaultTree:
-        return None, None
+        return None, None, None
+    if isinstance(tree_fn, ErasuredNamespacedMerkleTreeConstructor):
+        fn = ctypes.cast(library().rsm_nmt_tree_root, ctypes.c_void_p)
+        return tree_fn.params, fn, ctypes.cast(ctypes.byref(tree_fn.params), ctypes.c_void_p)
 
     def cb(user, axis, index, leaves, n, leaf_size, root_out, root_len):
         try:
@@ -427,7 +522,7 @@ def _tree_callback(tree_fn):
             return RSM_ETREE
 
     c = _TREE_FN(cb)
-    return c, ctypes.cast(c, ctypes.c_void_p)
+    return c, ctypes.cast(c, ctypes.c_void_p), None
 
 
 def _default_root(leaves: Sequence[bytes]) -> bytes:
@@ -517,8 +612,8 @@ class ExtendedDataSquare:
         cap = 256
         out = ctypes.create_string_buffer(max(w * cap, 1))
         ln = ctypes.c_uint32(0)
-        keep, fn = _tree_callback(self._tree_fn)
-        _check(library().rsm_eds_roots(self._h, axis, fn, None, out, cap, ctypes.byref(ln)))
+        keep, fn, user = _tree_callback(self._tree_fn)
+        _check(library().rsm_eds_roots(self._h, axis, fn, user, out, cap, ctypes.byref(ln)))
         raw = out.raw
         return [raw[i * cap: i * cap + ln.value] for i in range(w)]
 
@@ -539,8 +634,8 @@ class ExtendedDataSquare:
         rr = b"".join(bytes(r) for r in rowRoots)
         cr = b"".join(bytes(c) for c in colRoots)
         byz = _Byz()
-        keep, fn = _tree_callback(self._tree_fn)
-        rc = L.rsm_eds_repair(self._h, rr, cr, root_len, fn, None, ctypes.byref(byz))
+        keep, fn, user = _tree_callback(self._tree_fn)
+        rc = L.rsm_eds_repair(self._h, rr, cr, root_len, fn, user, ctypes.byref(byz))
         if rc == RSM_OK:
             return
         if rc == RSM_EUNREPAIRABLE:
@@ -593,6 +688,17 @@ def ComputeExtendedDataSquare(data: Sequence[bytes], codec: Codec, treeCreatorFn
     h = ctypes.c_void_p()
     _check(library().rsm_eds_compute(device_context(_device_of(codec)), ptrs, lens, len(data), ctypes.byref(h)))
     return ExtendedDataSquare(h.value, codec, treeCreatorFn, _device_of(codec))
+
+
+def ComputeExtendedDataSquareWithBuffer(data: Sequence[bytes], codec: Codec, treeCreator: BufferedTreeConstructor):
+    """extendeddatasquare.go:81-92: ComputeExtendedDataSquare with the buffered
+    constructor's trees, root parallelism limited to treeCreator.TreeCount()."""
+    width = math.isqrt(len(data))
+    if width * width < len(data):
+        width += 1  # getWidth rounds up (datasquare.go:35-37); the shape check rejects it
+    eds = ComputeExtendedDataSquare(data, codec, treeCreator.NewConstructor(width))
+    eds.parallelOps = treeCreator.TreeCount()  # setParallelOps
+    return eds
 
 
 def ImportExtendedDataSquare(data: Sequence[Optional[bytes]], codec: Codec, treeCreatorFn=NewDefaultTree):

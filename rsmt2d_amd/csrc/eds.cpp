@@ -139,6 +139,8 @@ struct Tree {
     rsm_tree_root_fn fn;
     void* user;
     bool is_default() const { return fn == nullptr || fn == rsm_default_tree_root; }
+    // the library's own trees are pure functions: safe to call from many threads
+    bool pure() const { return is_default() || fn == rsm_nmt_tree_root; }
     // Returns 0 and the root, or non-zero on a tree error.
     int root(int axis, uint32_t index, const std::vector<const uint8_t*>& leaves, uint32_t S,
              std::vector<uint8_t>& out) const {
@@ -152,8 +154,8 @@ struct Tree {
     }
 };
 
-// Computes roots of many vectors; parallel over host threads for the default
-// (pure, thread-safe) tree, sequential for caller-provided trees.
+// Computes roots of many vectors; parallel over host threads for the library's
+// own (pure, thread-safe) trees, sequential for caller-provided trees.
 // jobs: (axis, index, leaves).  ok[i] = root computed; roots[i] = root bytes.
 void roots_many(const Tree& tree, const std::vector<int>& axes, const std::vector<uint32_t>& idxs,
                 const std::vector<std::vector<const uint8_t*>>& leaves, uint32_t S,
@@ -161,7 +163,7 @@ void roots_many(const Tree& tree, const std::vector<int>& axes, const std::vecto
     const size_t n = axes.size();
     roots.assign(n, {});
     rcs.assign(n, 0);
-    unsigned nt = tree.is_default() ? std::max(1u, std::min(64u, std::thread::hardware_concurrency())) : 1u;
+    unsigned nt = tree.pure() ? std::max(1u, std::min(64u, std::thread::hardware_concurrency())) : 1u;
     if (n < 8) nt = 1;
     if (nt == 1) {
         for (size_t i = 0; i < n; ++i) rcs[i] = tree.root(axes[i], idxs[i], leaves[i], S, roots[i]);
@@ -501,7 +503,7 @@ enum { kFallbackStuck = 1, kFallbackEncoding = 2, kFallbackRoots = 3 };
 // Flattened go by presence), and presence flips only after the device verification
 // passes.  Returns RSM_OK (repaired), 1 (fall back) or an RSM_E* error.
 int fast_repair_rows_zero_copy(rsm_eds* e, DevSquare& dev, const std::vector<uint32_t>& todo,
-                               const uint8_t* row_roots, const uint8_t* col_roots) {
+                               const uint8_t* row_roots, const uint8_t* col_roots, const DevTree& dt) {
     const uint32_t W = e->width, k = W / 2;
     const size_t S = e->S, row = (size_t)W * S;
     if (!e->data.pinned || ceil_pow2(k) != 128) return 1;
@@ -530,11 +532,16 @@ int fast_repair_rows_zero_copy(rsm_eds* e, DevSquare& dev, const std::vector<uin
     StreamScratch& ss = stream_scratch(dev.ctx, sv);
     std::lock_guard<std::mutex> lk(ss.mu);
     if ((r = hipStreamSynchronize(sv)) != hipSuccess) return hip_fail(r, "hipStreamSynchronize");
-    if ((r = ss.leaf.ensure((size_t)W * W * 32)) != hipSuccess) return hip_fail(r, "hipMalloc (leaf digests)");
+    if ((r = ss.leaf.ensure((size_t)W * W * (dt.nmt ? 64 : 32))) != hipSuccess)
+        return hip_fail(r, "hipMalloc (leaf digests)");
     uint32_t* leaf = static_cast<uint32_t*>(ss.leaf.ptr);
+    const uint32_t RL = dt.root_len;
     DevBuf& rb = dev.ctx->eds.roots;
-    if ((r = rb.ensure((size_t)2 * W * 32)) != hipSuccess) return hip_fail(r, "hipMalloc (roots)");
+    if ((r = rb.ensure((size_t)2 * W * RL)) != hipSuccess) return hip_fail(r, "hipMalloc (roots)");
     uint8_t* d_roots = static_cast<uint8_t*>(rb.ptr);
+    DevBuf& sb = dev.ctx->eds.status;
+    if ((r = sb.ensure((size_t)2 * W * 4)) != hipSuccess) return hip_fail(r, "hipMalloc (tree status)");
+    uint32_t* d_status = static_cast<uint32_t*>(sb.ptr);
     hipEvent_t ev[2];
     for (auto& x : ev) (void)hipEventCreateWithFlags(&x, hipEventDisableTiming);
     struct EvGuard {
@@ -605,24 +612,40 @@ int fast_repair_rows_zero_copy(rsm_eds* e, DevSquare& dev, const std::vector<uin
     cols.S = e->S;
     cols.pass = 1;
     if (int rc = launch_encode(dev.ctx, cols, sv)) return rc;
-    if ((r = launch_leaf_hashes(dev.d_eds, k * W, e->S, leaf, sv)) != hipSuccess) return hip_fail(r, "leaf hashes");
+    // DefaultTree: the top half's leaf digests while the bottom half is in flight
+    if (!dt.nmt && (r = launch_leaf_hashes(dev.d_eds, k * W, e->S, leaf, sv)) != hipSuccess)
+        return hip_fail(r, "leaf hashes");
     (void)hipStreamWaitEvent(sv, ev_bot, 0);
     e->stats.sweeps++;
     e->stats.decoded_vectors += (uint32_t)todo.size();
     uint32_t mismatch = 1;
-    std::vector<uint8_t> got((size_t)2 * W * 32);
-    if ((r = launch_leaf_hashes(dev.d_eds + (size_t)k * row, k * W, e->S, leaf + (size_t)k * W * 8, sv)) != hipSuccess ||
-        (r = hipMemsetAsync(dev.d_flags, 0, 4, sv)) != hipSuccess ||
+    std::vector<uint8_t> got((size_t)2 * W * RL);
+    std::vector<uint32_t> status((size_t)2 * W, 0);
+    if ((r = hipMemsetAsync(dev.d_flags, 0, 4, sv)) != hipSuccess ||
         (r = launch_compare(dev.d_eds + (size_t)k * row, dev.d_scratch + (size_t)k * row, (uint64_t)k * row,
-                            dev.d_flags, sv)) != hipSuccess ||
-        (r = launch_tree_roots(leaf, W, 0, 2 * W, d_roots, sv)) != hipSuccess ||  // latency-bound: one launch
-        (r = hipMemcpyAsync(&mismatch, dev.d_flags, 4, hipMemcpyDeviceToHost, sv)) != hipSuccess ||
+                            dev.d_flags, sv)) != hipSuccess)
+        return hip_fail(r, "verify (encoding)");
+    if (dt.nmt) {
+        // namespaced trees: leaves and nodes of the whole square in one launch pair
+        // (leaf scratch: sv's StreamScratch, held above)
+        if ((r = launch_nmt_roots(dev.d_eds, W, e->S, dt.p.namespace_size, dt.p.square_size, dt.p.ignore_max_namespace,
+                                  leaf, d_roots, d_status, sv)) != hipSuccess)
+            return hip_fail(r, "NMT roots");
+    } else if ((r = launch_leaf_hashes(dev.d_eds + (size_t)k * row, k * W, e->S, leaf + (size_t)k * W * 8, sv)) !=
+                   hipSuccess ||
+               (r = launch_tree_roots(leaf, W, 0, 2 * W, d_roots, sv)) != hipSuccess) {  // latency-bound: one launch
+        return hip_fail(r, "verify (roots)");
+    }
+    if ((r = hipMemcpyAsync(&mismatch, dev.d_flags, 4, hipMemcpyDeviceToHost, sv)) != hipSuccess ||
         (r = hipMemcpyAsync(got.data(), d_roots, got.size(), hipMemcpyDeviceToHost, sv)) != hipSuccess ||
+        (dt.nmt && (r = hipMemcpyAsync(status.data(), d_status, status.size() * 4, hipMemcpyDeviceToHost, sv)) !=
+                       hipSuccess) ||
         (r = hipStreamSynchronize(sv)) != hipSuccess)
         return hip_fail(r, "verify");
     const bool enc_ok = mismatch == 0;
-    const bool roots_ok = memcmp(got.data(), row_roots, (size_t)W * 32) == 0 &&
-                          memcmp(got.data() + (size_t)W * 32, col_roots, (size_t)W * 32) == 0;
+    const bool roots_ok = std::all_of(status.begin(), status.end(), [](uint32_t x) { return x == 0; }) &&
+                          memcmp(got.data(), row_roots, (size_t)W * RL) == 0 &&
+                          memcmp(got.data() + (size_t)W * RL, col_roots, (size_t)W * RL) == 0;
     if (!enc_ok || !roots_ok) {
         e->stats.fallback_reason = enc_ok ? kFallbackRoots : kFallbackEncoding;
         return 1;
@@ -635,7 +658,9 @@ int fast_repair_rows_zero_copy(rsm_eds* e, DevSquare& dev, const std::vector<uin
 int fast_repair(rsm_eds* e, DevSquare& dev, const uint8_t* row_roots, const uint8_t* col_roots,
                 uint32_t root_len, const Tree& tree) {
     const uint32_t W = e->width, k = W / 2;
-    if (tree.is_default() && root_len == 32 && roots_dev_supported(W)) {
+    DevTree dt;
+    const bool dev_tree = device_tree_for(tree.fn, tree.user, W, &dt) && root_len == dt.root_len;
+    if (dev_tree) {
         // one row sweep completes the square?  then the pipelined form
         std::vector<uint32_t> todo;
         bool rows_only = true;
@@ -649,7 +674,7 @@ int fast_repair(rsm_eds* e, DevSquare& dev, const uint8_t* row_roots, const uint
             }
         }
         if (rows_only && !todo.empty()) {
-            int rc = fast_repair_rows_zero_copy(e, dev, todo, row_roots, col_roots);
+            int rc = fast_repair_rows_zero_copy(e, dev, todo, row_roots, col_roots, dt);
             if (rc <= 0 || e->stats.fallback_reason) return rc;  // repaired / error / byzantine evidence
         }
     }
@@ -699,22 +724,30 @@ int fast_repair(rsm_eds* e, DevSquare& dev, const uint8_t* row_roots, const uint
     // DefaultTree (kernels_sha.hip), through the host Tree plugin otherwise.  The
     // device check runs before any copy back, so an accepted square lands straight
     // in the EDS's own (already resident) buffer and a rejected one costs no D2H.
-    if (tree.is_default() && root_len == 32 && roots_dev_supported(W)) {
+    if (dev_tree) {
+        const uint32_t RL = dt.root_len;
         DevBuf& rb = dev.ctx->eds.roots;
-        if ((r = rb.ensure((size_t)2 * W * 32)) != hipSuccess) return hip_fail(r, "hipMalloc (roots)");
-        if (int rc = device_roots(dev.ctx, dev.d_eds, W, e->S, static_cast<uint8_t*>(rb.ptr), dev.st)) return rc;
-        std::vector<uint8_t> got((size_t)2 * W * 32);
+        DevBuf& sb = dev.ctx->eds.status;
+        if ((r = rb.ensure((size_t)2 * W * RL)) != hipSuccess) return hip_fail(r, "hipMalloc (roots)");
+        if ((r = sb.ensure((size_t)2 * W * 4)) != hipSuccess) return hip_fail(r, "hipMalloc (tree status)");
+        if (int rc = device_tree_roots(dev.ctx, dt, dev.d_eds, W, e->S, static_cast<uint8_t*>(rb.ptr),
+                                       static_cast<uint32_t*>(sb.ptr), dev.st))
+            return rc;
+        std::vector<uint8_t> got((size_t)2 * W * RL);
+        std::vector<uint32_t> status((size_t)2 * W);
         if ((r = hipMemcpyAsync(&mismatch, dev.d_flags, 4, hipMemcpyDeviceToHost, dev.st)) != hipSuccess)
             return hip_fail(r, "D2H flag");
-        if ((r = hipMemcpyAsync(got.data(), rb.ptr, got.size(), hipMemcpyDeviceToHost, dev.st)) != hipSuccess)
+        if ((r = hipMemcpyAsync(got.data(), rb.ptr, got.size(), hipMemcpyDeviceToHost, dev.st)) != hipSuccess ||
+            (r = hipMemcpyAsync(status.data(), sb.ptr, status.size() * 4, hipMemcpyDeviceToHost, dev.st)) != hipSuccess)
             return hip_fail(r, "D2H roots");
         if (int rc = dev.sync()) return rc;
         if (mismatch) {
             e->stats.fallback_reason = kFallbackEncoding;
             return 1;
         }
-        if (memcmp(got.data(), row_roots, (size_t)W * 32) != 0 ||
-            memcmp(got.data() + (size_t)W * 32, col_roots, (size_t)W * 32) != 0) {
+        if (!std::all_of(status.begin(), status.end(), [](uint32_t x) { return x == 0; }) ||
+            memcmp(got.data(), row_roots, (size_t)W * RL) != 0 ||
+            memcmp(got.data() + (size_t)W * RL, col_roots, (size_t)W * RL) != 0) {
             e->stats.fallback_reason = kFallbackRoots;
             return 1;
         }
@@ -884,25 +917,38 @@ int rsm_eds_roots(rsm_eds* e, int axis, rsm_tree_root_fn tree_fn, void* user, ui
     if (!e || !roots_out || !root_len || (axis != RSM_AXIS_ROW && axis != RSM_AXIS_COL))
         return fail(RSM_EINVAL, "roots: bad arguments");
     Tree tree{tree_fn, user};
-    if (tree.is_default() && e->ctx && root_cap >= 32 && roots_dev_supported(e->width) &&
+    DevTree dt;
+    if (e->ctx && device_tree_for(tree_fn, user, e->width, &dt) && root_cap >= dt.root_len &&
         std::all_of(e->present.begin(), e->present.end(), [](uint8_t p) { return p != 0; })) {
-        // complete square + DefaultTree: every leaf and node hash on the GPU
-        const uint32_t W = e->width;
+        // complete square + a tree the GPU computes (DefaultTree, NMT): every leaf
+        // and node hash on the device
+        const uint32_t W = e->width, RL = dt.root_len;
         std::lock_guard<std::mutex> lk(e->ctx->eds_mu);
         DevSquare dev{};
         if (int rc = dev.init(e->ctx, W, e->S)) return rc;
         hipError_t r = hipMemcpyAsync(dev.d_eds, e->data.data(), e->data.size(), hipMemcpyHostToDevice, dev.st);
         if (r != hipSuccess) return hip_fail(r, "H2D square");
         DevBuf& rb = e->ctx->eds.roots;
-        if ((r = rb.ensure((size_t)2 * W * 32)) != hipSuccess) return hip_fail(r, "hipMalloc (roots)");
-        if (int rc = device_roots(e->ctx, dev.d_eds, W, e->S, static_cast<uint8_t*>(rb.ptr), dev.st)) return rc;
-        std::vector<uint8_t> got((size_t)W * 32);
-        if ((r = hipMemcpyAsync(got.data(), static_cast<uint8_t*>(rb.ptr) + (size_t)(axis == RSM_AXIS_COL) * W * 32,
-                                got.size(), hipMemcpyDeviceToHost, dev.st)) != hipSuccess)
+        DevBuf& sb = e->ctx->eds.status;
+        if ((r = rb.ensure((size_t)2 * W * RL)) != hipSuccess) return hip_fail(r, "hipMalloc (roots)");
+        if ((r = sb.ensure((size_t)2 * W * 4)) != hipSuccess) return hip_fail(r, "hipMalloc (tree status)");
+        if (int rc = device_tree_roots(e->ctx, dt, dev.d_eds, W, e->S, static_cast<uint8_t*>(rb.ptr),
+                                       static_cast<uint32_t*>(sb.ptr), dev.st))
+            return rc;
+        const size_t ax = axis == RSM_AXIS_COL ? 1 : 0;
+        std::vector<uint8_t> got((size_t)W * RL);
+        std::vector<uint32_t> status(W);
+        if ((r = hipMemcpyAsync(got.data(), static_cast<uint8_t*>(rb.ptr) + ax * W * RL, got.size(),
+                                hipMemcpyDeviceToHost, dev.st)) != hipSuccess ||
+            (r = hipMemcpyAsync(status.data(), static_cast<uint32_t*>(sb.ptr) + ax * W, status.size() * 4,
+                                hipMemcpyDeviceToHost, dev.st)) != hipSuccess)
             return hip_fail(r, "D2H roots");
         if (int rc = dev.sync()) return rc;
-        for (uint32_t i = 0; i < W; ++i) memcpy(roots_out + (size_t)i * root_cap, got.data() + (size_t)i * 32, 32);
-        *root_len = 32;
+        for (uint32_t i = 0; i < W; ++i) {
+            if (status[i]) return fail(RSM_ETREE, "tree error computing root %u (namespace push order)", i);
+            memcpy(roots_out + (size_t)i * root_cap, got.data() + (size_t)i * RL, RL);
+        }
+        *root_len = RL;
         return RSM_OK;
     }
     std::vector<int> axes;

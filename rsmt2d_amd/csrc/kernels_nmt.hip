@@ -1,0 +1,284 @@
+// kernels_nmt.hip -- row and column namespaced-Merkle-tree roots of a
+// device-resident EDS, as rsmt2d's erasured NMT wrappers build them
+// (nmtwrapper_test.go:94-120; the pooled tree nmtbuffered_tree_test.go:118-152
+// pushes identically) over celestiaorg/nmt v0.24.3 (go.mod:7, not vendored;
+// published algorithm restated in merkle.cpp and oracle/nmt.py):
+//   cell (r, c) is pushed as ns || share, ns = share[:NS] when r < k and c < k
+//   (quadrant 0; the same for the cell's row tree and its column tree), else the
+//   parity namespace 0xFF..;
+//   leaf node  = ns || ns || H(0x00 || ns || share);
+//   inner node = l.min || max || H(0x01 || l || r), max = l.max when r.min is the
+//                parity namespace (IgnoreMaxNamespace), else r.max;
+//   root       = RFC 6962 split: pairing level by level and carrying an unpaired
+//                last node up unchanged gives the same tree.
+// Push order (namespaces non-decreasing along a vector) and sibling order are
+// checked; a failing tree reports status 1 (the reference's Push/Root error,
+// which Repair turns into ErrByzantineData, extendeddatacrossword.go:316-320).
+//
+// Two kernels, as for the DefaultTree (kernels_sha.hip):
+//   nmt_leaf_kernel : one thread per cell, streams ns || share through SHA-256;
+//                     one leaf record (ns, digest) serves the cell's row and column.
+//   nmt_tree_kernel : one workgroup per tree, levels ping-pong in LDS; each thread
+//                     lays its node message out in its own LDS bytes and hashes it.
+// Namespace sizes up to 32 bytes (Celestia: 29), widths up to 1024 (LDS permitting).
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#include "sha256_dev.hpp"
+
+namespace rsm {
+
+namespace {
+
+constexpr uint32_t kMaxNs = 32;
+constexpr uint32_t kNsWords = kMaxNs / 4;
+constexpr uint32_t kNodeWords = 3 * kNsWords;  // min[8] | max[8] | digest[8] (LDS)
+constexpr uint32_t kLeafWords = 16;            // ns[8] | digest[8] (global, per cell)
+constexpr uint32_t kMaxWidth = 1024;
+constexpr size_t kLdsCap = 160 * 1024 - 256;  // per workgroup, less the static words
+
+// SHA blocks of a node message 0x01 || l || r (nodes of 2 ns + 32 bytes)
+__host__ __device__ constexpr uint32_t node_blocks(uint32_t ns) { return (1 + 2 * (2 * ns + 32) + 8) / 64 + 1; }
+size_t tree_lds_bytes(uint32_t W, uint32_t ns) {
+    return ((size_t)2 * (W / 2) * kNodeWords + (size_t)256 * 16 * node_blocks(ns)) * 4;
+}
+
+// the first n bytes of a big-endian word (n clamped to 0..4)
+__device__ __forceinline__ uint32_t head_mask(int n) {
+    return n <= 0 ? 0u : (n >= 4 ? 0xFFFFFFFFu : ~(0xFFFFFFFFu >> (8 * n)));
+}
+__device__ __forceinline__ uint32_t be_word(const uint32_t* p, int i) { return __builtin_bswap32(p[i]); }
+
+// Leaf records: leaf[cell][0..7] = namespace (big-endian words, zero padded),
+// leaf[cell][8..15] = SHA256(0x00 || ns || share).
+__global__ __launch_bounds__(256) void nmt_leaf_kernel(const uint8_t* __restrict__ eds, uint32_t W, uint32_t S,
+                                                       uint32_t ns, uint32_t k, uint32_t* __restrict__ leaf) {
+    const uint32_t cell = blockIdx.x * 256u + threadIdx.x;
+    if (cell >= W * W) return;
+    const uint32_t r = cell / W, c = cell - r * W;
+    const bool q0 = r < k && c < k;
+    const uint32_t* dw = reinterpret_cast<const uint32_t*>(eds + (uint64_t)cell * S);
+    const int nD = (int)(S / 4u);
+    const int off = 1 + (int)ns;           // message bytes before the share
+    const int L = off + (int)S;            // message length
+    const int m0 = off >> 2;               // first word holding share bytes
+    const uint32_t sh = 8u * (uint32_t)(off & 3);
+    const int nb = (L + 8) / 64 + 1;       // SHA blocks
+    // the namespace prefix words (message words 0..8 at most): 0x00 || ns
+    uint32_t d0[kNsWords + 1];
+#pragma unroll
+    for (int i = 0; i <= (int)kNsWords; ++i) d0[i] = be_word(dw, i < nD ? i : 0);
+    uint32_t h[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) h[i] = kH0[i];
+    uint32_t prev = 0;
+    for (int b = 0; b < nb; ++b) {
+        uint32_t w[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int m = 16 * b + i;
+            const int p = 4 * m;  // byte position of the word
+            uint32_t pre = 0;
+            if (m <= (int)kNsWords) {  // only block 0 reaches here (m <= 8)
+                const uint32_t lo = d0[i <= (int)kNsWords ? i : 0];
+                const uint32_t hi = i >= 1 && i <= (int)kNsWords + 1 ? d0[i >= 1 ? i - 1 : 0] : 0u;
+                pre = q0 ? __builtin_amdgcn_alignbit(m == 0 ? 0u : hi, lo, 8) : (m == 0 ? 0x00FFFFFFu : 0xFFFFFFFFu);
+            }
+            const int j = m - m0;  // share word index of this message word
+            const uint32_t cur = be_word(dw, j < 0 ? 0 : (j < nD ? j : nD - 1));
+            const uint32_t r2 = __builtin_amdgcn_alignbit(j <= 0 ? 0u : prev, cur, sh);
+            prev = cur;
+            const uint32_t mpre = head_mask(off - p);
+            const uint32_t mr2 = head_mask(L - p) & ~mpre;
+            uint32_t x = (pre & mpre) | (r2 & mr2);
+            if (p <= L && L < p + 4) x |= 0x80u << (8 * (3 - (L - p)));
+            if (b == nb - 1 && i == 15) x = 8u * (uint32_t)L;  // bit length (< 2^32), word 14 stays 0
+            w[i] = x;
+        }
+        sha_block(h, w);
+    }
+    uint32_t* o = leaf + (uint64_t)cell * kLeafWords;
+#pragma unroll
+    for (int i = 0; i < (int)kNsWords; ++i) o[i] = (q0 ? d0[i] : 0xFFFFFFFFu) & head_mask((int)ns - 4 * i);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[kNsWords + i] = h[i];
+}
+
+struct Node {
+    uint32_t mn[kNsWords], mx[kNsWords], d[8];
+};
+
+// a < b over namespaces held as zero-padded big-endian words
+__device__ __forceinline__ bool ns_less(const uint32_t (&a)[kNsWords], const uint32_t (&b)[kNsWords]) {
+#pragma unroll
+    for (int i = 0; i < (int)kNsWords; ++i)
+        if (a[i] != b[i]) return a[i] < b[i];
+    return false;
+}
+
+// byte i of a big-endian word array (i static after unrolling)
+__device__ __forceinline__ uint8_t be_byte(const uint32_t* w, int i) { return (uint8_t)(w[i >> 2] >> (24 - 8 * (i & 3))); }
+
+// HashNode(l, r) (nmt hasher): message 0x01 || l || r laid out in this thread's
+// LDS bytes `mb`, then hashed as big-endian words.  Returns false on unordered
+// siblings (r.min < l.max).
+__device__ __forceinline__ bool hash_node(const Node& l, const Node& r, uint32_t ns, bool ignore_max, uint8_t* mb, Node& out) {
+    const int NL = 2 * (int)ns + 32;
+    const int len = 1 + 2 * NL;
+    const int nb = (int)node_blocks(ns);
+    uint32_t* mw = reinterpret_cast<uint32_t*>(mb);
+    for (int i = 0; i < 16 * nb; ++i) mw[i] = 0;
+    mb[0] = 0x01;
+    auto put = [&](const Node& n, int at) {
+#pragma unroll
+        for (int i = 0; i < (int)kMaxNs; ++i)
+            if (i < (int)ns) {
+                mb[at + i] = be_byte(n.mn, i);
+                mb[at + (int)ns + i] = be_byte(n.mx, i);
+            }
+#pragma unroll
+        for (int i = 0; i < 32; ++i) mb[at + 2 * (int)ns + i] = be_byte(n.d, i);
+    };
+    put(l, 1);
+    put(r, 1 + NL);
+    mb[len] = 0x80;
+    const uint32_t bits = 8u * (uint32_t)len;
+    mb[64 * nb - 2] = (uint8_t)(bits >> 8);
+    mb[64 * nb - 1] = (uint8_t)bits;
+    uint32_t h[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) h[i] = kH0[i];
+    for (int b = 0; b < nb; ++b) {
+        uint32_t w[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w[i] = __builtin_bswap32(mw[16 * b + i]);
+        sha_block(h, w);
+    }
+    bool rmin_is_max = true;
+#pragma unroll
+    for (int i = 0; i < (int)kNsWords; ++i) rmin_is_max &= r.mn[i] == head_mask((int)ns - 4 * i);
+    const bool ok = !ns_less(r.mn, l.mx);
+#pragma unroll
+    for (int i = 0; i < (int)kNsWords; ++i) {
+        out.mn[i] = l.mn[i];
+        out.mx[i] = (ignore_max && rmin_is_max) ? l.mx[i] : r.mx[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) out.d[i] = h[i];
+    return ok;
+}
+
+__device__ __forceinline__ void leaf_node(const uint32_t* __restrict__ leaf, uint64_t cell, Node& n) {
+    const uint32_t* s = leaf + cell * kLeafWords;
+#pragma unroll
+    for (int i = 0; i < (int)kNsWords; ++i) n.mn[i] = n.mx[i] = s[i];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) n.d[i] = s[kNsWords + i];
+}
+__device__ __forceinline__ void lds_node(const uint32_t* p, Node& n) {
+#pragma unroll
+    for (int i = 0; i < (int)kNsWords; ++i) n.mn[i] = p[i], n.mx[i] = p[kNsWords + i];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) n.d[i] = p[2 * kNsWords + i];
+}
+__device__ __forceinline__ void lds_store(uint32_t* p, const Node& n) {
+#pragma unroll
+    for (int i = 0; i < (int)kNsWords; ++i) p[i] = n.mn[i], p[kNsWords + i] = n.mx[i];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) p[2 * kNsWords + i] = n.d[i];
+}
+
+// One workgroup per tree (blockIdx.x < W: row tree, else column tree).  Dynamic
+// LDS: two levels of W/2 nodes (ping-pong) + 256 per-thread message buffers.
+__global__ __launch_bounds__(256) void nmt_tree_kernel(const uint32_t* __restrict__ leaf, uint32_t W, uint32_t ns,
+                                                       uint32_t ignore_max, uint8_t* __restrict__ roots,
+                                                       uint32_t* __restrict__ status) {
+    extern __shared__ uint32_t lds[];
+    const uint32_t half = W / 2;
+    auto lvl = [&](uint32_t which) -> uint32_t* { return lds + (size_t)which * half * kNodeWords; };
+    uint8_t* mb = reinterpret_cast<uint8_t*>(lds + (size_t)2 * half * kNodeWords) + threadIdx.x * (64u * node_blocks(ns));
+    __shared__ uint32_t bad;
+    if (threadIdx.x == 0) bad = 0;
+    __syncthreads();
+    const uint32_t tree = blockIdx.x;
+    const uint32_t axis = tree >= W ? 1u : 0u;
+    const uint32_t idx = tree - axis * W;
+    auto cell_of = [&](uint32_t pos) -> uint64_t { return axis == 0 ? (uint64_t)idx * W + pos : (uint64_t)pos * W + idx; };
+    const bool ig = ignore_max != 0;
+    uint32_t my_bad = 0;
+    // level 1 from the leaf records: pairs (2j, 2j+1); push order checked on
+    // every consecutive leaf pair
+    uint32_t cnt = W;
+    uint32_t next = (cnt + 1) / 2;
+    for (uint32_t j = threadIdx.x; j < next; j += 256u) {
+        Node a, b, o;
+        leaf_node(leaf, cell_of(2 * j), a);
+        if (2 * j + 1 < cnt) {
+            leaf_node(leaf, cell_of(2 * j + 1), b);
+            if (ns_less(b.mn, a.mn)) my_bad = 1;
+            if (2 * j + 2 < cnt) {
+                Node c;
+                leaf_node(leaf, cell_of(2 * j + 2), c);
+                if (ns_less(c.mn, b.mn)) my_bad = 1;
+            }
+            if (!hash_node(a, b, ns, ig, mb, o)) my_bad = 1;
+        } else {
+            o = a;
+        }
+        lds_store(lvl(0) + (size_t)j * kNodeWords, o);
+    }
+    __syncthreads();
+    uint32_t cur = 0;
+    for (cnt = next; cnt > 1; cnt = next) {
+        next = (cnt + 1) / 2;
+        for (uint32_t j = threadIdx.x; j < next; j += 256u) {
+            Node a, b, o;
+            lds_node(lvl(cur) + (size_t)(2 * j) * kNodeWords, a);
+            if (2 * j + 1 < cnt) {
+                lds_node(lvl(cur) + (size_t)(2 * j + 1) * kNodeWords, b);
+                if (!hash_node(a, b, ns, ig, mb, o)) my_bad = 1;
+            } else {
+                o = a;
+            }
+            lds_store(lvl(cur ^ 1u) + (size_t)j * kNodeWords, o);
+        }
+        __syncthreads();
+        cur ^= 1u;
+    }
+    if (my_bad) atomicOr(&bad, 1u);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        Node rt;
+        lds_node(lvl(cur), rt);
+        uint8_t* o = roots + (uint64_t)tree * (2 * ns + 32);
+#pragma unroll
+        for (int i = 0; i < (int)kMaxNs; ++i)
+            if (i < (int)ns) {
+                o[i] = be_byte(rt.mn, i);
+                o[ns + i] = be_byte(rt.mx, i);
+            }
+#pragma unroll
+        for (int i = 0; i < 32; ++i) o[2 * ns + i] = be_byte(rt.d, i);
+        if (status) status[tree] = bad;
+    }
+}
+
+}  // namespace
+
+bool nmt_dev_supported(uint32_t W, uint32_t ns) {
+    return W >= 2 && W <= kMaxWidth && ns >= 1 && ns <= kMaxNs && tree_lds_bytes(W, ns) <= kLdsCap;
+}
+
+// d_leaf: W*W*64 bytes of scratch.
+hipError_t launch_nmt_roots(const uint8_t* d_eds, uint32_t W, uint32_t S, uint32_t ns, uint32_t k, uint32_t ignore_max,
+                            uint32_t* d_leaf, uint8_t* d_roots, uint32_t* d_status, hipStream_t st) {
+    const uint32_t cells = W * W;
+    hipLaunchKernelGGL(nmt_leaf_kernel, dim3((cells + 255) / 256), dim3(256), 0, st, d_eds, W, S, ns, k, d_leaf);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const size_t lds = tree_lds_bytes(W, ns);
+    hipLaunchKernelGGL(nmt_tree_kernel, dim3(2 * W), dim3(256), lds, st, d_leaf, W, ns, ignore_max, d_roots, d_status);
+    return hipGetLastError();
+}
+
+}  // namespace rsm

@@ -17,55 +17,11 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
+#include "sha256_dev.hpp"
+
 namespace rsm {
 
 namespace {
-
-__constant__ uint32_t kK[64] = {
-    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
-    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
-    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
-    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
-    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
-    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
-    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
-    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
-
-constexpr uint32_t kH0[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
-                             0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
-
-__device__ __forceinline__ uint32_t rotr(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, n); }
-// Big-endian message word whose first byte is the last byte of `prev` and whose
-// other three are the first three bytes of `cur` (both big-endian words): the
-// 1-byte domain prefix shifts every share word by one byte.
-__device__ __forceinline__ uint32_t shift8(uint32_t prev, uint32_t cur) {
-    return __builtin_amdgcn_alignbit(prev, cur, 8);
-}
-
-// three-input XOR in one VALU op (gfx950 v_bitop3_b32, truth table 0x96)
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
-}
-
-__device__ __forceinline__ void sha_block(uint32_t (&h)[8], uint32_t (&w)[16]) {
-    uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
-#pragma unroll
-    for (int i = 0; i < 64; ++i) {
-        if (i >= 16) {
-            const uint32_t x = w[(i + 1) & 15], y = w[(i + 14) & 15];
-            const uint32_t s0 = xor3(rotr(x, 7), rotr(x, 18), x >> 3);
-            const uint32_t s1 = xor3(rotr(y, 17), rotr(y, 19), y >> 10);
-            w[i & 15] += s0 + w[(i + 9) & 15] + s1;
-        }
-        const uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
-        const uint32_t ch = (e & f) ^ (~e & g);
-        const uint32_t t1 = hh + S1 + ch + kK[i] + w[i & 15];
-        const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
-        const uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
-        hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
-    }
-    h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
-}
 
 // SHA256(0x01 || L || R) for digests held as 8 big-endian words each.
 __device__ __forceinline__ void node_hash(const uint32_t (&L)[8], const uint32_t (&R)[8], uint32_t (&out)[8]) {

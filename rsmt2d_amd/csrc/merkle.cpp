@@ -5,6 +5,11 @@
 // (push joins equal-height subtrees; Root folds the stack from the newest).
 // The Tree plugin is out of the GPU hot path: it stays on
 // the host, and callers may pass their own rsm_tree_root_fn instead.
+//
+// Also the host form of the namespaced Merkle tree (celestiaorg/nmt v0.24.3, a
+// go.mod dependency absent from /root/reference) as rsmt2d's NMT wrappers push it
+// (nmtwrapper_test.go:94-120, nmtbuffered_tree_test.go:118-152): see
+// rsm_nmt_tree_root below; the device form is kernels_nmt.hip.
 #include <cstdint>
 #include <cstring>
 #include <vector>
@@ -106,7 +111,94 @@ Digest node_hash(const Digest& l, const Digest& r) {
     return o;
 }
 
+// ---- namespaced Merkle tree (celestiaorg/nmt v0.24.3, published algorithm) ----
+// A node is minNs || maxNs || digest.  HashLeaf(ndata) = ns || ns || H(0x00 || ndata)
+// with ns = ndata[:nsSize]; HashNode(l, r) = l.min || max || H(0x01 || l || r) where
+// max = l.max when IgnoreMaxNamespace and r.min is the all-0xFF namespace, else
+// r.max; the root over n leaves splits at the largest power of two below n
+// (RFC 6962 MTH).  Empty tree: zero namespaces || H("").
+struct NmtNode {
+    std::vector<uint8_t> b;  // 2*ns + 32 bytes
+};
+
+NmtNode nmt_leaf(const uint8_t* ns, uint32_t nsz, const uint8_t* share, uint32_t S) {
+    Sha256 s;
+    uint8_t pre = 0x00;
+    s.update(&pre, 1);
+    s.update(ns, nsz);
+    s.update(share, S);
+    NmtNode o;
+    o.b.resize(2 * nsz + 32);
+    memcpy(o.b.data(), ns, nsz);
+    memcpy(o.b.data() + nsz, ns, nsz);
+    s.final(o.b.data() + 2 * nsz);
+    return o;
+}
+
+bool nmt_node(const NmtNode& l, const NmtNode& r, uint32_t nsz, bool ignore_max, NmtNode& o) {
+    const uint8_t *lmin = l.b.data(), *lmax = lmin + nsz, *rmin = r.b.data(), *rmax = rmin + nsz;
+    if (memcmp(lmax, rmin, nsz) > 0) return false;  // validateSiblingsNamespaceOrder
+    bool rmin_is_max = true;
+    for (uint32_t i = 0; i < nsz; ++i) rmin_is_max &= rmin[i] == 0xFF;
+    const uint8_t* mx = (ignore_max && rmin_is_max) ? lmax : rmax;
+    Sha256 s;
+    uint8_t pre = 0x01;
+    s.update(&pre, 1);
+    s.update(l.b.data(), l.b.size());
+    s.update(r.b.data(), r.b.size());
+    o.b.resize(2 * nsz + 32);
+    memcpy(o.b.data(), lmin, nsz);
+    memcpy(o.b.data() + nsz, mx, nsz);
+    s.final(o.b.data() + 2 * nsz);
+    return true;
+}
+
+bool nmt_root(const std::vector<NmtNode>& leaf, uint32_t lo, uint32_t hi, uint32_t nsz, bool ignore_max, NmtNode& out) {
+    const uint32_t n = hi - lo;
+    if (n == 1) {
+        out = leaf[lo];
+        return true;
+    }
+    uint32_t k = 1;
+    while (k * 2 < n) k *= 2;  // largest power of two < n
+    NmtNode l, r;
+    return nmt_root(leaf, lo, lo + k, nsz, ignore_max, l) && nmt_root(leaf, lo + k, hi, nsz, ignore_max, r) &&
+           nmt_node(l, r, nsz, ignore_max, out);
+}
+
 }  // namespace
+
+extern "C" int rsm_nmt_tree_root(void* user, int /*axis*/, uint32_t index, const uint8_t* const* leaves,
+                                 uint32_t n_leaves, uint32_t leaf_size, uint8_t* root_out, uint32_t* root_len) {
+    const auto* p = static_cast<const rsm_nmt_params*>(user);
+    if (!p || !root_len || !root_out || p->namespace_size == 0 || p->square_size == 0) return RSM_EINVAL;
+    const uint32_t nsz = p->namespace_size, k = p->square_size;
+    if (*root_len < 2 * nsz + 32) return RSM_EINVAL;
+    // erasuredNamespacedMerkleTree.Push (nmtwrapper_test.go:94-120)
+    if (index + 1 > 2 * k || n_leaves > 2 * k) return RSM_ETREE;  // pushed past predetermined square size
+    if (leaf_size < nsz) return RSM_ETREE;                         // data is too short to contain namespace ID
+    std::vector<uint8_t> parity(nsz, 0xFF);
+    std::vector<NmtNode> leaf(n_leaves);
+    const uint8_t* prev = nullptr;
+    for (uint32_t i = 0; i < n_leaves; ++i) {
+        if (!leaves[i]) return RSM_ETREE;
+        const uint8_t* ns = (i < k && index < k) ? leaves[i] : parity.data();  // isQuadrantZero
+        if (prev && memcmp(ns, prev, nsz) < 0) return RSM_ETREE;           // nmt: ErrInvalidPushOrder
+        prev = ns;
+        leaf[i] = nmt_leaf(ns, nsz, leaves[i], leaf_size);
+    }
+    NmtNode root;
+    if (n_leaves == 0) {
+        Sha256 s;
+        root.b.assign(2 * nsz + 32, 0);
+        s.final(root.b.data() + 2 * nsz);
+    } else if (!nmt_root(leaf, 0, n_leaves, nsz, p->ignore_max_namespace != 0, root)) {
+        return RSM_ETREE;
+    }
+    memcpy(root_out, root.b.data(), root.b.size());
+    *root_len = (uint32_t)root.b.size();
+    return RSM_OK;
+}
 
 extern "C" int rsm_default_tree_root(void* /*user*/, int /*axis*/, uint32_t /*index*/,
                                      const uint8_t* const* leaves, uint32_t n_leaves, uint32_t leaf_size,

@@ -67,7 +67,15 @@ struct StreamScratch {
 // Buffers of the ExtendedDataSquare layer (Repair, device roots of an EDS):
 // used only under rsm_ctx::eds_mu, on the context stream.
 struct EdsBufs {
-    DevBuf eds, scratch, pres, idx, flags, roots;
+    DevBuf eds, scratch, pres, idx, flags, roots, status;
+};
+
+// A Tree plugin the GPU computes itself: the DefaultTree (tree_fn NULL or
+// rsm_default_tree_root) or the namespaced Merkle tree (rsm_nmt_tree_root).
+struct DevTree {
+    bool nmt = false;
+    rsm_nmt_params p{};
+    uint32_t root_len = 32;
 };
 
 }  // namespace rsm
@@ -136,5 +144,12 @@ int extend_squares(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, uint32_
 // when W is outside roots_dev_supported().
 int device_roots(rsm_ctx* ctx, const uint8_t* d_eds, uint32_t W, uint32_t S, uint8_t* d_roots, hipStream_t st,
                  uint32_t squares = 1);
+// Whether (tree_fn, user) is a tree the GPU computes for a square of width W.
+bool device_tree_for(rsm_tree_root_fn fn, void* user, uint32_t W, DevTree* out);
+// Roots of all 2W trees of a complete device square: d_roots 2W * t.root_len bytes
+// (rows, then columns); d_status 2W words, non-zero where a tree fails (NMT push
+// order; all zero for the DefaultTree).  Asynchronous on st.
+int device_tree_roots(rsm_ctx* ctx, const DevTree& t, const uint8_t* d_eds, uint32_t W, uint32_t S,
+                      uint8_t* d_roots, uint32_t* d_status, hipStream_t st);
 
 }  // namespace rsm

@@ -280,6 +280,46 @@ int device_roots(rsm_ctx* ctx, const uint8_t* d_eds, uint32_t W, uint32_t S, uin
     return RSM_OK;
 }
 
+bool device_tree_for(rsm_tree_root_fn fn, void* user, uint32_t W, DevTree* out) {
+    DevTree t;
+    if (fn == nullptr || fn == rsm_default_tree_root) {
+        if (!roots_dev_supported(W)) return false;
+    } else if (fn == rsm_nmt_tree_root && user) {
+        t.nmt = true;
+        t.p = *static_cast<const rsm_nmt_params*>(user);
+        // the plugin's own errors (past the square, too short) stay on the host path
+        if (!nmt_dev_supported(W, t.p.namespace_size) || t.p.square_size == 0 || W > 2 * t.p.square_size)
+            return false;
+        t.root_len = 2 * t.p.namespace_size + 32;
+    } else {
+        return false;
+    }
+    *out = t;
+    return true;
+}
+
+int device_tree_roots(rsm_ctx* ctx, const DevTree& t, const uint8_t* d_eds, uint32_t W, uint32_t S,
+                      uint8_t* d_roots, uint32_t* d_status, hipStream_t st) {
+    hipError_t e;
+    if (!t.nmt) {
+        if (d_status && (e = hipMemsetAsync(d_status, 0, (size_t)2 * W * 4, st)) != hipSuccess)
+            return hip_fail(e, "hipMemsetAsync (status)");
+        return device_roots(ctx, d_eds, W, S, d_roots, st);
+    }
+    if (S < t.p.namespace_size) return fail(RSM_ETREE, "data is too short to contain namespace ID");
+    StreamScratch& ss = stream_scratch(ctx, st);
+    std::lock_guard<std::mutex> lk(ss.mu);
+    const size_t need = (size_t)W * W * 64;
+    if (need > ss.leaf.cap) {
+        if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+        if ((e = ss.leaf.ensure(need)) != hipSuccess) return hip_fail(e, "hipMalloc (NMT leaves)");
+    }
+    if ((e = launch_nmt_roots(d_eds, W, S, t.p.namespace_size, t.p.square_size, t.p.ignore_max_namespace,
+                              static_cast<uint32_t*>(ss.leaf.ptr), d_roots, d_status, st)) != hipSuccess)
+        return hip_fail(e, "NMT roots kernel launch");
+    return RSM_OK;
+}
+
 // One square host -> device -> host on `st`: the ODS goes straight into the EDS's
 // top-left quadrant (the EDS aliases the ODS); only Q1, Q2 and Q3 come back, the
 // caller's Q0 quadrant is filled from its own ODS on the host.
@@ -625,6 +665,19 @@ int rsm_roots_dev(rsm_ctx* ctx, const void* d_eds, uint32_t width, uint32_t shar
     if (int rc = use_device(ctx)) return rc;
     return device_roots(ctx, static_cast<const uint8_t*>(d_eds), width, share_size, static_cast<uint8_t*>(d_roots),
                         pick(ctx, stream));
+}
+
+int rsm_nmt_roots_dev(rsm_ctx* ctx, const void* d_eds, uint32_t width, uint32_t share_size,
+                      const rsm_nmt_params* params, void* d_roots, void* d_status, void* stream) {
+    if (!ctx || !d_eds || !d_roots || !params || width == 0) return fail(RSM_EINVAL, "rsm_nmt_roots_dev: bad arguments");
+    if (int rc = validate_chunk_size(share_size)) return rc;
+    if (int rc = use_device(ctx)) return rc;
+    DevTree t;
+    if (!device_tree_for(rsm_nmt_tree_root, const_cast<rsm_nmt_params*>(params), width, &t))
+        return fail(RSM_EUNSUPPORTED, "device NMT roots: width %u, namespace size %u not supported", width,
+                    params->namespace_size);
+    return device_tree_roots(ctx, t, static_cast<const uint8_t*>(d_eds), width, share_size,
+                             static_cast<uint8_t*>(d_roots), static_cast<uint32_t*>(d_status), pick(ctx, stream));
 }
 
 int rsm_roots_squares_dev(rsm_ctx* ctx, const void* d_eds, uint32_t width, uint32_t share_size, uint32_t count,

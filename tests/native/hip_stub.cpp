@@ -135,6 +135,14 @@ hipError_t launch_tree_roots(const uint32_t* d_leaf, uint32_t W, uint32_t first,
     (void)W;
     return hipSuccess;
 }
+bool nmt_dev_supported(uint32_t W, uint32_t ns) { return W >= 2 && W <= 1024 && ns >= 1 && ns <= 32; }
+hipError_t launch_nmt_roots(const uint8_t* d_eds, uint32_t W, uint32_t S, uint32_t ns, uint32_t, uint32_t,
+                            uint32_t* d_leaf, uint8_t* d_roots, uint32_t* d_status, hipStream_t) {
+    for (uint64_t c = 0; c < (uint64_t)W * W; ++c) d_leaf[c * 16] = d_eds[c * S];
+    memset(d_roots, 0, (size_t)2 * W * (2 * ns + 32));
+    if (d_status) memset(d_status, 0, (size_t)2 * W * 4);
+    return hipSuccess;
+}
 hipError_t launch_fill_random(void* p, uint64_t bytes, uint64_t seed, hipStream_t) {
     memset(p, (int)(seed & 0xFF), bytes);
     return hipSuccess;

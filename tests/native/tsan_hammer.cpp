@@ -78,6 +78,9 @@ int main() {
             uint32_t rl = 0;
             CHECK(rsm_eds_roots(e, RSM_AXIS_ROW, nullptr, nullptr, rr.data(), 32, &rl));
             CHECK(rsm_eds_roots(e, RSM_AXIS_COL, nullptr, nullptr, cr.data(), 32, &rl));
+            rsm_nmt_params np{29, 1, k};  // namespaced trees: device path for the complete square
+            std::vector<uint8_t> nr(W * 90);
+            CHECK(rsm_eds_roots(e, RSM_AXIS_ROW, rsm_nmt_tree_root, &np, nr.data(), 90, &rl));
             CHECK(rsm_eds_flattened(e, flat.data(), pres.data()));
             std::vector<const uint8_t*> fp(W * W);
             std::vector<uint32_t> fl(W * W, S);
