@@ -554,7 +554,7 @@ def main():
     row_bytes = 2 * ods_bytes * B  # row pass: Q0 in, Q1 out
     bitsliced = 64 < k <= 128
     kname = ("encode_gf8_bs128u_kernel" if bitsliced else "encode_gf8_kernel" if k <= 64
-             else "enc16_a/b/c (GF(2^16) passes)")
+             else "enc16_kernel (GF(2^16) single pass)")
     col_dom = t_col >= t_row
     dominant = ((kname + " column pass", col_bytes, t_col) if col_dom else (kname + " row pass", row_bytes, t_row))
     ach = dominant[1] / dominant[2] / 1e9

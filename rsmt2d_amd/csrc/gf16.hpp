@@ -15,9 +15,16 @@ struct alignas(16) PermTab16 {
     uint32_t w[24];
 };
 
+// Twiddle tables by skew index for the single-pass encoder: skewperm[i] =
+// perm[skew[i]], or all-zero where skew[i] is the modulus (the butterfly's
+// multiply is skipped), so a butterfly's table is ONE uniform load with no
+// dependent skew lookup and no branch.  Indices < kSkewPermN cover m <= 1024.
+constexpr uint32_t kSkewPermN = 2048;
+
 struct Gf16Host {
     std::vector<uint16_t> exp, log, skew, logwalsh;
-    std::vector<PermTab16> perm;  // 65536 entries
+    std::vector<PermTab16> perm;      // 65536 entries
+    std::vector<PermTab16> skewperm;  // kSkewPermN entries
 };
 const Gf16Host& gf16_host();
 
@@ -26,6 +33,8 @@ struct Gf16Dev {
     const PermTab16* perm = nullptr;  // [65536]
     const uint16_t* skew = nullptr;   // [65535]
     const uint16_t* logwalsh = nullptr;
+    const PermTab16* skewperm = nullptr;  // [kSkewPermN]
+    uint32_t cus = 256;                   // persistent-grid size (the context's CUs)
     uint8_t* scratch = nullptr;       // work arrays
     uint64_t scratch_bytes = 0;
     uint16_t* errs = nullptr;         // decoder error locators [count][n]

@@ -97,6 +97,11 @@ const Gf16Host& gf16_host() {
                 p.w[4 * c + 3] = h1;  // output-hi table, entries 4..7
             }
         }
+        // twiddle tables by skew index (encoder): zero table where the skew is the
+        // modulus (that butterfly adds nothing)
+        t.skewperm.assign(kSkewPermN, PermTab16{});
+        for (unsigned i = 0; i < kSkewPermN; ++i)
+            if (t.skew[i] != kOrder - 1) t.skewperm[i] = t.perm[t.skew[i]];
     });
     return t;
 }

@@ -6,13 +6,16 @@
 // bytes, 4 hi bytes), so a wavefront spans 8 blocks = 512 bytes of share width
 // and every multiply-by-constant is 12 v_perm_b32 lookups (PermTab16).
 //
-// The m-point transforms (m = ceilPow2(k) in {256, 512}) do not fit in one
-// lane's registers, so they run as radix-16 passes through a global scratch
-// work array ([codeword][element][S], L2/MALL-resident for the batch sizes the
-// launcher picks):
-//   encode: A group layout  (16 consecutive elements): IFFT layers 1..8
-//           B residue layout (elements r, r+16, ...):  IFFT layers 16..m/2, FFT m/2..16
-//           C group layout:                            FFT layers 8..1, parity out
+// Encode (m = ceilPow2(k) in {256, 512}) is ONE pass per codeword: a workgroup of
+// m/32 waves owns a (codeword, 512-byte chunk) and keeps its m-point IFFT + FFT on
+// chip -- each wave holds E = 32 elements in registers, and one LDS exchange
+// buffer ([element][lane] dwords, one plane at a time) switches between
+//   group layout   (wave w: elements 32 w .. 32 w + 31):  layers d < 32
+//   residue layout (wave w: residues r = (32/R) w + s, elements r + 32 j, j < R =
+//                   m/32):                                 layers d = 32 .. m/2
+// so the data shares are read once and the parity shares written once.
+// The decoder's n = 2m transforms still run as radix-16 passes through a global
+// work array ([codeword][element][S]):
 //   decode (n = 2m): 1 group: scale by the error locator + IFFT low
 //                    2 residue: IFFT high; also H(in) = high-bit half of the formal derivative
 //                    3 group: out = in + L(in) + H(in)  (the derivative's closed form)
@@ -211,91 +214,300 @@ __device__ __forceinline__ TaskIdx task_of(uint32_t count, uint32_t chunks, uint
 }
 
 // ---------------------------------------------------------------------------
-// Encoder passes (codewords q0 .. q0 + count of the CodewordSet; scratch row
-// (q - q0) holds that codeword's m-element work array)
+// Single-pass encoder
 // ---------------------------------------------------------------------------
 struct Enc16 {
     CodewordSet cs;
-    Res r;
-    uint8_t* scratch;
-    uint32_t q0, count, chunks;
+    const PermTab16* tw;  // skewperm: twiddle table by skew index (zero where skipped)
+    uint32_t chunks;
 };
 
-template <int M>
-__global__ __launch_bounds__(256) void enc16_a(Enc16 p) {
-    const TaskIdx t = task_of(p.count, p.chunks, M / 16);
-    if (!t.valid) return;
-    const Lane ln = lane_of(t.chunk, p.cs.S);
-    const auto in = rsrc(p.cs.base + cw_rel(p.cs, p.q0 + t.q));
-    const auto wk = rsrc(p.scratch + (uint64_t)t.q * M * p.cs.S);
-    const uint32_t es = (uint32_t)p.cs.elem_stride, k = p.cs.k, S = p.cs.S;
-    uint32_t l[16], h[16];
-    sfor<16>([&](auto E) {
-        constexpr int i = decltype(E)::value;
-        const uint32_t e = 16 * t.g + i;
-        const uint32_t so = e < k ? e * es : kOob16;
-        l[i] = ld(in, ln.lo, so);
-        h[i] = ld(in, ln.lo + 32, so);
+constexpr int ilog2c(int x) { return x <= 1 ? 0 : 1 + ilog2c(x / 2); }
+
+// The 20 PermTab16 words muladd16 reads, in this order (w[9], w[11], w[21] and
+// w[23] are unused): a compact twiddle table of 80 bytes.
+constexpr int kTabW = 20;
+__device__ __forceinline__ int tab_word(int j) { return j < 9 ? j : (j == 9 ? 10 : (j < 18 ? j + 2 : (j == 18 ? 20 : 22))); }
+
+// (xl, xh) ^= (yl, yh) * exp(L) with the compact table c in VGPRs (both v_perm
+// sources are VGPRs: no copies through the one-SGPR-per-instruction bus).
+__device__ __forceinline__ void muladd16v(uint32_t& xl, uint32_t& xh, uint32_t yl, uint32_t yh, const uint32_t (&c)[kTabW]) {
+    const uint32_t sa = yl & 0x07070707u, sb = (yl >> 3) & 0x07070707u, sc = (yl >> 6) & 0x03030303u;
+    const uint32_t sd = yh & 0x07070707u, se = (yh >> 3) & 0x07070707u, sf = (yh >> 6) & 0x03030303u;
+    // c: 0..7 = w0..w7, 8 = w8, 9 = w10, 10..17 = w12..w19, 18 = w20, 19 = w22
+    xl = x3(x3(xl, pm(c[1], c[0], sa), pm(c[5], c[4], sb)),
+            x3(pm(c[8], c[8], sc), pm(c[11], c[10], sd), pm(c[15], c[14], se)), pm(c[18], c[18], sf));
+    xh = x3(x3(xh, pm(c[3], c[2], sa), pm(c[7], c[6], sb)),
+            x3(pm(c[9], c[9], sc), pm(c[13], c[12], sd), pm(c[17], c[16], se)), pm(c[19], c[19], sf));
+}
+typedef uint32_t v4u16 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void tab_load(const uint32_t* lds, uint32_t (&c)[kTabW]) {
+    sfor<kTabW / 4>([&](auto Q) {
+        constexpr int q = decltype(Q)::value;
+        const v4u16 v = *reinterpret_cast<const v4u16*>(lds + 4 * q);
+        c[4 * q] = v.x; c[4 * q + 1] = v.y; c[4 * q + 2] = v.z; c[4 * q + 3] = v.w;
     });
-    group_ifft(l, h, t.g, M - 1, p.r);
-    sfor<16>([&](auto E) {
-        constexpr int i = decltype(E)::value;
-        const uint32_t so = (16 * t.g + i) * S;
-        st(wk, l[i], ln.lo, so);
-        st(wk, h[i], ln.lo + 32, so);
+}
+// Butterflies with the twiddle table given directly (zero table = no multiply).
+__device__ __forceinline__ void ifft2t(uint32_t& xl, uint32_t& xh, uint32_t& yl, uint32_t& yh, const PermTab16& t) {
+    yl ^= xl;
+    yh ^= xh;
+    muladd16(xl, xh, yl, yh, t);
+}
+__device__ __forceinline__ void fft2t(uint32_t& xl, uint32_t& xh, uint32_t& yl, uint32_t& yh, const PermTab16& t) {
+    muladd16(xl, xh, yl, yh, t);
+    yl ^= xl;
+    yh ^= xh;
+}
+__device__ __forceinline__ void ifft2v(uint32_t& xl, uint32_t& xh, uint32_t& yl, uint32_t& yh, const uint32_t (&c)[kTabW]) {
+    yl ^= xl;
+    yh ^= xh;
+    muladd16v(xl, xh, yl, yh, c);
+}
+__device__ __forceinline__ void fft2v(uint32_t& xl, uint32_t& xh, uint32_t& yl, uint32_t& yh, const uint32_t (&c)[kTabW]) {
+    muladd16v(xl, xh, yl, yh, c);
+    yl ^= xl;
+    yh ^= xh;
+}
+
+// Twiddle tables of a transform stage over n-point runs, one per (layer, block):
+// layer d = 2^L has n/(2d) blocks at slots (n - (n >> L)) + block, n - 1 slots.
+__device__ __forceinline__ int slot_layer(int slot, int n) {
+    int L = 0;
+#pragma unroll
+    for (int t = 1; t < 12; ++t) L += (n >> t) > 0 && slot >= n - (n >> t) ? 1 : 0;
+    return L;
+}
+
+// Stage into LDS `tab` the group-layout tables of every wave (wave w: E - 1
+// slots, elements E w ..): IFFT SKEW[off + b + d] or FFT SKEW[b + d - 1].  Fixed
+// trip count, loads first: every thread's table words are in flight at once.
+template <int WAVES, int E, bool FFT>
+__device__ __forceinline__ void stage_grp(uint32_t* tab, const PermTab16* tw, int off) {
+    constexpr int NT = WAVES * (E - 1), THREADS = WAVES * 64, PER = (NT * kTabW + THREADS - 1) / THREADS;
+    uint32_t v[PER];
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+        const int n = (int)threadIdx.x + r * THREADS;
+        const int T = n / kTabW, j = n - T * kTabW;
+        const int w = T / (E - 1), slot = T - w * (E - 1);
+        const int L = slot_layer(slot, E);
+        const int d = 1 << L, bl = (slot - (E - (E >> L))) * 2 * d;
+        const int idx = FFT ? E * w + bl + d - 1 : off + E * w + bl + d;
+        v[r] = n < NT * kTabW ? tw[idx].w[tab_word(j)] : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+        const int n = (int)threadIdx.x + r * THREADS;
+        if (n < NT * kTabW) tab[n] = v[r];
+    }
+}
+// Residue-layout tables (shared by all waves): slots 0..R-2 IFFT, R-1..2R-3 FFT.
+template <int R, int E, int THREADS>
+__device__ __forceinline__ void stage_res(uint32_t* tab, const PermTab16* tw, int off) {
+    constexpr int NW = 2 * (R - 1) * kTabW, PER = (NW + THREADS - 1) / THREADS;
+    uint32_t v[PER];
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+        const int n = (int)threadIdx.x + r * THREADS;
+        const int T = n / kTabW, j = n - T * kTabW;
+        const bool fft = T >= R - 1;
+        const int slot = fft ? T - (R - 1) : T;
+        const int L = slot_layer(slot, R);
+        const int dj = 1 << L, bl = (slot - (R - (R >> L))) * 2 * dj;
+        const int idx = fft ? E * bl + E * dj - 1 : off + E * bl + E * dj;
+        v[r] = n < NW ? tw[idx].w[tab_word(j)] : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+        const int n = (int)threadIdx.x + r * THREADS;
+        if (n < NW) tab[n] = v[r];
+    }
+}
+
+// Group layout (E elements per wave): IFFT layers d = 1..E/2 ascending / FFT
+// d = E/2..1 descending; the table of (layer, block) from this wave's E-1 slots.
+template <int E, bool FFT>
+__device__ __forceinline__ void grp_xform(uint32_t (&l)[E], uint32_t (&h)[E], const uint32_t* wtab) {
+    constexpr int LN = ilog2c(E);
+    sfor<LN>([&](auto LGi) {
+        constexpr int L = FFT ? LN - 1 - decltype(LGi)::value : decltype(LGi)::value;
+        constexpr int d = 1 << L;
+        sfor<E / 2 / d>([&](auto Bk) {
+            constexpr int block = decltype(Bk)::value;
+            uint32_t c[kTabW];
+            tab_load(wtab + (E - (E >> L) + block) * kTabW, c);
+            sfor<d>([&](auto Q) {
+                constexpr int i = block * 2 * d + decltype(Q)::value;
+                if constexpr (FFT) fft2v(l[i], h[i], l[i + d], h[i + d], c);
+                else ifft2v(l[i], h[i], l[i + d], h[i + d], c);
+            });
+        });
+    });
+}
+// The same with each table read straight from global memory (wave-uniform:
+// scalar loads), for the 16-wave m = 512 form whose registers leave no room for
+// LDS-staged tables: IFFT SKEW[off + base + b + d], FFT SKEW[base + b + d - 1].
+template <int E, bool FFT>
+__device__ __forceinline__ void grp_xform_g(uint32_t (&l)[E], uint32_t (&h)[E], const PermTab16* tw, int base, int off) {
+    constexpr int LN = ilog2c(E);
+    sfor<LN>([&](auto LGi) {
+        constexpr int L = FFT ? LN - 1 - decltype(LGi)::value : decltype(LGi)::value;
+        constexpr int d = 1 << L;
+        sfor<E / 2 / d>([&](auto Bk) {
+            constexpr int bl = decltype(Bk)::value * 2 * d;
+            const PermTab16& t = tw[FFT ? base + bl + d - 1 : off + base + bl + d];
+            sfor<d>([&](auto Q) {
+                constexpr int i = bl + decltype(Q)::value;
+                if constexpr (FFT) fft2t(l[i], h[i], l[i + d], h[i + d], t);
+                else ifft2t(l[i], h[i], l[i + d], h[i + d], t);
+            });
+        });
+    });
+}
+template <int E, int R, bool FFT>
+__device__ __forceinline__ void res_xform_g(uint32_t (&l)[E], uint32_t (&h)[E], const PermTab16* tw, int off) {
+    constexpr int LN = ilog2c(R);
+    sfor<LN>([&](auto LGi) {
+        constexpr int L = FFT ? LN - 1 - decltype(LGi)::value : decltype(LGi)::value;
+        constexpr int dj = 1 << L;
+        sfor<R / 2 / dj>([&](auto Bk) {
+            constexpr int bl = decltype(Bk)::value * 2 * dj;
+            const PermTab16& t = tw[FFT ? E * bl + E * dj - 1 : off + E * bl + E * dj];
+            sfor<dj>([&](auto Q) {
+                constexpr int j = bl + decltype(Q)::value;
+                sfor<E / R>([&](auto Sx) {
+                    constexpr int i = R * decltype(Sx)::value + j;
+                    if constexpr (FFT) fft2t(l[i], h[i], l[i + dj], h[i + dj], t);
+                    else ifft2t(l[i], h[i], l[i + dj], h[i + dj], t);
+                });
+            });
+        });
+    });
+}
+// Residue layout: register s*R + j holds element r_s + E j; a layer over j at
+// distance dj joins elements E dj apart (block start E bl): one table per
+// (layer, block) for every residue of every wave.
+template <int E, int R, bool FFT>
+__device__ __forceinline__ void res_xform(uint32_t (&l)[E], uint32_t (&h)[E], const uint32_t* rtab) {
+    constexpr int LN = ilog2c(R);
+    sfor<LN>([&](auto LGi) {
+        constexpr int L = FFT ? LN - 1 - decltype(LGi)::value : decltype(LGi)::value;
+        constexpr int dj = 1 << L;
+        sfor<R / 2 / dj>([&](auto Bk) {
+            constexpr int block = decltype(Bk)::value;
+            uint32_t c[kTabW];
+            tab_load(rtab + ((FFT ? R - 1 : 0) + (R - (R >> L)) + block) * kTabW, c);
+            sfor<dj>([&](auto Q) {
+                constexpr int j = block * 2 * dj + decltype(Q)::value;
+                sfor<E / R>([&](auto Sx) {
+                    constexpr int i = R * decltype(Sx)::value + j;
+                    if constexpr (FFT) fft2v(l[i], h[i], l[i + dj], h[i + dj], c);
+                    else ifft2v(l[i], h[i], l[i + dj], h[i + dj], c);
+                });
+            });
+        });
     });
 }
 
-template <int M>
-__global__ __launch_bounds__(256) void enc16_b(Enc16 p) {
-    constexpr int R = M / 16;
-    const TaskIdx t = task_of(p.count, p.chunks, 16);
-    if (!t.valid) return;
-    const Lane ln = lane_of(t.chunk, p.cs.S);
-    const auto wk = rsrc(p.scratch + (uint64_t)t.q * M * p.cs.S);
-    const uint32_t S = p.cs.S;
-    uint32_t l[R], h[R];
-    sfor<R>([&](auto J) {
-        constexpr int j = decltype(J)::value;
-        const uint32_t so = (t.g + 16 * j) * S;
-        l[j] = ld(wk, ln.lo, so);
-        h[j] = ld(wk, ln.lo + 32, so);
+// One plane of the layout switch through LDS xch[element][lane].  Residue
+// register s*R + j holds element (E/R) w + s + E j.
+template <int E, int R, bool TO_RESIDUE>
+__device__ __forceinline__ void xch_plane(uint32_t (&v)[E], uint32_t (*xch)[64], uint32_t w, uint32_t lane) {
+    constexpr int RPW = E / R;  // residues per wave
+    sfor<E>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        const uint32_t e = TO_RESIDUE ? E * w + i : (RPW * w + i / R) + E * (i % R);
+        xch[e][lane] = v[i];
     });
-    residue_ifft<R>(l, h, M - 1, p.r);
-    residue_fft<R>(l, h, p.r);
-    sfor<R>([&](auto J) {
-        constexpr int j = decltype(J)::value;
-        const uint32_t so = (t.g + 16 * j) * S;
-        st(wk, l[j], ln.lo, so);
-        st(wk, h[j], ln.lo + 32, so);
+    __syncthreads();
+    sfor<E>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        const uint32_t e = TO_RESIDUE ? (RPW * w + i / R) + E * (i % R) : E * w + i;
+        v[i] = xch[e][lane];
     });
+    __syncthreads();
 }
 
+// Encoder: parity of codeword q, chunk c (512 bytes) = FFT(IFFT(data)).  The
+// encoder's IFFT uses SKEW[m - 1 + b + d] (data occupy the upper half of the
+// 2m-point domain), its FFT SKEW[b + d - 1]; every index is < 2m <= kSkewPermN.
+// Twiddle tables: staged in LDS per workgroup (the group stages' 31 per wave in
+// the exchange buffer, which is idle then; the residue stages' in rtab), read by
+// uniform ds_read_b128 -- a table load from L2 per butterfly would leave the waves
+// waiting on scalar loads (the tables of one transform exceed the scalar cache).
+// m/32 waves of E = 32 elements; residues of R = m/32 elements.
+//   m = 256: 8 waves (2 per SIMD, up to 256 registers), persistent (one workgroup
+//            per CU), twiddle tables staged once into LDS and read by uniform
+//            ds_read_b128 -- one scalar table load from L2 per butterfly left the
+//            waves waiting (the tables of a transform exceed the scalar cache);
+//   m = 512: 16 waves (128 registers each, no room for LDS-read tables), one
+//            workgroup per task, tables by scalar loads (A/B: faster here).
 template <int M>
-__global__ __launch_bounds__(256) void enc16_c(Enc16 p) {
-    const TaskIdx t = task_of(p.count, p.chunks, M / 16);
-    if (!t.valid) return;
-    const Lane ln = lane_of(t.chunk, p.cs.S);
-    const uint64_t rel = cw_rel(p.cs, p.q0 + t.q);
-    const auto out = rsrc(p.cs.out_base + rel);
-    const auto wk = rsrc(p.scratch + (uint64_t)t.q * M * p.cs.S);
-    const uint32_t es = (uint32_t)p.cs.elem_stride, k = p.cs.k, S = p.cs.S;
+__global__ __launch_bounds__(M * 2, M == 256 ? 2 : 4) void enc16_kernel(Enc16 p) {
+    constexpr int WAVES = M / 32, E = 32, R = M / E;
+    constexpr bool LDS_TAB = M == 256;
+    constexpr int GT = WAVES * (E - 1) * kTabW;
+    __shared__ uint32_t xch[M][64];
+    __shared__ uint32_t tabs[LDS_TAB ? 2 * GT + 2 * (R - 1) * kTabW : 1];
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    uint32_t* gI = tabs;
+    uint32_t* gF = tabs + GT;
+    uint32_t* rtab = tabs + 2 * GT;
+    if constexpr (LDS_TAB) {
+        stage_grp<WAVES, E, false>(gI, p.tw, M - 1);
+        stage_grp<WAVES, E, true>(gF, p.tw, 0);
+        stage_res<R, E, WAVES * 64>(rtab, p.tw, M - 1);
+    }
+    const uint32_t es = (uint32_t)p.cs.elem_stride, k = p.cs.k;
     const uint32_t oo = (uint32_t)p.cs.out_offset;
-    uint32_t l[16], h[16];
-    sfor<16>([&](auto E) {
-        constexpr int i = decltype(E)::value;
-        const uint32_t so = (16 * t.g + i) * S;
-        l[i] = ld(wk, ln.lo, so);
-        h[i] = ld(wk, ln.lo + 32, so);
-    });
-    group_fft(l, h, t.g, p.r);
-    sfor<16>([&](auto E) {
-        constexpr int i = decltype(E)::value;
-        const uint32_t e = 16 * t.g + i;
-        const uint32_t so = e < k ? oo + e * es : kOob16;
-        st(out, l[i], ln.lo, so);
-        st(out, h[i], ln.lo + 32, so);
-    });
+    const uint32_t tasks = p.cs.count * p.chunks;
+    auto run = [&](uint32_t task) {
+        const uint32_t q = task / p.chunks, chunk = task - q * p.chunks;
+        const Lane ln = lane_of(chunk, p.cs.S);
+        const uint64_t rel = cw_rel(p.cs, q);
+        const auto in = rsrc(p.cs.base + rel);
+        uint32_t l[E], h[E];
+        sfor<E>([&](auto I) {
+            constexpr int i = decltype(I)::value;
+            const uint32_t e = E * w + i;
+            const uint32_t so = e < k ? e * es : kOob16;
+            l[i] = ld(in, ln.lo, so);
+            h[i] = ld(in, ln.lo + 32, so);
+        });
+        if constexpr (LDS_TAB) {
+            __syncthreads();  // tables staged (first task)
+            grp_xform<E, false>(l, h, gI + w * (E - 1) * kTabW);
+        } else {
+            grp_xform_g<E, false>(l, h, p.tw, (int)(E * w), M - 1);
+        }
+        xch_plane<E, R, true>(l, xch, w, lane);
+        xch_plane<E, R, true>(h, xch, w, lane);
+        if constexpr (LDS_TAB) {
+            res_xform<E, R, false>(l, h, rtab);
+            res_xform<E, R, true>(l, h, rtab);
+        } else {
+            res_xform_g<E, R, false>(l, h, p.tw, M - 1);
+            res_xform_g<E, R, true>(l, h, p.tw, 0);
+        }
+        xch_plane<E, R, false>(l, xch, w, lane);
+        xch_plane<E, R, false>(h, xch, w, lane);
+        if constexpr (LDS_TAB) grp_xform<E, true>(l, h, gF + w * (E - 1) * kTabW);
+        else grp_xform_g<E, true>(l, h, p.tw, (int)(E * w), 0);
+        const auto out = rsrc(p.cs.out_base + rel);
+        sfor<E>([&](auto I) {
+            constexpr int i = decltype(I)::value;
+            const uint32_t e = E * w + i;
+            const uint32_t so = e < k ? oo + e * es : kOob16;
+            st(out, l[i], ln.lo, so);
+            st(out, h[i], ln.lo + 32, so);
+        });
+    };
+    if constexpr (LDS_TAB) {
+        for (uint32_t task = blockIdx.x; task < tasks; task += gridDim.x) run(task);
+    } else {
+        run(blockIdx.x);  // grid = tasks
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -532,41 +744,19 @@ __global__ __launch_bounds__(256) void dec16_p5(Dec16 p) {  // group: FFT low + 
 
 inline uint32_t blocks_for(uint64_t tasks) { return (uint32_t)((tasks + 3) / 4); }
 
-// Work-array bytes per encode launch triple (A, B, C).  Measured on config 4 (k=256,
-// S=2048) and 5 (k=512, S=512): capping a batch at 64 MiB so that its work arrays
-// stay in the Infinity Cache between the passes is SLOWER (175 vs 196 GiB/s, 0.90
-// vs 0.77 ms) than one launch triple over up to 1 GiB of work arrays -- the extra
-// launches cost more than the HBM round trips they save.  RSM_GF16_BATCH_MB
-// overrides it in the diagnostic build only (A/B measurements).
-static uint64_t gf16_batch_bytes() {
-#ifdef RSM_DIAG
-    static const uint64_t b = [] {
-        const char* v = getenv("RSM_GF16_BATCH_MB");
-        const uint64_t mb = v ? strtoull(v, nullptr, 10) : 0;
-        return (mb ? mb : 1024ull) << 20;
-    }();
-    return b;
-#else
-    return 1024ull << 20;
-#endif
-}
-
 template <int M>
 hipError_t run_encode(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st) {
     const uint32_t chunks = (cs.S + 511) / 512;
-    const uint64_t per_cw = (uint64_t)M * cs.S;
-    uint32_t batch = (uint32_t)((g.scratch_bytes < gf16_batch_bytes() ? g.scratch_bytes : gf16_batch_bytes()) / per_cw);
-    if (batch == 0) batch = (uint32_t)(g.scratch_bytes / per_cw);
-    if (batch == 0) return hipErrorOutOfMemory;
-    for (uint32_t q0 = 0; q0 < cs.count; q0 += batch) {
-        Enc16 p{cs, Res{g.perm, g.skew}, g.scratch, q0, cs.count - q0 < batch ? cs.count - q0 : batch, chunks};
-        hipLaunchKernelGGL(enc16_a<M>, dim3(blocks_for((uint64_t)p.count * chunks * (M / 16))), dim3(256), 0, st, p);
-        hipLaunchKernelGGL(enc16_b<M>, dim3(blocks_for((uint64_t)p.count * chunks * 16)), dim3(256), 0, st, p);
-        hipLaunchKernelGGL(enc16_c<M>, dim3(blocks_for((uint64_t)p.count * chunks * (M / 16))), dim3(256), 0, st, p);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-    }
-    return hipSuccess;
+    const uint64_t tasks = (uint64_t)cs.count * chunks;
+    if (tasks == 0) return hipSuccess;
+    if (tasks >= (1ull << 31)) return hipErrorInvalidValue;
+    Enc16 p{cs, g.skewperm, chunks};
+    // m = 256: persistent, one workgroup per CU (its twiddle tables stay in LDS);
+    // m = 512: one workgroup per task (measured faster: the 16-wave form leaves no
+    // registers for a persistent loop's state)
+    const uint32_t grid = M == 256 && tasks > g.cus ? g.cus : (uint32_t)tasks;
+    hipLaunchKernelGGL(enc16_kernel<M>, dim3(grid), dim3(M * 2), 0, st, p);
+    return hipGetLastError();
 }
 
 template <int M>

@@ -100,7 +100,7 @@ struct rsm_ctx {
     // GF(2^16) tables, uploaded once
     std::mutex gf16_mu;
     bool gf16_ready = false;
-    rsm::DevBuf gf16_perm, gf16_skew, gf16_logwalsh;
+    rsm::DevBuf gf16_perm, gf16_skew, gf16_logwalsh, gf16_skewperm;
     rsm::Gf16Dev gf16{};  // table pointers only (scratch comes per stream)
 
     rsm::DevBuf zero_index;  // one device u32 = 0 (index list of a single-codeword decode)

@@ -137,14 +137,17 @@ int ensure_gf16_tables(rsm_ctx* ctx) {
     if (ctx->gf16_ready) return RSM_OK;
     const Gf16Host& t = gf16_host();
     const size_t pb = t.perm.size() * sizeof(PermTab16), sb = t.skew.size() * 2, lb = t.logwalsh.size() * 2;
+    const size_t kb = t.skewperm.size() * sizeof(PermTab16);
     hipError_t e;
     if ((e = ctx->gf16_perm.ensure(pb)) != hipSuccess || (e = ctx->gf16_skew.ensure(sb)) != hipSuccess ||
-        (e = ctx->gf16_logwalsh.ensure(lb)) != hipSuccess)
+        (e = ctx->gf16_logwalsh.ensure(lb)) != hipSuccess || (e = ctx->gf16_skewperm.ensure(kb)) != hipSuccess)
         return hip_fail(e, "hipMalloc (GF16 tables)");
     if ((e = hipMemcpy(ctx->gf16_perm.ptr, t.perm.data(), pb, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipMemcpy(ctx->gf16_skew.ptr, t.skew.data(), sb, hipMemcpyHostToDevice)) != hipSuccess ||
-        (e = hipMemcpy(ctx->gf16_logwalsh.ptr, t.logwalsh.data(), lb, hipMemcpyHostToDevice)) != hipSuccess)
+        (e = hipMemcpy(ctx->gf16_logwalsh.ptr, t.logwalsh.data(), lb, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(ctx->gf16_skewperm.ptr, t.skewperm.data(), kb, hipMemcpyHostToDevice)) != hipSuccess)
         return hip_fail(e, "upload GF16 tables");
+    ctx->gf16.skewperm = static_cast<const PermTab16*>(ctx->gf16_skewperm.ptr);
     ctx->gf16.perm = static_cast<const PermTab16*>(ctx->gf16_perm.ptr);
     ctx->gf16.skew = static_cast<const uint16_t*>(ctx->gf16_skew.ptr);
     ctx->gf16.logwalsh = static_cast<const uint16_t*>(ctx->gf16_logwalsh.ptr);
@@ -191,11 +194,10 @@ int launch_encode(rsm_ctx* ctx, const CodewordSet& cs0, hipStream_t st) {
         e = launch_encode_gf8(cs, st);
     } else {
         if (!gf16_supported(cs.k)) return fail(RSM_EUNSUPPORTED, "encode: k=%u (m > 512) not supported in this build", cs.k);
-        const uint64_t per_cw = (uint64_t)ceil_pow2(cs.k) * cs.S;
-        StreamScratch& ss = stream_scratch(ctx, st);
-        std::lock_guard<std::mutex> lk(ss.mu);
-        Gf16Dev g;
-        if (int rc = gf16_for_stream(ctx, ss, st, gf16_budget(per_cw, cs.count), 0, &g)) return rc;
+        // single pass per codeword: the tables only, no work arrays
+        if (int rc = ensure_gf16_tables(ctx)) return rc;
+        Gf16Dev g = ctx->gf16;
+        g.cus = ctx->cus;
         e = launch_encode_gf16(cs, g, st);
     }
     if (e != hipSuccess) return hip_fail(e, "encode kernel launch");
