@@ -565,7 +565,7 @@ def main():
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_latest.json")
     if bitsliced and os.path.exists(pmc_path):
-        want = "encode_gf8_bs128u_kernel<40, %d>" % (1 if col_dom else 0)
+        want = "encode_gf8_bs128u_kernel<%d, %d>" % ((56, 1) if col_dom else (40, 0))
         sets = (W if col_dom else k) * B * S // 2048
         grid_threads = min(sets, 256) * 512  # persistent grid: one 512-thread workgroup per CU
         for row in json.load(open(pmc_path)).get("launches", []):

@@ -20,6 +20,9 @@ extern "C" {
  * rev_col: column pass in reverse set order; xcd: bit 0 rows / bit 1 columns in
  * XCD-grouped set order. */
 int rsm_diag_set_bs_mode(int mode, int rev_col, int xcd);
+/* Kernel variant of the row pass alone (same codes; the setting above then applies
+ * to every other launch). */
+int rsm_diag_set_bs_row_mode(int mode);
 /* Both passes of `count` in-place k = 128 squares in ONE persistent launch
  * (encode_gf8_bs128f_kernel).  Synchronous; fails if the kernel's bounded wait
  * timed out (its output is then invalid). */

@@ -702,19 +702,23 @@ bool bs128_applicable(const CodewordSet& cs) {
     return span + sym < kOobBs;
 }
 
-// Production launch: MODE 40 (ds_write_addtid_b32 exchange + non-temporal loads,
-// measured best: profiles/r01e_bench_ab.txt); the column pass walks its sets in
-// reverse order (its first reads are the squares the row pass wrote last).  The
-// persistent grid is the caller's (the context's CU count or per-pass cap).
+// Production launch: row pass MODE 40 (ds_write_addtid_b32 exchange + non-temporal
+// loads: its Q1 stores keep the default policy), column pass MODE 56 (+ non-temporal
+// stores: Q2/Q3 are final output, never re-read; 3-4 % faster per step than MODE 40 in
+// the two-stream schedule, profiles/r02d_sched_ab.jsonl).  The column pass walks its
+// sets in reverse order (its first reads are the squares the row pass wrote last).
+// The persistent grid is the caller's (the context's CU count or per-pass cap).
 #ifdef RSM_DIAG
 static std::atomic<int> g_diag_mode{40};
 static std::atomic<int> g_diag_rev{1};
 static std::atomic<int> g_diag_xcd{0};
+static std::atomic<int> g_diag_row_mode{40};
 void set_bs128_diag_mode(int mode, int rev_col, int xcd) {
     g_diag_mode.store(mode);
     g_diag_rev.store(rev_col);
     g_diag_xcd.store(xcd);
 }
+void set_bs128_diag_row_mode(int mode) { g_diag_row_mode.store(mode); }
 #endif
 
 hipError_t launch_encode_gf8_bs128(const CodewordSet& cs, hipStream_t st) {
@@ -727,7 +731,7 @@ hipError_t launch_encode_gf8_bs128(const CodewordSet& cs, hipStream_t st) {
     hipLaunchKernelGGL((encode_gf8_bs128u_kernel<m, p>), dim3(grid), dim3(512), 0, st, cs, (uint32_t)sets, rev)
 #ifdef RSM_DIAG
     {
-        const int mode = g_diag_mode.load();
+        const int mode = row ? g_diag_row_mode.load() : g_diag_mode.load();
         const uint32_t xcd = (uint32_t)g_diag_xcd.load();
         const uint32_t rev = (row ? 0u : (uint32_t)g_diag_rev.load()) | (((xcd >> (row ? 0 : 1)) & 1u) << 1);
         switch (mode) {
@@ -737,16 +741,21 @@ hipError_t launch_encode_gf8_bs128(const CodewordSet& cs, hipStream_t st) {
             case 8: RSM_BS_LAUNCH(8, 1); return hipGetLastError();
             case 24: RSM_BS_LAUNCH(24, 1); return hipGetLastError();
             case 56: RSM_BS_LAUNCH(56, 1); return hipGetLastError();
+            case 32: RSM_BS_LAUNCH(32, 1); return hipGetLastError();   // NT loads, dword exchange writes
+            case 16: RSM_BS_LAUNCH(16, 1); return hipGetLastError();
+            case 42: RSM_BS_LAUNCH(42, 1); return hipGetLastError();  // no arithmetic (wrong output)
+            case 58: RSM_BS_LAUNCH(58, 1); return hipGetLastError();  // no arithmetic (wrong output)
+            case 44: RSM_BS_LAUNCH(44, 1); return hipGetLastError();  // no global memory (wrong output)
             default: break;
         }
         if (row) RSM_BS_LAUNCH(40, 0);
-        else RSM_BS_LAUNCH(40, 1);
+        else RSM_BS_LAUNCH(56, 1);
         return hipGetLastError();
     }
 #else
     const uint32_t rev = row ? 0u : 1u;
     if (row) RSM_BS_LAUNCH(40, 0);
-    else RSM_BS_LAUNCH(40, 1);
+    else RSM_BS_LAUNCH(56, 1);
 #endif
 #undef RSM_BS_LAUNCH
     return hipGetLastError();

@@ -52,6 +52,11 @@ int rsm_diag_set_bs_mode(int mode, int rev_col, int xcd) {
     return RSM_OK;
 }
 
+int rsm_diag_set_bs_row_mode(int mode) {
+    set_bs128_diag_row_mode(mode);
+    return RSM_OK;
+}
+
 // Both passes of `count` in-place k = 128 squares as ONE persistent launch (the
 // row sets of square s + lag interleaved with the column sets of square s).
 // Synchronous: reads back the kernel's stuck-wait flag and fails if it is set.

@@ -123,6 +123,7 @@ hipError_t launch_encode_gf8_bs128_dual(const DualPlan& p, hipStream_t st);
 // A-B kernel variant of the bit-sliced encode: 40 production, 0/8/24/56 A-B
 // variants, 2 = no arithmetic, 4 = no global memory (wrong output by design)
 void set_bs128_diag_mode(int mode, int rev_col, int xcd);
+void set_bs128_diag_row_mode(int mode);
 #endif
 
 }  // namespace rsm
