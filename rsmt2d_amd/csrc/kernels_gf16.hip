@@ -742,6 +742,230 @@ __global__ __launch_bounds__(256) void dec16_p5(Dec16 p) {  // group: FFT low + 
     });
 }
 
+
+// ---------------------------------------------------------------------------
+// Generic multi-pass transforms for m = ceilPow2(k) >= 1024 (k up to 32768, the
+// reference's MaxChunks: leopard.go:76-84).  The m- (encode) or n = 2m- (decode)
+// point transforms no longer fit one workgroup, so they run as radix-2^b passes
+// through a global work array [codeword][point][S]: a wave owns one group of
+// G = 2^b points e = base + j D (j < G) of one 512-byte chunk and applies the
+// layers d = D, 2D, .., D G / 2 (IFFT ascending, then -- in the top pass -- FFT
+// descending), with the twiddle of (layer, block) read per butterfly (wave-uniform
+// scalar loads, as the decoder's passes above).  Bit groups: 4 bits per pass from
+// the bottom, the top group takes the remainder.
+//   encode: pass(group 0, IFFT) reads the data shares (zero past k), ...,
+//           pass(top, IFFT + FFT), ..., pass(group 0, FFT) writes parity e < k.
+//   decode: errloc16g_kernel; pass(group 0, IFFT) reads the present shares scaled
+//           by the error locator; IFFT passes up to the top -> work A; the formal
+//           derivative as one pass per bit group (B = A + sum_g T_g(A), every
+//           term from the pre-derivative A: the closed form of the reference's
+//           sequential loop); FFT passes on B down to group 0, which reveals the
+//           missing shares (times exp(-err)).
+// ---------------------------------------------------------------------------
+struct G16Pass {
+    CodewordSet cs;        // encode: shares (first pass reads data, last writes parity)
+    DecodeSet ds;          // decode: shares and presence
+    Res r;
+    const uint16_t* errs;  // decode: error locators [count][n] (log domain)
+    uint16_t* errs_out;    // the same array, written by errloc16g_kernel
+    const uint16_t* logwalsh;
+    uint8_t* work;         // [count][2][npts][S] (decode) or [count][npts][S] (encode)
+    uint64_t cw_bytes;     // bytes of one codeword's work (all arrays)
+    uint32_t npts, m, k, S, chunks;
+    uint32_t q0, count;    // codewords [q0, q0 + count) of the set, work slot q - q0
+    uint32_t D, bits;      // group stride and size (G = 2^bits <= 16)
+    uint32_t nifft, nfft;  // IFFT layers (ascending from d = D), then FFT layers (descending to D)
+    int ifft_off;          // encode: m - 1; decode: -1
+    uint32_t src, dst;     // 0 work A; 1 work B; 2 shares (first / last pass)
+    uint32_t decode;
+};
+
+__device__ __forceinline__ uint64_t g16_share(const G16Pass& p, uint32_t q, uint32_t e, bool out) {
+    // byte offset of share e (encode: data e, or parity e when out) of codeword q
+    const uint64_t rel = cw_rel(p.cs, q);
+    return rel + (out ? p.cs.out_offset : 0ull) + (uint64_t)e * p.cs.elem_stride;
+}
+
+template <int BITS, int NI, int NF>
+__global__ __launch_bounds__(256) void g16_pass_kernel(G16Pass p) {
+    constexpr uint32_t G = 1u << BITS;
+    const uint32_t groups = p.npts >> BITS;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+    if (wv >= p.count * p.chunks * groups) return;
+    const uint32_t g = wv % groups, rest = wv / groups;
+    const uint32_t chunk = rest % p.chunks, qi = rest / p.chunks, q = p.q0 + qi;
+    const Lane ln = lane_of(chunk, p.S);
+    const uint32_t D = p.D;
+    const uint32_t base = (g / D) * G * D + (g % D);
+    uint8_t* const wk = p.work + (uint64_t)qi * p.cw_bytes;
+    const uint64_t arr = (uint64_t)p.npts * p.S;  // decode: array B follows A
+    uint32_t l[G], h[G];
+    // load
+    sfor<G>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        const uint32_t e = base + (uint32_t)j * D;
+        l[j] = 0u;
+        h[j] = 0u;
+        if (p.src <= 1u) {
+            const auto rs = rsrc(wk + (p.src ? arr : 0ull) + (uint64_t)e * p.S);
+            l[j] = ld(rs, ln.lo, 0u);
+            h[j] = ld(rs, ln.lo + 32, 0u);
+        } else if (!p.decode) {
+            if (e < p.k) {
+                const auto rs = rsrc(p.cs.base + g16_share(p, q, e, false));
+                l[j] = ld(rs, ln.lo, 0u);
+                h[j] = ld(rs, ln.lo + 32, 0u);
+            }
+        } else {
+            // decoder input: point e < k <- parity share k + e, m <= e < m + k <- data e - m
+            uint32_t srcs = 0xFFFFFFFFu;
+            if (e < p.k) srcs = p.k + e;
+            else if (e >= p.m && e < p.m + p.k) srcs = e - p.m;
+            if (srcs != 0xFFFFFFFFu) {
+                const uint64_t cell = cell_of(p.ds, q, srcs);
+                const bool have = __builtin_amdgcn_readfirstlane(p.ds.presence[cell] ? 1u : 0u) != 0;
+                if (have) {
+                    const auto rs = rsrc(p.ds.base + cell * p.S);
+                    l[j] = ld(rs, ln.lo, 0u);
+                    h[j] = ld(rs, ln.lo + 32, 0u);
+                    const uint32_t L = __builtin_amdgcn_readfirstlane((uint32_t)p.errs[(uint64_t)qi * p.npts + e]);
+                    mul16(l[j], h[j], p.r.perm[L]);
+                }
+            }
+        }
+    });
+    // IFFT layers d = D 2^t (t < NI ascending), then FFT layers (t = NF-1 .. 0)
+    sfor<NI>([&](auto T) {
+        constexpr int t = decltype(T)::value, dj = 1 << t;
+        const uint32_t d = D << t;
+        sfor<G / 2>([&](auto Q) {
+            constexpr int qq = decltype(Q)::value;
+            constexpr int j = (qq / dj) * 2 * dj + (qq % dj);
+            const uint32_t bl = (base + (uint32_t)j * D) & ~(2u * d - 1u);
+            ifft2(l[j], h[j], l[j + dj], h[j + dj], skew_at(p.r, p.ifft_off + (int)(bl + d)), p.r);
+        });
+    });
+    sfor<NF>([&](auto T) {
+        constexpr int t = NF - 1 - decltype(T)::value, dj = 1 << t;
+        const uint32_t d = D << t;
+        sfor<G / 2>([&](auto Q) {
+            constexpr int qq = decltype(Q)::value;
+            constexpr int j = (qq / dj) * 2 * dj + (qq % dj);
+            const uint32_t bl = (base + (uint32_t)j * D) & ~(2u * d - 1u);
+            fft2(l[j], h[j], l[j + dj], h[j + dj], skew_at(p.r, (int)(bl + d) - 1), p.r);
+        });
+    });
+    // store
+    sfor<G>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        const uint32_t e = base + (uint32_t)j * D;
+        if (p.dst <= 1u) {
+            const auto rs = rsrc(wk + (p.dst ? arr : 0ull) + (uint64_t)e * p.S);
+            st(rs, l[j], ln.lo, 0u);
+            st(rs, h[j], ln.lo + 32, 0u);
+        } else if (!p.decode) {
+            if (e < p.k) {
+                const auto rs = rsrc(p.cs.out_base + g16_share(p, q, e, true));
+                st(rs, l[j], ln.lo, 0u);
+                st(rs, h[j], ln.lo + 32, 0u);
+            }
+        } else {
+            uint32_t dsts = 0xFFFFFFFFu;
+            if (e < p.k) dsts = p.k + e;
+            else if (e >= p.m && e < p.m + p.k) dsts = e - p.m;
+            if (dsts != 0xFFFFFFFFu) {
+                const uint64_t cell = cell_of(p.ds, q, dsts);
+                const bool missing = __builtin_amdgcn_readfirstlane(p.ds.presence[cell] ? 0u : 1u) != 0;
+                if (missing) {
+                    const uint32_t L = kMod16 - __builtin_amdgcn_readfirstlane((uint32_t)p.errs[(uint64_t)qi * p.npts + e]);
+                    mul16(l[j], h[j], p.r.perm[L]);
+                    const auto rs = rsrc(p.ds.base + cell * p.S);
+                    st(rs, l[j], ln.lo, 0u);
+                    st(rs, h[j], ln.lo + 32, 0u);
+                }
+            }
+        }
+    });
+}
+
+// One bit group of the decoder's formal derivative: B[e] (^)= XOR over the group's
+// bits t with bit t of e clear of A[e + 2^t]; the first group also adds A[e].
+template <int BITS>
+__global__ __launch_bounds__(256) void g16_deriv_kernel(G16Pass p) {
+    constexpr uint32_t G = 1u << BITS;
+    const uint32_t groups = p.npts >> BITS;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+    if (wv >= p.count * p.chunks * groups) return;
+    const uint32_t g = wv % groups, rest = wv / groups;
+    const uint32_t chunk = rest % p.chunks, qi = rest / p.chunks;
+    const Lane ln = lane_of(chunk, p.S);
+    const uint32_t D = p.D;
+    const uint32_t base = (g / D) * G * D + (g % D);
+    uint8_t* const wk = p.work + (uint64_t)qi * p.cw_bytes;
+    const uint64_t arr = (uint64_t)p.npts * p.S;
+    const bool first = p.src != 0u;  // src = 1 marks the first group (B starts as A)
+    uint32_t al[G], ah[G];
+    sfor<G>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        const auto rs = rsrc(wk + (uint64_t)(base + (uint32_t)j * D) * p.S);
+        al[j] = ld(rs, ln.lo, 0u);
+        ah[j] = ld(rs, ln.lo + 32, 0u);
+    });
+    sfor<G>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        const uint32_t e = base + (uint32_t)j * D;
+        const auto rb = rsrc(wk + arr + (uint64_t)e * p.S);
+        uint32_t ol = first ? al[j] : ld(rb, ln.lo, 0u);
+        uint32_t oh = first ? ah[j] : ld(rb, ln.lo + 32, 0u);
+        sfor<BITS>([&](auto T) {
+            constexpr int t = decltype(T)::value;
+            if constexpr (((j >> t) & 1) == 0) {
+                ol ^= al[j + (1 << t)];
+                oh ^= ah[j + (1 << t)];
+            }
+        });
+        st(rb, ol, ln.lo, 0u);
+        st(rb, oh, ln.lo + 32, 0u);
+    });
+}
+
+// Error locator for any m (the m <= 512 kernel with m a runtime value).
+__global__ __launch_bounds__(1024) void errloc16g_kernel(G16Pass p) {
+    __shared__ uint16_t err[65536];
+    const uint32_t qi = blockIdx.x, q = p.q0 + qi;
+    const uint32_t k = p.k, M = p.m;
+#pragma unroll 2
+    for (uint32_t i = threadIdx.x; i < 65536u; i += 1024u) {
+        uint32_t v = 0;
+        if (i < k) v = p.ds.presence[cell_of(p.ds, q, k + i)] ? 0u : 1u;
+        else if (i < M) v = 1u;
+        else if (i < M + k) v = p.ds.presence[cell_of(p.ds, q, i - M)] ? 0u : 1u;
+        err[i] = (uint16_t)v;
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll 1
+        for (uint32_t d = 1; d < 65536u; d <<= 1) {
+#pragma unroll 4
+            for (uint32_t b = threadIdx.x; b < 32768u; b += 1024u) {
+                const uint32_t i = (b / d) * 2 * d + (b % d);
+                const uint32_t a = err[i], c = err[i + d];
+                err[i] = (uint16_t)addm(a, c);
+                err[i + d] = (uint16_t)subm(a, c);
+            }
+            __syncthreads();
+        }
+        if (pass == 0) {
+#pragma unroll 4
+            for (uint32_t i = threadIdx.x; i < 65536u; i += 1024u)
+                err[i] = (uint16_t)(((uint32_t)err[i] * p.logwalsh[i]) % kMod16);
+            __syncthreads();
+        }
+    }
+    for (uint32_t i = threadIdx.x; i < p.npts; i += 1024u) p.errs_out[(uint64_t)qi * p.npts + i] = err[i];
+}
+
 inline uint32_t blocks_for(uint64_t tasks) { return (uint32_t)((tasks + 3) / 4); }
 
 template <int M>
@@ -783,13 +1007,170 @@ hipError_t run_decode(const DecodeSet& ds, const Gf16Dev& g, const uint16_t* log
     return hipSuccess;
 }
 
+
+// ---- generic multi-pass launchers (m >= 1024) ----
+template <int BITS, int NI, int NF>
+static void g16_go(const G16Pass& p, hipStream_t st) {
+    const uint64_t waves = (uint64_t)p.count * p.chunks * (p.npts >> BITS);
+    hipLaunchKernelGGL((g16_pass_kernel<BITS, NI, NF>), dim3(blocks_for(waves)), dim3(256), 0, st, p);
+}
+// pass shapes: lower groups IFFT-only / FFT-only (4 bits); the top group (1..4
+// bits) IFFT + FFT (encode), or IFFT-only and FFT-only around the derivative (decode)
+static hipError_t g16_pass(const G16Pass& p, uint32_t bits, uint32_t ni, uint32_t nf, hipStream_t st) {
+#define RSM_G16(b)                                          \
+    case b:                                                 \
+        if (ni == b && nf == b) g16_go<b, b, b>(p, st);     \
+        else if (ni == b && nf == 0) g16_go<b, b, 0>(p, st); \
+        else if (ni == 0 && nf == b) g16_go<b, 0, b>(p, st); \
+        else return hipErrorInvalidValue;                   \
+        break;
+    switch (bits) {
+        RSM_G16(1)
+        RSM_G16(2)
+        RSM_G16(3)
+        RSM_G16(4)
+        default: return hipErrorInvalidValue;
+    }
+#undef RSM_G16
+    return hipGetLastError();
+}
+template <int BITS>
+static void g16_deriv_go(const G16Pass& p, hipStream_t st) {
+    const uint64_t waves = (uint64_t)p.count * p.chunks * (p.npts >> BITS);
+    hipLaunchKernelGGL((g16_deriv_kernel<BITS>), dim3(blocks_for(waves)), dim3(256), 0, st, p);
+}
+static hipError_t g16_deriv(const G16Pass& p, uint32_t bits, hipStream_t st) {
+    switch (bits) {
+        case 1: g16_deriv_go<1>(p, st); break;
+        case 2: g16_deriv_go<2>(p, st); break;
+        case 3: g16_deriv_go<3>(p, st); break;
+        case 4: g16_deriv_go<4>(p, st); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// bit groups of an L-bit transform: 4 bits per group from the bottom, the
+// remainder (1..4 bits) on top
+struct G16Groups {
+    uint32_t n = 0, bits[4] = {}, D[4] = {};
+};
+static G16Groups g16_groups(uint32_t L) {
+    G16Groups g;
+    g.n = (L + 3) / 4;
+    for (uint32_t i = 0; i < g.n; ++i) {
+        g.bits[i] = i + 1 < g.n ? 4u : L - 4u * (g.n - 1);
+        g.D[i] = 1u << (4u * i);
+    }
+    return g;
+}
+static uint32_t ilog2u(uint32_t x) {
+    uint32_t r = 0;
+    while ((1u << r) < x) ++r;
+    return r;
+}
+
+static hipError_t run_encode_generic(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st) {
+    const uint32_t m = ceil_pow2(cs.k);
+    const uint32_t chunks = (cs.S + 511) / 512;
+    const uint64_t per_cw = (uint64_t)m * cs.S;
+    const uint32_t batch = (uint32_t)(g.scratch_bytes / per_cw);
+    if (batch == 0) return hipErrorOutOfMemory;
+    const G16Groups gr = g16_groups(ilog2u(m));
+    for (uint32_t q0 = 0; q0 < cs.count; q0 += batch) {
+        G16Pass p{};
+        p.cs = cs;
+        p.r = Res{g.perm, g.skew};
+        p.work = g.scratch;
+        p.cw_bytes = per_cw;
+        p.npts = m;
+        p.m = m;
+        p.k = cs.k;
+        p.S = cs.S;
+        p.chunks = chunks;
+        p.q0 = q0;
+        p.count = cs.count - q0 < batch ? cs.count - q0 : batch;
+        p.ifft_off = (int)m - 1;
+        hipError_t e;
+        const uint32_t top = gr.n - 1;
+        for (uint32_t i = 0; i < top; ++i) {  // IFFT, lower groups (the first reads the data shares)
+            p.D = gr.D[i];
+            p.src = i == 0 ? 2u : 0u;
+            p.dst = 0u;
+            if ((e = g16_pass(p, 4, 4, 0, st)) != hipSuccess) return e;
+        }
+        p.D = gr.D[top];
+        p.src = top == 0 ? 2u : 0u;
+        p.dst = top == 0 ? 2u : 0u;
+        if ((e = g16_pass(p, gr.bits[top], gr.bits[top], gr.bits[top], st)) != hipSuccess) return e;
+        for (uint32_t i = top; i-- > 0;) {  // FFT, lower groups (the last writes the parity)
+            p.D = gr.D[i];
+            p.src = 0u;
+            p.dst = i == 0 ? 2u : 0u;
+            if ((e = g16_pass(p, 4, 0, 4, st)) != hipSuccess) return e;
+        }
+    }
+    return hipSuccess;
+}
+
+static hipError_t run_decode_generic(const DecodeSet& ds, const Gf16Dev& g, hipStream_t st) {
+    const uint32_t m = ceil_pow2(ds.k), n = 2 * m;
+    const uint32_t chunks = (ds.S + 511) / 512;
+    const uint64_t per_cw = 2ull * n * ds.S;
+    uint32_t batch = (uint32_t)(g.scratch_bytes / per_cw);
+    const uint32_t ebatch = (uint32_t)(g.errs_bytes / (n * sizeof(uint16_t)));
+    if (ebatch < batch) batch = ebatch;
+    if (batch == 0) return hipErrorOutOfMemory;
+    const G16Groups gr = g16_groups(ilog2u(n));
+    const uint32_t top = gr.n - 1;
+    for (uint32_t q0 = 0; q0 < ds.count; q0 += batch) {
+        G16Pass p{};
+        p.ds = ds;
+        p.r = Res{g.perm, g.skew};
+        p.errs = g.errs;
+        p.errs_out = g.errs;
+        p.logwalsh = g.logwalsh;
+        p.work = g.scratch;
+        p.cw_bytes = per_cw;
+        p.npts = n;
+        p.m = m;
+        p.k = ds.k;
+        p.S = ds.S;
+        p.chunks = chunks;
+        p.q0 = q0;
+        p.count = ds.count - q0 < batch ? ds.count - q0 : batch;
+        p.ifft_off = -1;
+        p.decode = 1u;
+        hipLaunchKernelGGL(errloc16g_kernel, dim3(p.count), dim3(1024), 0, st, p);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        for (uint32_t i = 0; i <= top; ++i) {  // IFFT up to the top group -> A
+            p.D = gr.D[i];
+            p.src = i == 0 ? 2u : 0u;
+            p.dst = 0u;
+            if ((e = g16_pass(p, gr.bits[i], gr.bits[i], 0, st)) != hipSuccess) return e;
+        }
+        for (uint32_t i = 0; i <= top; ++i) {  // formal derivative: B = A + sum T_g(A)
+            p.D = gr.D[i];
+            p.src = i == 0 ? 1u : 0u;
+            if ((e = g16_deriv(p, gr.bits[i], st)) != hipSuccess) return e;
+        }
+        for (uint32_t i = top + 1; i-- > 0;) {  // FFT on B down to group 0, which reveals
+            p.D = gr.D[i];
+            p.src = 1u;
+            p.dst = i == 0 ? 2u : 1u;
+            if ((e = g16_pass(p, gr.bits[i], 0, gr.bits[i], st)) != hipSuccess) return e;
+        }
+    }
+    return hipSuccess;
+}
 }  // namespace
 
 hipError_t launch_encode_gf16(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st) {
     switch (ceil_pow2(cs.k)) {
         case 256: return run_encode<256>(cs, g, st);
         case 512: return run_encode<512>(cs, g, st);
-        default: return hipErrorNotSupported;
+        default: return cs.k <= 32768u ? run_encode_generic(cs, g, st) : hipErrorNotSupported;
     }
 }
 
@@ -797,7 +1178,7 @@ hipError_t launch_decode_gf16(const DecodeSet& ds, const Gf16Dev& g, hipStream_t
     switch (ceil_pow2(ds.k)) {
         case 256: return run_decode<256>(ds, g, g.logwalsh, st);
         case 512: return run_decode<512>(ds, g, g.logwalsh, st);
-        default: return hipErrorNotSupported;
+        default: return ds.k <= 32768u ? run_decode_generic(ds, g, st) : hipErrorNotSupported;
     }
 }
 

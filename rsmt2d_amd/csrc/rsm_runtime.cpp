@@ -128,9 +128,12 @@ StreamScratch& stream_scratch(rsm_ctx* ctx, hipStream_t st) {
 // ---------------------------------------------------------------------------
 // Launch helpers (device-resident, asynchronous on `st`)
 // ---------------------------------------------------------------------------
-// GF(2^16) kernels support m = ceilPow2(k) in {256, 512} (2k <= 1024 shards:
-// every configuration in BASELINE.json); larger k returns RSM_EUNSUPPORTED.
-static bool gf16_supported(uint32_t k) { return k > 128 && k <= 512; }
+// GF(2^16): m = ceilPow2(k) in {256, 512} runs the on-chip single-pass kernels
+// (every configuration in BASELINE.json); 512 < k <= 32768 (the reference's
+// MaxChunks = 32768^2, leopard.go:76-84) the multi-pass generic kernels through
+// per-stream work arrays.
+static bool gf16_supported(uint32_t k) { return k > 128 && k <= 32768; }
+static bool gf16_generic(uint32_t k) { return ceil_pow2(k) > 512; }
 
 int ensure_gf16_tables(rsm_ctx* ctx) {
     std::lock_guard<std::mutex> lk(ctx->gf16_mu);
@@ -193,12 +196,24 @@ int launch_encode(rsm_ctx* ctx, const CodewordSet& cs0, hipStream_t st) {
         cs.grid = (cap > 0 && cap < ctx->cus) ? cap : ctx->cus;
         e = launch_encode_gf8(cs, st);
     } else {
-        if (!gf16_supported(cs.k)) return fail(RSM_EUNSUPPORTED, "encode: k=%u (m > 512) not supported in this build", cs.k);
-        // single pass per codeword: the tables only, no work arrays
-        if (int rc = ensure_gf16_tables(ctx)) return rc;
-        Gf16Dev g = ctx->gf16;
-        g.cus = ctx->cus;
-        e = launch_encode_gf16(cs, g, st);
+        if (!gf16_supported(cs.k)) return fail(RSM_EUNSUPPORTED, "encode: k=%u exceeds 32768", cs.k);
+        if ((uint64_t)ceil_pow2(cs.k) * 2 * cs.S >= (1ull << 31))
+            return fail(RSM_EUNSUPPORTED, "encode: k=%u with %u-byte shares exceeds the 2 GiB work-array offsets", cs.k, cs.S);
+        if (!gf16_generic(cs.k)) {
+            // single pass per codeword: the tables only, no work arrays
+            if (int rc = ensure_gf16_tables(ctx)) return rc;
+            Gf16Dev g = ctx->gf16;
+            g.cus = ctx->cus;
+            e = launch_encode_gf16(cs, g, st);
+        } else {
+            const uint64_t per_cw = (uint64_t)ceil_pow2(cs.k) * cs.S;
+            StreamScratch& ss = stream_scratch(ctx, st);
+            std::lock_guard<std::mutex> lk(ss.mu);
+            Gf16Dev g;
+            if (int rc = gf16_for_stream(ctx, ss, st, gf16_budget(per_cw, cs.count), 0, &g)) return rc;
+            g.cus = ctx->cus;
+            e = launch_encode_gf16(cs, g, st);
+        }
     }
     if (e != hipSuccess) return hip_fail(e, "encode kernel launch");
     return RSM_OK;
@@ -211,7 +226,9 @@ int launch_decode(rsm_ctx* ctx, const DecodeSet& ds0, hipStream_t st) {
         ds.chunks = (ds.S + 255) / 256;
         e = launch_decode_gf8(ds, st);
     } else {
-        if (!gf16_supported(ds.k)) return fail(RSM_EUNSUPPORTED, "decode: k=%u (m > 512) not supported in this build", ds.k);
+        if (!gf16_supported(ds.k)) return fail(RSM_EUNSUPPORTED, "decode: k=%u exceeds 32768", ds.k);
+        if ((uint64_t)ceil_pow2(ds.k) * 2 * ds.S >= (1ull << 31))
+            return fail(RSM_EUNSUPPORTED, "decode: k=%u with %u-byte shares exceeds the 2 GiB work-array offsets", ds.k, ds.S);
         const uint64_t n = 2ull * ceil_pow2(ds.k);
         const uint64_t per_cw = 2ull * n * ds.S;
         const uint64_t budget = gf16_budget(per_cw, ds.count);

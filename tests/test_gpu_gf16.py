@@ -82,10 +82,3 @@ def test_gf16_repair(lib, rng):
     eds.Repair(rr, cr)
     assert eds.Equals(original)
     assert eds.repair_stats().fast_path == 1
-
-
-def test_unsupported_k_fails_loudly(lib, rng):
-    data = rand_shares(rng, 513, 64)
-    with pytest.raises(R.RSMError) as e:
-        R.NewLeoRSCodec().Encode(data)
-    assert e.value.code == R.RSM_EUNSUPPORTED
