@@ -43,7 +43,7 @@ def parse():
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
-    p.add_argument("--batch", type=int, default=0, help="squares per step (default: >= 512 MiB of EDS)")
+    p.add_argument("--batch", type=int, default=0, help="squares per step (default: >= 1 GiB of EDS; steps rotate over --buffers batches, so a step never finds its squares in the 256 MiB Infinity Cache)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-c5", action="store_true", help="skip the config-5 (sharded 512x512 square) line")
     p.add_argument("--no-c3", action="store_true", help="skip the config-3 (Repair) timings")
@@ -445,7 +445,7 @@ def main():
     k, S = wl["k"], wl["S"]
     W = 2 * k
     sq_bytes = W * W * S
-    B = a.batch or max(1, (512 << 20) // sq_bytes)
+    B = a.batch or max(1, (1 << 30) // sq_bytes)
     L = R.library()
     ctx = R.device_context(local)
 
@@ -565,7 +565,7 @@ def main():
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_latest.json")
     if bitsliced and os.path.exists(pmc_path):
-        want = "encode_gf8_bs128u_kernel<%d, %d>" % ((56, 1) if col_dom else (40, 0))
+        want = "encode_gf8_bs128u_kernel<%d, %d>" % ((184, 1) if col_dom else (104, 0))
         sets = (W if col_dom else k) * B * S // 2048
         grid_threads = min(sets, 256) * 512  # persistent grid: one 512-thread workgroup per CU
         for row in json.load(open(pmc_path)).get("launches", []):

@@ -190,11 +190,11 @@ __device__ __forceinline__ void xch_to_small(uint32_t (&X)[16][8], uint32_t wb, 
 #undef RSM_W_LARGE
 #undef RSM_SYNC
 
-template <bool NT>
+template <bool NT, int J0 = 0, int J1 = kPre>
 __device__ __forceinline__ void issue_dma_rt(const CodewordSet& cs, const SetAddr& a, uint32_t lds_base, uint32_t A) {
     const uint32_t k = cs.k, es = (uint32_t)cs.elem_stride;
-    bs8::sfor<kPre>([&](auto J) {
-        constexpr int j = decltype(J)::value;
+    bs8::sfor<J1 - J0>([&](auto J) {
+        constexpr int j = J0 + decltype(J)::value;
         const uint32_t so = sym_off(16u * A + j, k, 0, es);
         const uint32_t l = __builtin_amdgcn_readfirstlane(lds_base + kXchBytes + A * (kPre * 2048u) + j * 2048u);
         dma16<NT>(l, a.off[0], a.rs, so);
@@ -282,11 +282,18 @@ __device__ __forceinline__ void bs_uni_wave(const CodewordSet& cs, uint32_t sets
         const uint32_t tn = t + G;
         const bool more = tn < sets;
         SetAddr an = a;
+        // LATE (MODE 64, A/B): the direct half of the next set's loads is issued after
+        // the first exchange instead of with the LDS-DMA half (spreads the reads)
+        // A/B: MODE 64 issues the direct half of the next set's loads after the first
+        // exchange, 128 after the large layers; 256 splits the LDS-DMA half (symbols
+        // j >= kPre/2 after the first exchange) -- spreading the reads over the set
+        constexpr bool LATE = (MODE & (64 | 128)) != 0, LATER = (MODE & 128) != 0, SPLIT = (MODE & 256) != 0;
         if (more) {
             an = addr(tn);
             if (MEM) {
-                issue_dma_rt<NTL>(cs, an, lds_base, A);
-                issue_direct_rt<NTL>(cs, an, A, P);
+                if constexpr (SPLIT) issue_dma_rt<NTL, 0, kPre / 2>(cs, an, lds_base, A);
+                else issue_dma_rt<NTL>(cs, an, lds_base, A);
+                if constexpr (!LATE) issue_direct_rt<NTL>(cs, an, A, P);
             }
         }
         if constexpr (ARITH) {
@@ -294,7 +301,13 @@ __device__ __forceinline__ void bs_uni_wave(const CodewordSet& cs, uint32_t sets
             bs8::small_ifft_all(X, A);
         }
         bs8::sfor<8>([&](auto Pp) { xch_to_large<decltype(Pp)::value, ADDTID>(X, e_small, s_small, e_large); });
+        if (more && MEM) {
+            if constexpr (SPLIT) issue_dma_rt<NTL, kPre / 2, kPre>(cs, an, lds_base, A);
+            if constexpr (LATE && !LATER) issue_direct_rt<NTL>(cs, an, A, P);
+        }
         if constexpr (ARITH) bs8::large_ifft_fft(X);
+        if constexpr (LATER)
+            if (more && MEM) issue_direct_rt<NTL>(cs, an, A, P);
         bs8::sfor<8>([&](auto Pp) { xch_to_small<decltype(Pp)::value, ADDTID>(X, e_large, s_large, e_small); });
         if constexpr (ARITH) bs8::small_fft_all(X, A);
         {
@@ -702,10 +715,12 @@ bool bs128_applicable(const CodewordSet& cs) {
     return span + sym < kOobBs;
 }
 
-// Production launch: row pass MODE 40 (ds_write_addtid_b32 exchange + non-temporal
-// loads: its Q1 stores keep the default policy), column pass MODE 56 (+ non-temporal
-// stores: Q2/Q3 are final output, never re-read; 3-4 % faster per step than MODE 40 in
-// the two-stream schedule, profiles/r02d_sched_ab.jsonl).  The column pass walks its
+// Production launch: row pass MODE 104 (ds_write_addtid_b32 exchange + non-temporal
+// loads, the next set's direct loads issued after the first exchange: its Q1 stores
+// keep the default policy), column pass MODE 184 (+ non-temporal stores -- Q2/Q3 are
+// final output, never re-read -- and the direct loads after the large layers).
+// Measured in the two-stream schedule (profiles/r02d_sched_ab.jsonl): NT stores 3-4 %,
+// the spread-out load issue another 3-4 % per step.  The column pass walks its
 // sets in reverse order (its first reads are the squares the row pass wrote last).
 // The persistent grid is the caller's (the context's CU count or per-pass cap).
 #ifdef RSM_DIAG
@@ -746,16 +761,23 @@ hipError_t launch_encode_gf8_bs128(const CodewordSet& cs, hipStream_t st) {
             case 42: RSM_BS_LAUNCH(42, 1); return hipGetLastError();  // no arithmetic (wrong output)
             case 58: RSM_BS_LAUNCH(58, 1); return hipGetLastError();  // no arithmetic (wrong output)
             case 44: RSM_BS_LAUNCH(44, 1); return hipGetLastError();  // no global memory (wrong output)
+            case 104: RSM_BS_LAUNCH(104, 1); return hipGetLastError();  // 40 + late direct loads
+            case 120: RSM_BS_LAUNCH(120, 1); return hipGetLastError();  // 56 + late direct loads
+            case 184: RSM_BS_LAUNCH(184, 1); return hipGetLastError();  // 56 + later direct loads
+            case 376: RSM_BS_LAUNCH(376, 1); return hipGetLastError();  // 56 + late direct + split DMA
+            case 440: RSM_BS_LAUNCH(440, 1); return hipGetLastError();  // 56 + later direct + split DMA
+            case 168: RSM_BS_LAUNCH(168, 1); return hipGetLastError();  // 40 + later direct loads
+            case 360: RSM_BS_LAUNCH(360, 1); return hipGetLastError();  // 40 + late direct + split DMA
             default: break;
         }
-        if (row) RSM_BS_LAUNCH(40, 0);
-        else RSM_BS_LAUNCH(56, 1);
+        if (row) RSM_BS_LAUNCH(104, 0);
+        else RSM_BS_LAUNCH(184, 1);
         return hipGetLastError();
     }
 #else
     const uint32_t rev = row ? 0u : 1u;
-    if (row) RSM_BS_LAUNCH(40, 0);
-    else RSM_BS_LAUNCH(56, 1);
+    if (row) RSM_BS_LAUNCH(104, 0);
+    else RSM_BS_LAUNCH(184, 1);
 #endif
 #undef RSM_BS_LAUNCH
     return hipGetLastError();
