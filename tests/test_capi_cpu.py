@@ -144,10 +144,13 @@ def test_product_has_no_diagnostics(lib):
                  b"RSM_GF8_KERNEL", b"RSM_GF16_BATCH_MB"):
         assert name not in blob, name
     assert not re.search(rb"RSM_[A-Z0-9_]{3,}\x00", blob), re.search(rb"RSM_[A-Z0-9_]{3,}\x00", blob)
-    # kernel symbols embedded in the gfx950 code object: only MODE 40 of the
-    # bit-sliced encode, no fused (bs128f) or dual (bs128p) kernel
+    # kernel symbols embedded in the gfx950 code object: only the production modes
+    # of the bit-sliced encode (row pass 104, column pass 184: kernels_gf8_bs.hip),
+    # no diagnostic mode (bits 2 / 4: no arithmetic / no memory), no fused (bs128f)
+    # or dual (bs128p) kernel
     modes = set(re.findall(rb"encode_gf8_bs128u_kernelILi(\d+)E", blob))
-    assert modes == {b"40"}, modes
+    assert modes == {b"104", b"184"}, modes
+    assert not any(int(m) & 6 for m in modes)
     assert b"encode_gf8_bs128f_kernel" not in blob and b"encode_gf8_bs128p_kernel" not in blob
     txt = re.sub(r"/\*.*?\*/", "", open(DIAG_HEADER).read(), flags=re.S)
     for s in set(re.findall(r"\b(rsm_diag_[a-z0-9_]+)\s*\(", txt)):
