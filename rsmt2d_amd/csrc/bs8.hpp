@@ -134,42 +134,41 @@ RSM_HD void transpose8(uint32_t (&w)[8]) {
 
 #if defined(__HIPCC__)
 // Device 8x8 transpose as one asm block: per swap t1 = b << s, t2 = a >> s,
-// a = bfi(m << s, t1, a), b = bfi(m, t2, b) -- 4 VALU (the xor form above is 5 on
-// gfx9, which has no v_lshl_xor), two swaps interleaved so consecutive
-// instructions are independent.  Same permutation as transpose8.
-#define RSM_T8_PAIR(a, b, s, m, mh)                    \
-    "v_lshlrev_b32 %8, " #s ", %" #b "\n\t"             \
-    "v_lshrrev_b32 %9, " #s ", %" #a "\n\t"
-#define RSM_T8_PAIR2(a, b, s, m, mh)                   \
-    "v_lshlrev_b32 %10, " #s ", %" #b "\n\t"            \
-    "v_lshrrev_b32 %11, " #s ", %" #a "\n\t"
-#define RSM_T8_FIN(a, b, m, mh)                        \
-    "v_bfi_b32 %" #a ", %" #mh ", %8, %" #a "\n\t"        \
-    "v_bfi_b32 %" #b ", %" #m ", %9, %" #b "\n\t"
-#define RSM_T8_FIN2(a, b, m, mh)                       \
-    "v_bfi_b32 %" #a ", %" #mh ", %10, %" #a "\n\t"       \
-    "v_bfi_b32 %" #b ", %" #m ", %11, %" #b "\n\t"
-#define RSM_T8_2SWAPS(a0, b0, a1, b1, s, m, mh) \
-    RSM_T8_PAIR(a0, b0, s, m, mh) RSM_T8_PAIR2(a1, b1, s, m, mh) RSM_T8_FIN(a0, b0, m, mh) RSM_T8_FIN2(a1, b1, m, mh)
+// a = sel(m << s ? t1 : a), b = sel(m ? t2 : b), two swaps interleaved so
+// consecutive instructions are independent.  Same permutation as transpose8.
+// On gfx950 every shift and v_bfi_b32 issues at half rate (4.5 cycles per wave
+// instruction with two waves per SIMD) while v_bitop3_b32 and v_add_u32 issue at
+// full rate (2.4-2.9; profiles/r02d_aluprobe.jsonl), so the select is a
+// v_bitop3_b32 (truth table 0xD8: S2 ? S1 : S0) and the s = 1 left shift a
+// v_add_u32 (b + b).
+#define RSM_T8_SHL(d, b, s) "v_lshlrev_b32 %" #d ", " #s ", %" #b "\n\t"
+#define RSM_T8_SHL1(d, b, s) "v_add_u32 %" #d ", %" #b ", %" #b "\n\t"
+#define RSM_T8_PAIRS(SHL, a0, b0, a1, b1, s, m, mh)    \
+    SHL(8, b0, s)                                    \
+    "v_lshrrev_b32 %9, " #s ", %" #a0 "\n\t"           \
+    SHL(10, b1, s)                                   \
+    "v_lshrrev_b32 %11, " #s ", %" #a1 "\n\t"          \
+    "v_bitop3_b32 %" #a0 ", %" #a0 ", %8, %" #mh " bitop3:0xd8\n\t" \
+    "v_bitop3_b32 %" #b0 ", %" #b0 ", %9, %" #m " bitop3:0xd8\n\t"  \
+    "v_bitop3_b32 %" #a1 ", %" #a1 ", %10, %" #mh " bitop3:0xd8\n\t" \
+    "v_bitop3_b32 %" #b1 ", %" #b1 ", %11, %" #m " bitop3:0xd8\n\t"
 __device__ __forceinline__ void transpose8_dev(uint32_t (&w)[8]) {
     uint32_t t0, t1, t2, t3;
     asm volatile(
-        RSM_T8_2SWAPS(0, 4, 1, 5, 4, 12, 13)
-        RSM_T8_2SWAPS(2, 6, 3, 7, 4, 12, 13)
-        RSM_T8_2SWAPS(0, 2, 1, 3, 2, 14, 15)
-        RSM_T8_2SWAPS(4, 6, 5, 7, 2, 14, 15)
-        RSM_T8_2SWAPS(0, 1, 2, 3, 1, 16, 17)
-        RSM_T8_2SWAPS(4, 5, 6, 7, 1, 16, 17)
+        RSM_T8_PAIRS(RSM_T8_SHL, 0, 4, 1, 5, 4, 12, 13)
+        RSM_T8_PAIRS(RSM_T8_SHL, 2, 6, 3, 7, 4, 12, 13)
+        RSM_T8_PAIRS(RSM_T8_SHL, 0, 2, 1, 3, 2, 14, 15)
+        RSM_T8_PAIRS(RSM_T8_SHL, 4, 6, 5, 7, 2, 14, 15)
+        RSM_T8_PAIRS(RSM_T8_SHL1, 0, 1, 2, 3, 1, 16, 17)
+        RSM_T8_PAIRS(RSM_T8_SHL1, 4, 5, 6, 7, 1, 16, 17)
         : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]), "+v"(w[4]), "+v"(w[5]), "+v"(w[6]), "+v"(w[7]),
           "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3)
         : "s"(0x0F0F0F0Fu), "s"(0xF0F0F0F0u), "s"(0x33333333u), "s"(0xCCCCCCCCu), "s"(0x55555555u),
           "s"(0xAAAAAAAAu));
 }
-#undef RSM_T8_PAIR
-#undef RSM_T8_PAIR2
-#undef RSM_T8_FIN
-#undef RSM_T8_FIN2
-#undef RSM_T8_2SWAPS
+#undef RSM_T8_SHL
+#undef RSM_T8_SHL1
+#undef RSM_T8_PAIRS
 #endif
 
 constexpr int kM = 128;        // transform size handled here (65 <= k <= 128)

@@ -11,6 +11,7 @@
 //   7: exchange, two planes per round (ds_write_b64 / ds_read_b64, 64 KiB buffer)
 //   8: exchange, one plane per step, double-buffered (reads of p + writes of p+1, one barrier)
 //   9-14: 128 independent instructions of one kind per wave (per-instruction issue cost)
+//   15: exchange, two planes per round, hand-written ds_write_b64 / ds_read_b64 (64 KiB)
 // Usage: setprobe [iters]; prints one JSON line per variant (us per set per CU).
 #include "../../rsmt2d_amd/csrc/kernels_gf8_bs.hip"
 #include <cstdio>
@@ -1050,6 +1051,29 @@ __device__ __forceinline__ void xch_db(uint32_t (&X)[16][8], uint32_t* lds, uint
         __syncthreads();
     });
 }
+
+// hand-written two-plane exchange: [symbol][lane] x 8 B, ds_write_b64 / ds_read_b64 with
+// immediate offsets (small e = 16A + j: 8192 A + 512 j; large e = 8h + A: 512 A + 4096 h)
+typedef uint32_t v2u_ __attribute__((ext_vector_type(2)));
+#define XW64(j, o) "ds_write_b64 %16, %" #j " offset:" #o "\n\t"
+#define XR64(j, o) "ds_read_b64 %" #j ", %17 offset:" #o "\n\t"
+#define XSMALL(W) W(0, 0) W(1, 512) W(2, 1024) W(3, 1536) W(4, 2048) W(5, 2560) W(6, 3072) W(7, 3584) \
+    W(8, 4096) W(9, 4608) W(10, 5120) W(11, 5632) W(12, 6144) W(13, 6656) W(14, 7168) W(15, 7680)
+#define XLARGE(W) W(0, 0) W(1, 4096) W(2, 8192) W(3, 12288) W(4, 16384) W(5, 20480) W(6, 24576) W(7, 28672) \
+    W(8, 32768) W(9, 36864) W(10, 40960) W(11, 45056) W(12, 49152) W(13, 53248) W(14, 57344) W(15, 61440)
+template <bool TO_LARGE>
+__device__ __forceinline__ void xch64(v2u_ (&Y)[16], uint32_t wb, uint32_t rb) {
+    if constexpr (TO_LARGE)
+        asm volatile(XSMALL(XW64) "s_waitcnt lgkmcnt(0)\n\ts_barrier\n\t" XLARGE(XR64) "s_waitcnt lgkmcnt(0)\n\ts_barrier"
+                     : "+v"(Y[0]), "+v"(Y[1]), "+v"(Y[2]), "+v"(Y[3]), "+v"(Y[4]), "+v"(Y[5]), "+v"(Y[6]), "+v"(Y[7]),
+                       "+v"(Y[8]), "+v"(Y[9]), "+v"(Y[10]), "+v"(Y[11]), "+v"(Y[12]), "+v"(Y[13]), "+v"(Y[14]), "+v"(Y[15])
+                     : "v"(wb), "v"(rb) : "memory");
+    else
+        asm volatile(XLARGE(XW64) "s_waitcnt lgkmcnt(0)\n\ts_barrier\n\t" XSMALL(XR64) "s_waitcnt lgkmcnt(0)\n\ts_barrier"
+                     : "+v"(Y[0]), "+v"(Y[1]), "+v"(Y[2]), "+v"(Y[3]), "+v"(Y[4]), "+v"(Y[5]), "+v"(Y[6]), "+v"(Y[7]),
+                       "+v"(Y[8]), "+v"(Y[9]), "+v"(Y[10]), "+v"(Y[11]), "+v"(Y[12]), "+v"(Y[13]), "+v"(Y[14]), "+v"(Y[15])
+                     : "v"(wb), "v"(rb) : "memory");
+}
 typedef uint32_t v2u __attribute__((ext_vector_type(2)));
 // exchange with two planes per round through a 64 KiB [symbol][lane] x 8 B buffer
 template <int q>
@@ -1084,6 +1108,23 @@ __global__ __launch_bounds__(512, 1) void setprobe_kernel(uint32_t iters, uint32
         });
     });
     for (uint32_t n = 0; n < iters; ++n) {
+        if constexpr (V == 15) {
+            // X held as 64 two-plane pairs (the layout a b64 exchange needs)
+            v2u_ (&Y)[16][4] = *reinterpret_cast<v2u_ (*)[16][4]>(&X);
+            const uint32_t wsm = lds_base + 8192u * A + lane * 8u, wlg = lds_base + 512u * A + lane * 8u;
+            bs8::sfor<4>([&](auto Q) {
+                v2u_ T[16];
+                bs8::sfor<16>([&](auto J) { T[decltype(J)::value] = Y[decltype(J)::value][decltype(Q)::value]; });
+                xch64<true>(T, wsm, wlg);
+                bs8::sfor<16>([&](auto J) { Y[decltype(J)::value][decltype(Q)::value] = T[decltype(J)::value]; });
+            });
+            bs8::sfor<4>([&](auto Q) {
+                v2u_ T[16];
+                bs8::sfor<16>([&](auto J) { T[decltype(J)::value] = Y[decltype(J)::value][decltype(Q)::value]; });
+                xch64<false>(T, wlg, wsm);
+                bs8::sfor<16>([&](auto J) { Y[decltype(J)::value][decltype(Q)::value] = T[decltype(J)::value]; });
+            });
+        }
         if constexpr (V == 8) { xch_db<true>(X, lds, A, lane); xch_db<false>(X, lds, A, lane); }
         if constexpr (V == 9) alu_lshl(X);
         if constexpr (V == 10) alu_bfi(X);
@@ -1125,8 +1166,8 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    const char* names[] = {"set", "butterflies", "transposes", "exchange", "large", "transposes_x2_sgpr", "transposes_x2_vgpr", "exchange_b64", "exchange_dbuf", "alu_lshl_x128", "alu_bfi_sgpr_x128", "alu_bitop3_x128", "alu_xor_x128", "alu_perm_x128", "alu_bfi_vgpr_x128"};
-    for (int v = 0; v < 15; ++v) {
+    const char* names[] = {"set", "butterflies", "transposes", "exchange", "large", "transposes_x2_sgpr", "transposes_x2_vgpr", "exchange_b64", "exchange_dbuf", "alu_lshl_x128", "alu_bfi_sgpr_x128", "alu_bitop3_x128", "alu_xor_x128", "alu_perm_x128", "alu_bfi_vgpr_x128", "exchange_b64_asm"};
+    for (int v = 0; v < 16; ++v) {
         std::vector<float> ts;
         for (int r = 0; r < 8; ++r) {
             CK(hipEventRecord(e0, 0));
@@ -1146,6 +1187,7 @@ int main(int argc, char** argv) {
                 case 12: hipLaunchKernelGGL(rsm::setprobe_kernel<12>, dim3(cus), dim3(512), 0, 0, iters, sink); break;
                 case 13: hipLaunchKernelGGL(rsm::setprobe_kernel<13>, dim3(cus), dim3(512), 0, 0, iters, sink); break;
                 case 14: hipLaunchKernelGGL(rsm::setprobe_kernel<14>, dim3(cus), dim3(512), 0, 0, iters, sink); break;
+                case 15: hipLaunchKernelGGL(rsm::setprobe_kernel<15>, dim3(cus), dim3(512), 0, 0, iters, sink); break;
             }
             CK(hipGetLastError());
             CK(hipEventRecord(e1, 0));
