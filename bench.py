@@ -160,6 +160,53 @@ def bench_codec(local, L, R, k=128, S=512, calls=400, threads=64):
             "concurrent_GiB_s": round(n * k * S / dt / 2**30, 3)}
 
 
+def bench_fraud_proof(local, L, R, k=128, S=512, reps=300):
+    """Fraud-proof verification (extendeddatacrossword_test.go:116-163)
+    as a light client runs it on one byzantine row of a c2 square: Decode the 2k
+    shares of the proof (k of them nil), DefaultTree root of the rebuilt vector
+    (compared with the row root), re-Encode the first k and compare the parity half.
+    Latency of the whole check from host memory, one proof at a time."""
+    import ctypes
+    import numpy as np
+    ctx = R.device_context(local)
+    rng = np.random.default_rng(0xF4)
+    data = rng.integers(0, 256, (k, S), dtype=np.uint8)
+    par = np.empty((k, S), np.uint8)
+    dp = (ctypes.c_void_p * k)(*[data.ctypes.data + i * S for i in range(k)])
+    pp = (ctypes.c_void_p * k)(*[par.ctypes.data + i * S for i in range(k)])
+    R._check(L.rsm_encode(ctx, dp, k, S, pp))
+    full = np.concatenate([data, par])
+    present = np.ones(2 * k, np.uint8)
+    present[rng.choice(2 * k, size=k, replace=False)] = 0
+    work = np.empty_like(full)
+    wp = (ctypes.c_void_p * (2 * k))(*[work.ctypes.data + i * S for i in range(2 * k)])
+    p2 = np.empty((k, S), np.uint8)
+    pp2 = (ctypes.c_void_p * k)(*[p2.ctypes.data + i * S for i in range(k)])
+    root = ctypes.create_string_buffer(64)
+    rlen = ctypes.c_uint32()
+    lat, t_dec = [], []
+    for i in range(reps + 20):
+        work[:] = full * present[:, None]
+        t0 = time.perf_counter()
+        R._check(L.rsm_decode(ctx, wp, present.ctypes.data, 2 * k, S))
+        t1 = time.perf_counter()
+        rlen.value = 64
+        R._check(L.rsm_default_tree_root(None, 0, 0, wp, 2 * k, S, root, ctypes.byref(rlen)))
+        R._check(L.rsm_encode(ctx, wp, k, S, pp2))
+        ok = np.array_equal(p2, work[k:])
+        t2 = time.perf_counter()
+        if not ok or not np.array_equal(work, full):
+            raise SystemExit("bench fraud proof: rebuilt vector differs")
+        if i >= 20:
+            lat.append(t2 - t0)
+            t_dec.append(t1 - t0)
+    return {"workload": f"fraud-proof check of one row, k={k} S={S}: Decode of 2k shares (k nil) + DefaultTree "
+                        "root + re-Encode + parity compare (extendeddatacrossword_test.go:116-163)",
+            "latency_us_p50": round(pct(lat, 0.5) * 1e6, 1), "latency_us_p10": round(pct(lat, 0.1) * 1e6, 1),
+            "latency_us_p90": round(pct(lat, 0.9) * 1e6, 1), "decode_us_p50": round(pct(t_dec, 0.5) * 1e6, 1),
+            "proofs": reps}
+
+
 def bench_host_path(local, L, R, k, S, squares=8, seconds=2.0):
     """ComputeExtendedDataSquare from host memory (north_star: rate including
     hipMemcpyAsync both ways).  pinned: rsm_extend_squares_host over `squares`
@@ -613,6 +660,7 @@ def main():
             out["host_path"] = bench_host_path(local, L, R, k, S, squares=8 if k <= 128 else 2)
             if k <= 128:
                 out["codec"] = bench_codec(local, L, R)
+                out["fraud_proof"] = bench_fraud_proof(local, L, R)
         out["cpu_baseline"] = None if a.no_cpu_baseline else cpu_baseline(k, S, a.cpu_seconds)
     if rank == 0 and world == 1 and not a.no_roots:
         out["with_roots"] = bench_roots(local, L, R, buf, k, S, B, a.steps)

@@ -14,9 +14,69 @@
 #include <cstring>
 #include <vector>
 
+#if defined(__x86_64__)
+#include <cpuid.h>
+#include <immintrin.h>
+#endif
+
 #include "../../include/rsmt2d_hip.h"
 
 namespace {
+
+#if defined(__x86_64__)
+// SHA-256 compression with the x86 SHA extensions (the GPU box's EPYC and Intel
+// hosts since Ice Lake have them): ~5-7x the scalar loop below, which stays as the
+// fallback.  The host roots are on the fraud-proof and pre-repair paths.
+bool cpu_has_sha_ni() {
+    unsigned a = 0, b = 0, c = 0, d = 0;
+    if (!__get_cpuid_count(7, 0, &a, &b, &c, &d) || !(b & (1u << 29))) return false;  // SHA
+    if (!__get_cpuid(1, &a, &b, &c, &d)) return false;
+    return (c & (1u << 19)) && (c & (1u << 9));  // SSE4.1, SSSE3
+}
+
+alignas(16) constexpr uint32_t kShaK[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+
+__attribute__((target("sha,sse4.1,ssse3"))) void sha256_block_ni(uint32_t h[8], const uint8_t* p) {
+    const __m128i bswap = _mm_set_epi64x(0x0c0d0e0f08090a0bLL, 0x0405060700010203LL);
+    __m128i t = _mm_shuffle_epi32(_mm_loadu_si128(reinterpret_cast<const __m128i*>(h)), 0xB1);  // CDAB
+    __m128i s1 = _mm_shuffle_epi32(_mm_loadu_si128(reinterpret_cast<const __m128i*>(h + 4)), 0x1B);  // EFGH
+    __m128i s0 = _mm_alignr_epi8(t, s1, 8);  // ABEF
+    s1 = _mm_blend_epi16(s1, t, 0xF0);        // CDGH
+    const __m128i abef = s0, cdgh = s1;
+    __m128i w[4];
+    for (int g = 0; g < 16; ++g) {  // four rounds per group
+        __m128i m;
+        if (g < 4) {
+            m = _mm_shuffle_epi8(_mm_loadu_si128(reinterpret_cast<const __m128i*>(p + 16 * g)), bswap);
+        } else {  // W[t..t+3] from the groups g-4, g-3, g-2, g-1
+            m = _mm_sha256msg1_epu32(w[g & 3], w[(g + 1) & 3]);
+            m = _mm_add_epi32(m, _mm_alignr_epi8(w[(g + 3) & 3], w[(g + 2) & 3], 4));
+            m = _mm_sha256msg2_epu32(m, w[(g + 3) & 3]);
+        }
+        w[g & 3] = m;
+        const __m128i wk = _mm_add_epi32(m, _mm_load_si128(reinterpret_cast<const __m128i*>(kShaK + 4 * g)));
+        s1 = _mm_sha256rnds2_epu32(s1, s0, wk);
+        s0 = _mm_sha256rnds2_epu32(s0, s1, _mm_shuffle_epi32(wk, 0x0E));
+    }
+    s0 = _mm_add_epi32(s0, abef);
+    s1 = _mm_add_epi32(s1, cdgh);
+    t = _mm_shuffle_epi32(s0, 0x1B);      // FEBA
+    s1 = _mm_shuffle_epi32(s1, 0xB1);     // DCHG
+    s0 = _mm_blend_epi16(t, s1, 0xF0);    // DCBA
+    s1 = _mm_alignr_epi8(s1, t, 8);       // HGFE
+    _mm_storeu_si128(reinterpret_cast<__m128i*>(h), s0);
+    _mm_storeu_si128(reinterpret_cast<__m128i*>(h + 4), s1);
+}
+const bool kShaNi = cpu_has_sha_ni();
+#endif
 
 struct Sha256 {
     uint32_t h[8];
@@ -41,6 +101,12 @@ struct Sha256 {
     }
     static inline uint32_t rotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
     void block(const uint8_t* p) {
+#if defined(__x86_64__)
+        if (kShaNi) {
+            sha256_block_ni(h, p);
+            return;
+        }
+#endif
         uint32_t w[64];
         for (int i = 0; i < 16; ++i)
             w[i] = (uint32_t)p[4 * i] << 24 | (uint32_t)p[4 * i + 1] << 16 | (uint32_t)p[4 * i + 2] << 8 | p[4 * i + 3];
@@ -73,14 +139,11 @@ struct Sha256 {
         if (n) { memcpy(buf, p, n); blen = n; }
     }
     void final(uint8_t out[32]) {
-        uint64_t bits = len * 8;
-        uint8_t pad = 0x80;
-        update(&pad, 1);
-        uint8_t z = 0;
-        while (blen != 56) update(&z, 1);
-        uint8_t lb[8];
-        for (int i = 0; i < 8; ++i) lb[i] = (uint8_t)(bits >> (56 - 8 * i));
-        update(lb, 8);
+        const uint64_t bits = len * 8;
+        uint8_t pad[72] = {0x80};  // 0x80, zeros to 56 mod 64, then the bit length
+        const size_t zeros = (blen < 56 ? 56 - blen : 120 - blen) - 1;
+        for (int i = 0; i < 8; ++i) pad[1 + zeros + i] = (uint8_t)(bits >> (56 - 8 * i));
+        update(pad, 1 + zeros + 8);
         for (int i = 0; i < 8; ++i) {
             out[4 * i] = (uint8_t)(h[i] >> 24); out[4 * i + 1] = (uint8_t)(h[i] >> 16);
             out[4 * i + 2] = (uint8_t)(h[i] >> 8); out[4 * i + 3] = (uint8_t)h[i];
