@@ -13,7 +13,7 @@
 //   leaf_hash_kernel : one thread per cell, streams its share through SHA-256
 //                      (S/64 + 1 blocks); the digest of a cell serves both its row
 //                      tree and its column tree.
-//   tree_root_kernel : one workgroup per tree (2W trees), level by level in LDS.
+//   tree_root_kernel : a few trees per wave (2W trees), levels in place in LDS.
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
@@ -81,72 +81,94 @@ __global__ __launch_bounds__(256) void leaf_hash_kernel(const uint8_t* __restric
 }
 
 constexpr uint32_t kMaxLevel1 = 1024;  // W <= 2048
+constexpr uint32_t kTreesPerBlock = 4;  // one wave per tree
 
-// One workgroup per tree: blockIdx.x < W -> row tree blockIdx.x, else column tree;
-// blockIdx.y = square of a batch.  roots: [squares][2][W][32] bytes (big-endian
-// digest bytes, as Tree.Root() returns them).
+// LDS bytes of one tree: level-1 digests (W/2) in place, plus the carried
+// subtrees of the odd levels (16 digests)
+__host__ __device__ constexpr uint32_t tree_lds_words(uint32_t W) { return (W / 2) * 8u + 16u * 8u; }
+
+// TPW trees per WAVE (four waves per 256-thread workgroup): trees
+// (blockIdx.x * 4 + wave) * TPW + u (u < TPW) + first (< W: row tree, else column
+// tree) of square blockIdx.y.  A wave's trees are built level by level together
+// (node (u, j) of a level is lane-slot u * cnt + j), in place in the wave's own LDS
+// (a level's reads all precede its writes: node j reads 2j and 2j + 1 >= j), with
+// no workgroup barrier: the many waves of a CU interleave their dependent SHA
+// rounds, and packing TPW trees keeps the upper levels' lanes busy (the
+// level-by-level workgroup form left most lanes idle behind __syncthreads: 3x
+// slower).  roots: [squares][2][W][32] bytes (big-endian digest bytes, as
+// Tree.Root() returns them).
+template <int TPW>
 __global__ __launch_bounds__(256) void tree_root_kernel(const uint32_t* __restrict__ leaf, uint32_t W,
-                                                        uint8_t* __restrict__ roots, uint32_t first) {
+                                                        uint8_t* __restrict__ roots, uint32_t first, uint32_t count) {
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t t0 = (blockIdx.x * kTreesPerBlock + wv) * TPW;
+    if (t0 >= count) return;  // whole wave (the kernel has no workgroup barrier)
+    const uint32_t nt = count - t0 < (uint32_t)TPW ? count - t0 : (uint32_t)TPW;
     leaf += (uint64_t)blockIdx.y * W * W * 8u;
     roots += (uint64_t)blockIdx.y * 2u * W * 32u;
-    const uint32_t tree = blockIdx.x + first;  // < W: row tree, else column tree
-    // two ping-pong levels of W/2 digests, sized at launch (dynamic LDS): 8 KiB for
-    // W = 256 instead of a fixed 64 KiB, so 8 trees share a CU instead of 2
-    extern __shared__ uint32_t lvl_raw[];
-    const uint32_t half = W / 2;
-    auto lvl = [&](uint32_t buf, uint32_t j) -> uint32_t* { return lvl_raw + ((size_t)buf * half + j) * 8u; };
-    __shared__ uint32_t sub[16][8];
-    const uint32_t axis = tree >= W ? 1u : 0u;
-    const uint32_t idx = tree - axis * W;
+    extern __shared__ uint32_t lds_raw[];
+    uint32_t* const base = lds_raw + (size_t)wv * TPW * tree_lds_words(W);
+    auto lvl = [&](uint32_t u) { return base + (size_t)u * tree_lds_words(W); };
+    auto sub = [&](uint32_t u) { return lvl(u) + (W / 2) * 8u; };
     const uint32_t n = W;
-    auto leaf_at = [&](uint32_t pos, uint32_t (&d)[8]) {
+    auto leaf_at = [&](uint32_t tree, uint32_t pos, uint32_t (&d)[8]) {
+        const uint32_t axis = tree >= W ? 1u : 0u, idx = tree - axis * W;
         const uint64_t cell = axis == 0 ? (uint64_t)idx * W + pos : (uint64_t)pos * W + idx;
         const v4u* s = reinterpret_cast<const v4u*>(leaf + cell * 8u);
         const v4u a = s[0], b = s[1];
         d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w; d[4] = b.x; d[5] = b.y; d[6] = b.z; d[7] = b.w;
     };
-    if ((n & 1u) && threadIdx.x == 0) {  // height-0 subtree: the last leaf
+    auto wave_sync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    if ((n & 1u) && lane < nt) {  // height-0 subtree: the last leaf
         uint32_t d[8];
-        leaf_at(n - 1, d);
+        leaf_at(t0 + first + lane, n - 1, d);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) sub[0][i] = d[i];
+        for (int i = 0; i < 8; ++i) sub(lane)[i] = d[i];
     }
-    uint32_t cur = 0;
     for (uint32_t hgt = 1; (n >> hgt) > 0; ++hgt) {
         const uint32_t cnt = n >> hgt;
-        for (uint32_t j = threadIdx.x; j < cnt; j += 256u) {
+        for (uint32_t v = lane; v < nt * cnt; v += 64u) {
+            const uint32_t u = v / cnt, j = v - u * cnt;
             uint32_t L[8], R[8], o[8];
             if (hgt == 1) {
-                leaf_at(2 * j, L);
-                leaf_at(2 * j + 1, R);
+                leaf_at(t0 + first + u, 2 * j, L);
+                leaf_at(t0 + first + u, 2 * j + 1, R);
             } else {
+                const uint32_t* lv = lvl(u);
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {
-                    L[i] = lvl(cur ^ 1u, 2 * j)[i];
-                    R[i] = lvl(cur ^ 1u, 2 * j + 1)[i];
+                    L[i] = lv[(2 * j) * 8u + i];
+                    R[i] = lv[(2 * j + 1) * 8u + i];
                 }
             }
             node_hash(L, R, o);
+            uint32_t* lv = lvl(u);
 #pragma unroll
-            for (int i = 0; i < 8; ++i) lvl(cur, j)[i] = o[i];
+            for (int i = 0; i < 8; ++i) lv[j * 8u + i] = o[i];
             if (((n >> hgt) & 1u) && j == cnt - 1) {
 #pragma unroll
-                for (int i = 0; i < 8; ++i) sub[hgt][i] = o[i];
+                for (int i = 0; i < 8; ++i) sub(u)[hgt * 8u + i] = o[i];
             }
         }
-        __syncthreads();
-        cur ^= 1u;
+        wave_sync();
     }
-    if (threadIdx.x == 0) {
+    if (lane < nt) {
+        const uint32_t tree = t0 + first + lane;
+        const uint32_t axis = tree >= W ? 1u : 0u, idx = tree - axis * W;
+        const uint32_t* sb = sub(lane);
         uint32_t acc[8];
-        int lo = __builtin_ctz(n);
+        const int lo = __builtin_ctz(n);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) acc[i] = sub[lo][i];
+        for (int i = 0; i < 8; ++i) acc[i] = sb[lo * 8 + i];
         for (int hgt = lo + 1; hgt < 16; ++hgt) {
             if (!((n >> hgt) & 1u)) continue;
             uint32_t L[8], o[8];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) L[i] = sub[hgt][i];
+            for (int i = 0; i < 8; ++i) L[i] = sb[hgt * 8 + i];
             node_hash(L, acc, o);
 #pragma unroll
             for (int i = 0; i < 8; ++i) acc[i] = o[i];
@@ -155,6 +177,26 @@ __global__ __launch_bounds__(256) void tree_root_kernel(const uint32_t* __restri
 #pragma unroll
         for (int i = 0; i < 8; ++i) r[i] = __builtin_bswap32(acc[i]);
     }
+}
+
+// trees per wave: as many as keep four waves' LDS within a third of the CU (so
+// three workgroups share it), at least one
+inline uint32_t trees_per_wave(uint32_t W) {
+    for (uint32_t t = 4; t > 1; t >>= 1)
+        if ((size_t)kTreesPerBlock * t * tree_lds_words(W) * 4u <= 52u * 1024u) return t;
+    return 1;
+}
+hipError_t launch_tree_kernel(const uint32_t* d_leaf, uint32_t W, uint8_t* d_roots, uint32_t first, uint32_t count,
+                              uint32_t squares, hipStream_t st) {
+    const uint32_t tpw = trees_per_wave(W);
+    const uint32_t blocks = (count + kTreesPerBlock * tpw - 1) / (kTreesPerBlock * tpw);
+    const size_t lds = (size_t)kTreesPerBlock * tpw * tree_lds_words(W) * 4u;
+    switch (tpw) {
+        case 4: hipLaunchKernelGGL(tree_root_kernel<4>, dim3(blocks, squares), dim3(256), lds, st, d_leaf, W, d_roots, first, count); break;
+        case 2: hipLaunchKernelGGL(tree_root_kernel<2>, dim3(blocks, squares), dim3(256), lds, st, d_leaf, W, d_roots, first, count); break;
+        default: hipLaunchKernelGGL(tree_root_kernel<1>, dim3(blocks, squares), dim3(256), lds, st, d_leaf, W, d_roots, first, count); break;
+    }
+    return hipGetLastError();
 }
 
 }  // namespace
@@ -170,9 +212,7 @@ hipError_t launch_roots(const uint8_t* d_eds, uint32_t W, uint32_t S, uint32_t s
     hipLaunchKernelGGL(leaf_hash_kernel, dim3((cells + 255) / 256), dim3(256), 0, st, d_eds, cells, S, d_leaf);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(tree_root_kernel, dim3(2 * W, squares), dim3(256), (size_t)2 * (W / 2) * 32, st, d_leaf, W,
-                       d_roots, 0u);
-    return hipGetLastError();
+    return launch_tree_kernel(d_leaf, W, d_roots, 0u, 2 * W, squares, st);
 }
 
 // Pieces of launch_roots for one square, so a caller can hash rows as they become
@@ -187,9 +227,7 @@ hipError_t launch_leaf_hashes(const uint8_t* d_cells, uint32_t cells, uint32_t S
 hipError_t launch_tree_roots(const uint32_t* d_leaf, uint32_t W, uint32_t first, uint32_t count, uint8_t* d_roots,
                              hipStream_t st) {
     if (count == 0) return hipSuccess;
-    hipLaunchKernelGGL(tree_root_kernel, dim3(count, 1), dim3(256), (size_t)2 * (W / 2) * 32, st, d_leaf, W, d_roots,
-                       first);
-    return hipGetLastError();
+    return launch_tree_kernel(d_leaf, W, d_roots, first, count, 1, st);
 }
 
 }  // namespace rsm
