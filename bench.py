@@ -7,8 +7,10 @@ Metric (BASELINE.json): GiB/s of device-resident 2D RS encode, k=128 square,
 A "step" = ComputeExtendedDataSquare's arithmetic (erasureExtendSquare,
 extendeddatasquare.go:154-227) over one batch of `--batch` independent squares
 already resident in HBM (the EDS buffer holds each ODS in its top-left quadrant,
-as the Go EDS aliases its input).  The batch (16 x 32 MiB = 512 MiB by default) is
-larger than the 256 MiB Infinity Cache, so steps do not run out of cache.
+as the Go EDS aliases its input).  c2 default: 128 squares (4 GiB of EDS) per step
+as ONE queue-driven launch (both passes, extend_gf8_bs128q_kernel), steps rotating
+over 3 streams and 3 buffers (12 GiB), so no step finds its squares in the 256 MiB
+Infinity Cache.
 value = ODS bytes encoded per second over all ranks (GiB/s).
 
 N > 1 GPUs (one process per GPU, torch.distributed): every rank encodes its own
@@ -53,8 +55,14 @@ def parse():
                    help="initialise torch.distributed even at N=1 (rehearses the sharded c5 path on one GPU)")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--one-stream", action="store_true", help="GF(2^8): do not alternate steps over two streams")
-    p.add_argument("--streams", type=int, default=2, help="GF(2^8): streams the steps rotate over")
-    p.add_argument("--buffers", type=int, default=2, help="batches (EDS buffers) the steps rotate over")
+    p.add_argument("--streams", type=int, default=0,
+                   help="GF(2^8): streams the steps rotate over (default 3 for the single-launch k=128 "
+                        "schedule, 2 for the two-launch one)")
+    p.add_argument("--buffers", type=int, default=0, help="batches (EDS buffers) the steps rotate over "
+                   "(default: one per stream, at least 2)")
+    p.add_argument("--two-launch", action="store_true",
+                   help="k=128: the round-1 schedule (row pass launch + column pass launch) instead of the "
+                        "single queue-driven launch")
     p.add_argument("--row-grid", type=int, default=224,
                    help="GF(2^8) M=128 with >1 stream: CUs of the row-pass persistent grid (0 = all); the "
                         "remaining CUs run the other stream's column pass (profiles/r01h_grid_ab.txt)")
@@ -492,7 +500,11 @@ def main():
     k, S = wl["k"], wl["S"]
     W = 2 * k
     sq_bytes = W * W * S
-    B = a.batch or max(1, (1 << 30) // sq_bytes)
+    # k = 128: one queue-driven launch per step (both passes; rsm_extend_squares_dev
+    # takes it for batches of >= 2 squares) unless --two-launch
+    single = k == 128 and not a.two_launch and not a.one_stream
+    B = a.batch or (128 if single else max(1, (1 << 30) // sq_bytes))
+    nstreams = 1 if a.one_stream else (a.streams or (3 if single else 2))
     L = R.library()
     ctx = R.device_context(local)
 
@@ -500,7 +512,7 @@ def main():
     # square's top-left quadrant is its ODS (the other quadrants are overwritten).
     # Batches are used in rotation, so a step never finds the previous step's
     # squares in the 256 MiB Infinity Cache (rotate > 512 MiB).
-    bufs = [R.DeviceBuffer(B * sq_bytes, local) for _ in range(max(2, a.buffers))]
+    bufs = [R.DeviceBuffer(B * sq_bytes, local) for _ in range(max(2, a.buffers or nstreams))]
     for i, b in enumerate(bufs):
         b.fill_random(0x52534D543244 + 2 * rank + i)
     R._check(L.rsm_sync(ctx))
@@ -510,11 +522,11 @@ def main():
     # overlaps the next step's row-pass prologue.  (Every stream owns its scratch.)
     streams = [None]
     if not a.one_stream:
-        for _ in range(max(1, a.streams) - 1):
+        for _ in range(max(1, nstreams) - 1):
             s2 = ctypes.c_void_p()
             R._check(L.rsm_stream_create(ctx, ctypes.byref(s2)))
             streams.append(s2)
-    row_grid = a.row_grid if (len(streams) > 1 and 64 < k <= 128) else 0
+    row_grid = a.row_grid if (len(streams) > 1 and 64 < k <= 128 and not single) else 0
     prev_grid = ctypes.c_int()
     R._check(L.rsm_ctx_set_pass_grid(ctx, 0, row_grid, ctypes.byref(prev_grid)))
 
@@ -531,6 +543,12 @@ def main():
         st, b = streams[i % len(streams)], bufs[i % len(bufs)].ptr
         if ev is None:
             R._check(L.rsm_extend_squares_dev(ctx, b, k, S, B, st))
+            return
+        if single:
+            # the production step: ONE launch (both passes), an event either side
+            R._check(L.rsm_event_record(ctx, ev[0], st))
+            R._check(L.rsm_extend_squares_dev(ctx, b, k, S, B, st))
+            R._check(L.rsm_event_record(ctx, ev[2], st))
             return
         # the production step (two launches) with an event at each launch boundary
         R._check(L.rsm_event_record(ctx, ev[0], st))
@@ -550,10 +568,11 @@ def main():
     # correctness gate on one square before timing (the oracle is the checker only)
     if rank == 0:
         import oracle
-        got = buf.download(sq_bytes).reshape(W, W, S)
-        want = oracle.extend_square(got[:k, :k].copy(), nthreads=min(16, os.cpu_count() or 1))
-        if not np.array_equal(got, want):
-            raise SystemExit("bench: GPU EDS differs from oracle -- refusing to report")
+        for j in sorted({0, B - 1}):  # first and last square of the batch
+            got = buf.download(sq_bytes, j * sq_bytes).reshape(W, W, S)
+            want = oracle.extend_square(got[:k, :k].copy(), nthreads=min(16, os.cpu_count() or 1))
+            if not np.array_equal(got, want):
+                raise SystemExit("bench: GPU EDS differs from oracle -- refusing to report")
 
     def barrier():
         if dist is not None:
@@ -577,19 +596,33 @@ def main():
     rows, cols, spans = [], [], []
     ms = ctypes.c_float()
     for ev in events:
-        R._check(L.rsm_event_elapsed_ms(ev[0], ev[1], ctypes.byref(ms)))
-        rows.append(ms.value / 1e3)
-        R._check(L.rsm_event_elapsed_ms(ev[1], ev[2], ctypes.byref(ms)))
-        cols.append(ms.value / 1e3)
+        if not single:
+            R._check(L.rsm_event_elapsed_ms(ev[0], ev[1], ctypes.byref(ms)))
+            rows.append(ms.value / 1e3)
+            R._check(L.rsm_event_elapsed_ms(ev[1], ev[2], ctypes.byref(ms)))
+            cols.append(ms.value / 1e3)
         R._check(L.rsm_event_elapsed_ms(ev[0], ev[2], ctypes.byref(ms)))
         spans.append(ms.value / 1e3)
         for e in ev:
             L.rsm_event_destroy(e)
-    t_row, t_col = sum(rows) / len(rows), sum(cols) / len(cols)
+    t_row = sum(rows) / len(rows) if rows else 0.0
+    t_col = sum(cols) / len(cols) if cols else 0.0
+    t_span = sum(spans) / len(spans)
     # the same launches alone on one stream (no overlap with another step)
     r_ms, c_ms, s_ms = ctypes.c_float(), ctypes.c_float(), ctypes.c_float()
     R._check(L.rsm_time_extend(ctx, bufs[0].ptr, k, S, B, 10, ctypes.byref(r_ms), ctypes.byref(c_ms),
                                ctypes.byref(s_ms)))
+    iso_single = None
+    if single:
+        e0, e1 = new_event(), new_event()
+        R._check(L.rsm_event_record(ctx, e0, None))
+        for _ in range(5):
+            R._check(L.rsm_extend_squares_dev(ctx, bufs[0].ptr, k, S, B, None))
+        R._check(L.rsm_event_record(ctx, e1, None))
+        R._check(L.rsm_event_elapsed_ms(e0, e1, ctypes.byref(ms)))
+        iso_single = ms.value / 5 / 1e3
+        for e in (e0, e1):
+            L.rsm_event_destroy(e)
     R._check(L.rsm_ctx_set_pass_grid(ctx, 0, prev_grid.value, None))
 
     ods_bytes = k * k * S
@@ -603,7 +636,10 @@ def main():
     kname = ("encode_gf8_bs128u_kernel" if bitsliced else "encode_gf8_kernel" if k <= 64
              else "enc16_kernel (GF(2^16) single pass)")
     col_dom = t_col >= t_row
-    dominant = ((kname + " column pass", col_bytes, t_col) if col_dom else (kname + " row pass", row_bytes, t_row))
+    if single:
+        dominant = ("extend_gf8_bs128q_kernel (one launch: both passes)", algo_step, t_span)
+    else:
+        dominant = ((kname + " column pass", col_bytes, t_col) if col_dom else (kname + " row pass", row_bytes, t_row))
     ach = dominant[1] / dominant[2] / 1e9
     # HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC
     # passes (scripts/pmc_summary.py; FETCH_SIZE x2 gfx950 correction), matched by
@@ -612,8 +648,12 @@ def main():
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_latest.json")
     if bitsliced and os.path.exists(pmc_path):
-        want = "encode_gf8_bs128u_kernel<%d, %d>" % ((184, 1) if col_dom else (104, 0))
-        sets = (W if col_dom else k) * B * S // 2048
+        if single:
+            want = "extend_gf8_bs128q_kernel<104>"
+            sets = 3 * k * B * S // 2048
+        else:
+            want = "encode_gf8_bs128u_kernel<%d, %d>" % ((184, 1) if col_dom else (104, 0))
+            sets = (W if col_dom else k) * B * S // 2048
         grid_threads = min(sets, 256) * 512  # persistent grid: one 512-thread workgroup per CU
         for row in json.load(open(pmc_path)).get("launches", []):
             if want in row["kernel"] and row["grid_threads"] == grid_threads:
@@ -635,7 +675,8 @@ def main():
         "config": {"workload": f"{a.workload}: {wl['desc']}", "k": k, "share_size": S,
                    "squares_per_step": B, "eds_bytes_per_step": B * sq_bytes, "buffers": len(bufs),
                    "parallelism": f"independent squares per GPU x{world}",
-                   "schedule": "two-launch", "streams": len(streams), "row_pass_grid": row_grid or None},
+                   "schedule": "single-launch queue (both passes)" if single else "two-launch",
+                   "streams": len(streams), "row_pass_grid": row_grid or None},
         "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel": dominant[0], "avg_launch_us": us(dominant[2]),
@@ -644,14 +685,16 @@ def main():
         "step_roofline": {"algorithmic_bytes": algo_step,
                           "achieved": round(algo_step / (elapsed / a.steps) / 1e9, 1),
                           "frac": round(algo_step / (elapsed / a.steps) / 1e9 / HBM_PEAK_GBS, 4),
-                          "row_pass_us": {"mean": us(t_row), "p10": us(pct(rows, .1)), "p50": us(pct(rows, .5)),
-                                          "p90": us(pct(rows, .9))},
-                          "col_pass_us": {"mean": us(t_col), "p10": us(pct(cols, .1)), "p50": us(pct(cols, .5)),
-                                          "p90": us(pct(cols, .9))},
-                          "step_span_us": {"p10": us(pct(spans, .1)), "p50": us(pct(spans, .5)),
+                          **({} if single else {
+                              "row_pass_us": {"mean": us(t_row), "p10": us(pct(rows, .1)), "p50": us(pct(rows, .5)),
+                                              "p90": us(pct(rows, .9))},
+                              "col_pass_us": {"mean": us(t_col), "p10": us(pct(cols, .1)), "p50": us(pct(cols, .5)),
+                                              "p90": us(pct(cols, .9))}}),
+                          "step_span_us": {"mean": us(t_span), "p10": us(pct(spans, .1)), "p50": us(pct(spans, .5)),
                                            "p90": us(pct(spans, .9))},
-                          "isolated_one_stream_us": {"row": round(r_ms.value * 1e3, 2),
-                                                     "col": round(c_ms.value * 1e3, 2)}},
+                          "isolated_one_stream_us": dict(
+                              ({"single_launch": us(iso_single)} if single else {}),
+                              two_launch_row=round(r_ms.value * 1e3, 2), two_launch_col=round(c_ms.value * 1e3, 2))},
     }
     if rank == 0 and world == 1:
         model, ncpu = cpu_info()

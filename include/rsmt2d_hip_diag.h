@@ -24,10 +24,14 @@ int rsm_diag_set_bs_mode(int mode, int rev_col, int xcd);
  * to every other launch). */
 int rsm_diag_set_bs_row_mode(int mode);
 /* Both passes of `count` in-place k = 128 squares in ONE persistent launch
- * (encode_gf8_bs128f_kernel).  Synchronous; fails if the kernel's bounded wait
- * timed out (its output is then invalid). */
-int rsm_diag_extend_fused(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size, uint32_t count, uint32_t lag,
+ * (extend_gf8_bs128q_kernel: row and Q0-column sets from one queue, Q1-column sets
+ * from a ready list; `delay` squares of row sets lead the Q0-column sets).
+ * Asynchronous on `stream`. */
+int rsm_diag_extend_fused(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size, uint32_t count, uint32_t delay,
                           void* stream);
+/* Reads and clears the stuck-wait word of the queue launches on `stream`:
+ * RSM_EDEVICE if one timed out since the last check (its output is invalid). */
+int rsm_diag_queue_check(rsm_ctx* ctx, void* stream);
 /* ONE launch running the row pass of the squares at d_rows_eds and the column pass
  * of the squares at d_cols_eds (encode_gf8_bs128p_kernel); either may be NULL. */
 int rsm_diag_extend_pipeline_dev(rsm_ctx* ctx, void* d_rows_eds, void* d_cols_eds, uint32_t k, uint32_t share_size,

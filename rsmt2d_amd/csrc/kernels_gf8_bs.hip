@@ -349,246 +349,455 @@ __global__ __launch_bounds__(512, 1) void encode_gf8_bs128u_kernel(CodewordSet c
 }
 
 
-#ifdef RSM_DIAG
 // ---------------------------------------------------------------------------
-// Fused two-pass extension (FusedPlan, rsm_kernels.hpp).  Items are handed out by
-// one device-scope queue head in this order: the row sets of squares 0..lag-1,
-// then per square s: the row sets of s + lag followed by the column sets of s,
-// then the remaining column sets.  A column set of square s needs all rn row sets
-// of s (its Q1 inputs).  Deadlock freedom: a workgroup waits only for items that
-// precede its own in queue order and only while it holds no unfinished item, so
-// the earliest unfinished item always progresses, whatever the residency.
-// Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility): producers store
-// `sc1`, every wave waits for its stores, a barrier, then ONE lane adds to the
-// square's counter (agent scope); the consumer polls with an `sc1` load, takes an
-// agent acquire, and every wave loads after a barrier that follows it.  Waits are
-// bounded: a stuck counter sets ctr[2] and lets the launch drain (wrong output,
-// never a hung GPU).
-__device__ __forceinline__ void fused_item(const FusedPlan& p, uint32_t u, uint32_t& row, uint32_t& set,
-                                           uint32_t& sq) {
-    const uint32_t pro = p.lag * p.rn, blk = p.rn + p.cn, mid = (p.count - p.lag) * blk;
-    if (u < pro) {
-        row = 1u; set = u; sq = u / p.rn;
-    } else if (u - pro < mid) {
-        const uint32_t v = u - pro, b = v / blk, o = v - b * blk;
-        if (o < p.rn) { row = 1u; sq = p.lag + b; set = sq * p.rn + o; }
-        else { row = 0u; sq = b; set = b * p.cn + (o - p.rn); }
-    } else {
-        row = 0u; set = (p.count - p.lag) * p.cn + (u - pro - mid); sq = set / p.cn;
-    }
-}
-
+// Queue-driven single-launch extension (QueuePlan, rsm_kernels.hpp): the
+// production schedule for batches of k = 128 squares.
+//
+// Both passes of `count` squares in ONE persistent launch, so the column sets
+// re-read Q0 and Q1 while they are still in the 256 MiB Infinity Cache instead of
+// from HBM (the two-launch schedule moves 6k^2S per square, this one 4k^2S plus
+// whatever misses).  A square's sets are of three kinds:
+//   row sets      (rn): Q0 rows -> Q1 rows
+//   Q0-col sets   (rn): Q0 columns -> Q2 columns        (no dependency)
+//   Q1-col sets   (rn): Q1 columns -> Q3 columns        (need all rn row sets)
+// Row and Q0-col sets form the MAIN sequence (one queue head): row sets of
+// square s interleaved 1:1 with the Q0-col sets of square s - delay/rn (so both
+// read a square's Q0 within a set or two of each other, and the last squares'
+// Q0-col sets fill the tail).  A Q1-col set is never dequeued before it is
+// ready: the workgroup whose row set completes a square (the last add on the
+// square's counter) appends the square to a ready list, and Q1-col sets are
+// taken from that list (second head) in preference to main items.
+//
+// Deadlock freedom: a workgroup waits only when the main sequence is exhausted,
+// after publishing its own stored row set; every remaining row set is then held
+// by a workgroup that finishes it without waiting, so every claimed Q1-col set
+// becomes ready.  A claimed Q1-col set that is not ready yet (two workgroups raced
+// for the last ready one) is kept in reserve while the workgroup takes main items.
+//
+// Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility): row sets store Q1
+// `sc1`; every wave waits for its stores (vmcnt), a barrier, then ONE lane adds to
+// the square's counter (agent scope); a consumer sees the square in the ready
+// list through agent-scope loads, takes an agent acquire, and every wave loads
+// after a barrier that follows it.  Waits are bounded: a stuck wait sets the
+// error word and lets the launch drain (invalid output, never a hung GPU).
+constexpr uint32_t kQMain = 0, kQHead1 = 32, kQReady = 64, kQRes = 96, kQErr = 128, kQExit = 160, kQLeft = 192,
+                   kQRows = 224;
+constexpr uint32_t kNone = 0xFFFFFFFFu, kQ1 = 0x80000000u, kQExitCheck = 0xFFFFFFFEu;
 constexpr uint32_t kSpinLimit = 1u << 20;  // polls (~1 s) before a wait is declared stuck
 
+__device__ __forceinline__ uint32_t q_add(uint32_t* w) {
+    return __hip_atomic_fetch_add(w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t q_load(uint32_t* w) {
+    return __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t q_sub(uint32_t* w) {
+    return __hip_atomic_fetch_sub(w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void q_store(uint32_t* w, uint32_t v) {
+    __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// item word -> (row set?, set index in p.rows / p.cols); sq1 is a Q1 item's square
+__device__ __forceinline__ void q_item(const QueuePlan& p, uint32_t it, uint32_t sq1, uint32_t& row, uint32_t& set) {
+    if (it & kQ1) {
+        row = 0u;
+        set = sq1 * p.cn + p.rn + (it & ~kQ1) % p.rn;
+        return;
+    }
+    const uint32_t N = p.count * p.rn, D = p.delay;
+    uint32_t c;
+    if (it < D) {
+        row = 1u;
+        set = it;
+        return;
+    }
+    const uint32_t v = it - D;
+    if (v < 2u * (N - D)) {
+        const uint32_t pi = v >> 1;
+        if (!(v & 1u)) {
+            row = 1u;
+            set = D + pi;
+            return;
+        }
+        c = pi;
+    } else {
+        c = (N - D) + (v - 2u * (N - D));
+    }
+    row = 0u;
+    set = (c / p.rn) * p.cn + c % p.rn;
+}
+
+// Thread 0's view of the queue.
+struct QClaim {
+    uint32_t res = kNone;   // a claimed Q1 item that was not ready yet
+    uint32_t main_done = 0;
+    uint32_t rc = 0, qh = 0;  // hints: ready squares, Q1 head (loaded half a set earlier)
+};
+
+// the square of Q1 item q when it is ready, else kNone
+__device__ __forceinline__ uint32_t q_ready(const QueuePlan& p, uint32_t q) {
+    const uint32_t s1 = q_load(&p.ctr[kQRows + p.count + q / p.rn]);
+    return s1 ? s1 - 1u : kNone;
+}
+
+// This set's claim (its result is consumed half a set later).  A Q1 item is
+// claimed only while the (stale) hint shows more than `margin` unclaimed ready
+// ones, so a claim rarely overtakes the ready list; at the end of the main
+// sequence any remaining Q1 item is claimed (and waited for).
+__device__ __forceinline__ uint32_t q_claim(const QueuePlan& p, const QClaim& c) {
+    if (c.res != kNone) return c.res;
+    if (c.qh + p.margin < c.rc * p.rn) return kQ1 | q_add(&p.ctr[kQHead1]);
+    if (!c.main_done) return q_add(&p.ctr[kQMain]);
+    if (c.qh < c.rc * p.rn) return kQ1 | q_add(&p.ctr[kQHead1]);
+    return c.qh < p.nq1 ? kQExitCheck : kNone;
+}
+
+// Main sequence exhausted and (as far as thread 0 knows) no ready Q1 item: leave
+// the launch if the workgroups that stay still outnumber the unclaimed Q1 items
+// (each of them takes one before it may leave: the count of live workgroups never
+// drops below the unclaimed items, so none is stranded, and the CUs of the others
+// go to the next launch on another stream); otherwise claim a Q1 item (it may have
+// to be waited for).  Returns kNone (leave) or the claimed Q1 item.
+__device__ __forceinline__ uint32_t q_leave_or_claim(const QueuePlan& p) {
+    const uint32_t e = q_add(&p.ctr[kQLeft]);
+    uint32_t qh = q_load(&p.ctr[kQHead1]);
+    qh = qh < p.nq1 ? qh : p.nq1;
+    if (gridDim.x - e - 1u >= p.nq1 - qh) return kNone;
+    q_sub(&p.ctr[kQLeft]);
+    return kQ1 | q_add(&p.ctr[kQHead1]);
+}
+
+// Synchronous take (prologue): a main item, else a Q1 item, waited for only when
+// `wait` (the workgroup then holds no other item); otherwise rdy = 0 for a Q1 item
+// that is not ready (the slow path waits for it after the first set).
+__device__ __forceinline__ uint32_t q_wait(const QueuePlan& p, uint32_t it);
+__device__ __forceinline__ uint32_t q_take(const QueuePlan& p, QClaim& c, bool wait, uint32_t& sq, uint32_t& rdy) {
+    sq = 0u;
+    rdy = 1u;
+    if (!c.main_done) {
+        const uint32_t u = q_add(&p.ctr[kQMain]);
+        if (u < p.nmain) return u;
+        c.main_done = 1u;
+    }
+    const uint32_t it = q_leave_or_claim(p);
+    if (it == kNone || (it & ~kQ1) >= p.nq1) return kNone;
+    const uint32_t q = it & ~kQ1;
+    if (wait) {
+        sq = q_wait(p, kQ1 | q);
+    } else {
+        sq = q_ready(p, q);
+        if (sq == kNone) {
+            sq = 0u;
+            rdy = 0u;
+        } else {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        }
+    }
+    return kQ1 | q;
+}
+
+// Bounded wait for Q1 item `it`; returns its square.
+__device__ __forceinline__ uint32_t q_wait(const QueuePlan& p, uint32_t it) {
+    uint32_t s = kNone;
+    for (uint32_t n = 0; (s = q_ready(p, it & ~kQ1)) == kNone; ++n) {
+        if (n >= kSpinLimit) {
+            q_store(&p.ctr[kQErr], 1u);
+            s = 0u;
+            break;
+        }
+        __builtin_amdgcn_s_sleep(4);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    return s;
+}
+
+// The last row set of square sq is stored (old = rn - 1 from its counter add):
+// append the square to the ready list.
+__device__ __forceinline__ void q_publish(const QueuePlan& p, uint32_t sq) {
+    const uint32_t slot = q_add(&p.ctr[kQRes]);
+    q_store(&p.ctr[kQRows + p.count + slot], sq + 1u);
+    q_add(&p.ctr[kQReady]);
+}
+__device__ __forceinline__ void q_signal(const QueuePlan& p, uint32_t sq) {
+    if (q_add(&p.ctr[kQRows + sq]) == p.rn - 1u) q_publish(p, sq);
+}
+
 template <int MODE>
-__device__ __forceinline__ void bs_fused_wave(const FusedPlan& p, uint32_t* lds, uint32_t lds_base, uint32_t A) {
-    constexpr bool ADDTID = (MODE & 8) != 0, NTL = (MODE & 32) != 0;
+__device__ __forceinline__ void bs_queue_wave(const QueuePlan& p, uint32_t* lds, uint32_t lds_base, uint32_t A) {
+    // Where the direct half of the next set's loads is issued: MODE 64 right after
+    // the first exchange, 128 the same for row sets only (column sets after the large
+    // layers), 256 with the LDS-DMA half at the top of the set; default after the
+    // large layers.  MODE 512: Q0 read non-temporal by both its readers (A/B).
+    constexpr bool ADDTID = (MODE & 8) != 0, ARITH = !(MODE & 2), EARLY = (MODE & 256) != 0,
+                   NTQ0 = (MODE & 512) != 0;
+    constexpr int DPOS = EARLY ? 0 : (MODE & 64) ? 1 : (MODE & 128) ? 3 : 2;
+    const bool MEM = !(MODE & 4) || p.rows.S == 1;  // runtime-false in mode 4 (keeps the code alive)
     const uint32_t lane = threadIdx.x & 63u;
     const bool t0 = threadIdx.x == 0;
     const uint32_t dread = lds_base + kXchBytes + A * 16384u + lane * 16u;
     const uint32_t s_small = __builtin_amdgcn_readfirstlane(lds_base + 4096u * A);
     const uint32_t s_large = __builtin_amdgcn_readfirstlane(lds_base + 256u * A);
     const uint32_t e_small = s_small + lane * 4u, e_large = s_large + lane * 4u;
-    uint32_t* const ctr = p.ctr;
     uint32_t X[16][8];
     uint32_t P[16 - kPre][8];
+    QClaim qc;
 
-    auto dequeue = [&]() { return __hip_atomic_fetch_add(&ctr[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-    auto poll = [&](uint32_t sq) { return __hip_atomic_load(&ctr[3 + sq], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-    auto signal = [&](uint32_t sq) {
-        __hip_atomic_fetch_add(&ctr[3 + sq], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    };
-    // thread 0: wait until square sq's row sets are all stored, then acquire
-    auto wait_rows = [&](uint32_t sq) {
-        for (uint32_t n = 0; poll(sq) < p.rn; ++n) {
-            if (n >= kSpinLimit) {
-                __hip_atomic_store(&ctr[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(4);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    };
-    // row sets read Q0 with the default policy (it stays in the Infinity Cache for
-    // the column sets); column sets read once, non-temporal (MODE 32)
-    auto issue = [&](uint32_t row, const SetAddr& a) {
-        if (row) {
-            issue_dma_rt<false>(p.rows, a, lds_base, A);
-            issue_direct_rt<false>(p.rows, a, A, P);
-        } else {
-            issue_dma_rt<NTL>(p.cols, a, lds_base, A);
-            issue_direct_rt<NTL>(p.cols, a, A, P);
-        }
-    };
     auto addr = [&](uint32_t row, uint32_t set) { return set_addr(row ? p.rows : p.cols, set, lane); };
+    // row sets and Q0-col sets read Q0 with the default policy (the other kind
+    // re-reads it from the Infinity Cache); Q1-col sets are the last readers of Q1
+    auto issue_dma = [&](uint32_t row, uint32_t q1, const SetAddr& a) {
+        if (!MEM) return;
+        if (row) issue_dma_rt<NTQ0>(p.rows, a, lds_base, A);
+        else if (q1) issue_dma_rt<true>(p.cols, a, lds_base, A);
+        else issue_dma_rt<NTQ0>(p.cols, a, lds_base, A);
+    };
+    auto issue_direct = [&](uint32_t row, uint32_t q1, const SetAddr& a) {
+        if (!MEM) return;
+        if (row) issue_direct_rt<NTQ0>(p.rows, a, A, P);
+        else if (q1) issue_direct_rt<true>(p.cols, a, A, P);
+        else issue_direct_rt<NTQ0>(p.cols, a, A, P);
+    };
 
-    // prologue: first two items, first one loaded synchronously
+    // prologue: the first two items, taken synchronously; the first one loaded
     if (t0) {
-        const uint32_t c = dequeue(), n = dequeue();
-        lds[0] = c;
-        lds[1] = n;
+        uint32_t sq0 = 0, sq1 = 0, r0 = 1, r1 = 1;
+        const uint32_t c0 = q_take(p, qc, true, sq0, r0);
+        const uint32_t c1 = c0 == kNone ? kNone : q_take(p, qc, false, sq1, r1);
+        lds[0] = c0;
+        lds[1] = sq0;
+        lds[4] = c1;
+        lds[5] = sq1;
+        lds[6] = r1;
+        qc.rc = q_load(&p.ctr[kQReady]);
+        qc.qh = q_load(&p.ctr[kQHead1]);
     }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     uint32_t cur = __builtin_amdgcn_readfirstlane(lds[0]);
-    uint32_t nxt = __builtin_amdgcn_readfirstlane(lds[1]);
+    const uint32_t csq = __builtin_amdgcn_readfirstlane(lds[1]);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    uint32_t crow = 0, cset = 0, csq = 0;
-    uint32_t pend = 0xFFFFFFFFu;  // square of a stored-but-unsignalled row set
-    if (cur < p.total) {
-        fused_item(p, cur, crow, cset, csq);
-        if (!crow && t0) wait_rows(csq);
-        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-        issue(crow, addr(crow, cset));
+    uint32_t pend = kNone;  // square of a stored-but-unsignalled row set
+    if (cur != kNone) {
+        uint32_t crow, cset;
+        q_item(p, cur, csq, crow, cset);
+        {
+            const SetAddr a = addr(crow, cset);
+            issue_dma(crow, cur & kQ1, a);
+            issue_direct(crow, cur & kQ1, a);
+        }
         if (t0) {
-            uint32_t r = 1u, nr = 0, ns = 0, nq = 0;
-            if (nxt < p.total) {
-                fused_item(p, nxt, nr, ns, nq);
-                if (!nr) {
-                    r = poll(nq) >= p.rn;
-                    if (r) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                }
-            }
-            lds[0] = nxt;
-            lds[2] = r;
+            lds[0] = lds[4];
+            lds[1] = lds[5];
+            lds[2] = lds[6];
         }
         __builtin_amdgcn_s_waitcnt(0x0F70);
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    }
-    uint32_t path = 1u, iter = 0u;
-    for (; cur < p.total;) {
-        if (p.trace && t0) p.trace[cur] = (blockIdx.x << 8) | ((iter & 63u) << 2) | path;
-        {
-            v4u g[8];
-            bs8::sfor<2>([&](auto Hh) {
-                constexpr int hh = decltype(Hh)::value;
-                ds_r16x8<8192 * hh, 1024>(dread, g);
-                bs8::sfor<4>([&](auto J) {
-                    constexpr int j = 4 * hh + decltype(J)::value;
-                    const v4u x = g[2 * (j & 3)], y = g[2 * (j & 3) + 1];
-                    X[j][0] = x.x; X[j][1] = x.y; X[j][2] = x.z; X[j][3] = x.w;
-                    X[j][4] = y.x; X[j][5] = y.y; X[j][6] = y.z; X[j][7] = y.w;
+        // thread 0, carried across the loop: the pending claim, the next-next item
+        // (nn, its square, state 0 ready / 1 readiness load rv pending), the pending
+        // row-counter add of a signalled row set
+        uint32_t cand = kNone, nn = kNone, nnsq = 0, nst = 0, rv = 0, sig = 0, sig_sq = kNone;
+        for (;;) {
+            {
+                v4u g[8];
+                bs8::sfor<2>([&](auto Hh) {
+                    constexpr int hh = decltype(Hh)::value;
+                    ds_r16x8<8192 * hh, 1024>(dread, g);
+                    bs8::sfor<4>([&](auto J) {
+                        constexpr int j = 4 * hh + decltype(J)::value;
+                        const v4u x = g[2 * (j & 3)], y = g[2 * (j & 3) + 1];
+                        X[j][0] = x.x; X[j][1] = x.y; X[j][2] = x.z; X[j][3] = x.w;
+                        X[j][4] = y.x; X[j][5] = y.y; X[j][6] = y.z; X[j][7] = y.w;
+                    });
                 });
-            });
-        }
-        bs8::sfor<16 - kPre>([&](auto J) {
-            constexpr int j = decltype(J)::value;
-            bs8::sfor<8>([&](auto I) { X[kPre + j][decltype(I)::value] = P[j][decltype(I)::value]; });
-        });
-        // the slot (E words 0..2) holds the next item and its readiness; everyone reads
-        // it before the first exchange overwrites E
-        nxt = __builtin_amdgcn_readfirstlane(lds[0]);
-        const uint32_t rdy = __builtin_amdgcn_readfirstlane(lds[2]);
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        const bool more = nxt < p.total;
-        uint32_t nrow = 0, nset = 0, nsq = 0;
-        if (more) fused_item(p, nxt, nrow, nset, nsq);
-        const bool pre = more && rdy && !(p.flags & 1u);
-        if (pre) issue(nrow, addr(nrow, nset));
-        uint32_t nn = 0;
-        if (t0) nn = dequeue();
-
-        bs8::sfor<16>([&](auto J) { bs8::transpose8_dev(X[decltype(J)::value]); });
-        bs8::small_ifft_all(X, A);
-        bs8::sfor<8>([&](auto Pp) { xch_to_large<decltype(Pp)::value, ADDTID>(X, e_small, s_small, e_large); });
-        bs8::large_ifft_fft(X);
-        bs8::sfor<8>([&](auto Pp) { xch_to_small<decltype(Pp)::value, ADDTID>(X, e_large, s_large, e_small); });
-
-        // the dequeued id is first touched here: keep the compiler from hoisting its use
-        // (and the vmcnt(0) wait for it, which would drain this wave's prefetch loads)
-        // to the top of the set
-        asm volatile("" : "+v"(nn));
-        // thread 0: readiness of the item after next (poll now, read after the FFT)
-        uint32_t pv = 0, nnr = 1, nnq = 0;
-        if (t0 && nn < p.total) {
-            uint32_t ns2 = 0;
-            fused_item(p, nn, nnr, ns2, nnq);
-            if (!nnr) pv = poll(nnq);
-        }
-        bs8::small_fft_all(X, A);
-
-        // signal the previous row set (its stores were issued one set ago)
-        if (pend != 0xFFFFFFFFu) {
-            if (pre) asm volatile("s_waitcnt vmcnt(32)\n\ts_barrier" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-            if (t0) signal(pend);
-            pend = 0xFFFFFFFFu;
-        }
-        if (t0) {
-            uint32_t r = 1u;
-            if (nn < p.total && !nnr) {
-                r = pv >= p.rn;
-                if (r) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             }
-            lds[0] = nn;
-            lds[2] = r;
-        }
-        {
-            const SetAddr a = addr(crow, cset);
-            const __amdgpu_buffer_rsrc_t ro = as_rsrc(a.ro);
-            const uint32_t k = p.rows.k;
-            const uint32_t oo = (uint32_t)(crow ? p.rows.out_offset : p.cols.out_offset);
-            const uint32_t es = (uint32_t)(crow ? p.rows.elem_stride : p.cols.elem_stride);
-            bs8::sfor<16>([&](auto J) {
+            bs8::sfor<16 - kPre>([&](auto J) {
                 constexpr int j = decltype(J)::value;
-                bs8::transpose8_dev(X[j]);
-                const uint32_t so = sym_off(16u * A + j, k, oo, es);
-                v4u x, y;
-                x.x = X[j][0]; x.y = X[j][1]; x.z = X[j][2]; x.w = X[j][3];
-                y.x = X[j][4]; y.y = X[j][5]; y.z = X[j][6]; y.w = X[j][7];
-                __builtin_amdgcn_raw_buffer_store_b128(x, ro, a.off[0], so, 16);  // sc1
-                __builtin_amdgcn_raw_buffer_store_b128(y, ro, a.off[1], so, 16);
-                asm volatile("s_nop 2" ::: "memory");  // store-data hazard, see bs_uni_wave
+                bs8::sfor<8>([&](auto I) { X[kPre + j][decltype(I)::value] = P[j][decltype(I)::value]; });
             });
-        }
-        if (crow) pend = csq;
-        if (!more) break;
-        if (!pre) {
-            // slow path: publish our own row set first (the next item may need it),
-            // then wait for the next item's rows and load it synchronously
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-            if (t0) {
-                if (pend != 0xFFFFFFFFu) signal(pend);
-                if (!nrow) wait_rows(nsq);
+            // the slot (E words 0..2) holds the next item; everyone reads it before the
+            // first exchange overwrites E
+            const uint32_t nxt = __builtin_amdgcn_readfirstlane(lds[0]);
+            uint32_t nsq = __builtin_amdgcn_readfirstlane(lds[1]);
+            const uint32_t rdy = __builtin_amdgcn_readfirstlane(lds[2]);
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            const bool more = nxt != kNone;
+            const bool pre = more && rdy;
+            uint32_t nrow = 0, nset = 0;
+            SetAddr an{};
+            if (pre) {
+                q_item(p, nxt, nsq, nrow, nset);
+                an = addr(nrow, nset);
+                issue_dma(nrow, nxt & kQ1, an);
+                if constexpr (DPOS == 0) issue_direct(nrow, nxt & kQ1, an);
             }
-            pend = 0xFFFFFFFFu;
-            asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-            issue(nrow, addr(nrow, nset));
-            __builtin_amdgcn_s_waitcnt(0x0F70);
-            asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-            path = 3u;
-        } else {
-            asm volatile("s_waitcnt vmcnt(32) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-            path = 2u;
+            // direct loads issued since the previous set's stores, at the publish point
+            const bool dearly = pre && (DPOS <= 1 || (DPOS == 3 && nrow));
+            // no claim in a workgroup's last set (nothing would take the item)
+            if (t0) cand = more ? q_claim(p, qc) : kNone;
+
+            if constexpr (ARITH) {
+                bs8::sfor<16>([&](auto J) { bs8::transpose8_dev(X[decltype(J)::value]); });
+                bs8::small_ifft_all(X, A);
+            }
+            bs8::sfor<8>([&](auto Pp) { xch_to_large<decltype(Pp)::value, ADDTID>(X, e_small, s_small, e_large); });
+            if constexpr (DPOS == 1 || DPOS == 3)
+                if (pre && (DPOS == 1 || nrow)) issue_direct(nrow, nxt & kQ1, an);
+            if constexpr (ARITH) bs8::large_ifft_fft(X);
+
+            // publish the row set stored at the end of the previous set (its stores
+            // were issued before this set's loads: wait for them only); the counter
+            // add's result is consumed after the small layers
+            if (pend != kNone) {
+                // ops issued since those stores: this set's LDS-DMA loads (16) and, with
+                // LATE, its direct loads (16)
+                if (dearly) asm volatile("s_waitcnt vmcnt(32)\n\ts_barrier" ::: "memory");
+                else if (pre) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+                if (t0) {
+                    sig = q_add(&p.ctr[kQRows + pend]);
+                    sig_sq = pend;
+                }
+                pend = kNone;
+            }
+            // the claim (issued at the top of the set) becomes the next-next item; a Q1
+            // item's readiness is loaded now and read after the small layers
+            asm volatile("" : "+v"(cand));
+            if (t0) {
+                nnsq = 0u;
+                nst = 0u;
+                uint32_t it = cand;
+                if (it != kNone && it != kQExitCheck && !(it & kQ1) && it >= p.nmain) {
+                    qc.main_done = 1u;
+                    it = qc.res != kNone ? qc.res : kQExitCheck;
+                }
+                if (it == kQExitCheck) it = q_leave_or_claim(p);
+                if (it == kNone || ((it & kQ1) && (it & ~kQ1) >= p.nq1)) {
+                    nn = kNone;
+                } else {
+                    nn = it;
+                    if (it & kQ1) {
+                        nst = 1u;
+                        rv = q_load(&p.ctr[kQRows + p.count + (it & ~kQ1) / p.rn]);
+                    }
+                }
+                qc.rc = q_load(&p.ctr[kQReady]);
+                qc.qh = q_load(&p.ctr[kQHead1]);
+            }
+            if (pre && (DPOS == 2 || (DPOS == 3 && !nrow))) issue_direct(nrow, nxt & kQ1, an);
+            bs8::sfor<8>([&](auto Pp) { xch_to_small<decltype(Pp)::value, ADDTID>(X, e_large, s_large, e_small); });
+            if constexpr (ARITH) bs8::small_fft_all(X, A);
+            if (t0) {
+                asm volatile("" : "+v"(sig), "+v"(rv));
+                if (sig_sq != kNone) {
+                    if (sig == p.rn - 1u) q_publish(p, sig_sq);
+                    sig_sq = kNone;
+                }
+                uint32_t r = 1u;
+                if (nst == 1u) {
+                    if (rv != 0u) {
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                        nnsq = rv - 1u;
+                        if (nn == qc.res) qc.res = kNone;
+                    } else {
+                        // not published yet: keep it in reserve and take a main item
+                        qc.res = nn;
+                        uint32_t u = p.nmain;
+                        if (!qc.main_done) u = q_add(&p.ctr[kQMain]);
+                        if (u < p.nmain) {
+                            nn = u;
+                        } else {
+                            qc.main_done = 1u;
+                            qc.res = kNone;
+                            r = 0u;  // main sequence exhausted: the slow path waits for it
+                        }
+                    }
+                }
+                lds[0] = nn;
+                lds[1] = nnsq;
+                lds[2] = r;
+            }
+            {
+                const SetAddr a = addr(crow, cset);
+                const __amdgpu_buffer_rsrc_t ro = as_rsrc(a.ro);
+                const uint32_t k = p.rows.k;
+                const uint32_t oo = (uint32_t)(crow ? p.rows.out_offset : p.cols.out_offset);
+                const uint32_t es = (uint32_t)(crow ? p.rows.elem_stride : p.cols.elem_stride);
+                // Q1 write-through (sc1: another workgroup reads it soon); Q2/Q3 non-temporal
+                const bool rs = crow != 0;
+                bs8::sfor<16>([&](auto J) {
+                    constexpr int j = decltype(J)::value;
+                    if constexpr (ARITH) bs8::transpose8_dev(X[j]);
+                    const uint32_t so = sym_off(16u * A + j, k, oo, es);
+                    v4u x, y;
+                    x.x = X[j][0]; x.y = X[j][1]; x.z = X[j][2]; x.w = X[j][3];
+                    y.x = X[j][4]; y.y = X[j][5]; y.z = X[j][6]; y.w = X[j][7];
+                    if (!MEM) {
+                    } else if (rs) {
+                        __builtin_amdgcn_raw_buffer_store_b128(x, ro, a.off[0], so, 16);
+                        __builtin_amdgcn_raw_buffer_store_b128(y, ro, a.off[1], so, 16);
+                    } else {
+                        __builtin_amdgcn_raw_buffer_store_b128(x, ro, a.off[0], so, 2);
+                        __builtin_amdgcn_raw_buffer_store_b128(y, ro, a.off[1], so, 2);
+                    }
+                    asm volatile("s_nop 2" ::: "memory");  // store-data hazard, see bs_uni_wave
+                });
+            }
+            if (crow) pend = cset / p.rn;
+            if (!more) break;
+            if (!pre) {
+                // slow path (main sequence exhausted, next Q1 set not ready): publish our
+                // own row set first, wait, then load the next set synchronously
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+                if (t0) {
+                    if (pend != kNone) q_signal(p, pend);
+                    lds[3] = q_wait(p, nxt);
+                }
+                pend = kNone;
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+                nsq = __builtin_amdgcn_readfirstlane(lds[3]);
+                q_item(p, nxt, nsq, nrow, nset);
+                an = addr(nrow, nset);
+                issue_dma(nrow, nxt & kQ1, an);
+                issue_direct(nrow, nxt & kQ1, an);
+                __builtin_amdgcn_s_waitcnt(0x0F70);
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(32) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            }
+            cur = nxt;
+            crow = nrow;
+            cset = nset;
         }
-        ++iter;
-        cur = nxt;
-        crow = nrow;
-        cset = nset;
-        csq = nsq;
     }
     // drain: every wave's stores, then the last row set's signal and the exit count;
-    // the last workgroup out re-zeroes the queue for the next launch on this buffer
+    // the last workgroup out re-zeroes the queue for the next launch on these words
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     if (t0) {
-        if (pend != 0xFFFFFFFFu) signal(pend);
+        if (pend != kNone) q_signal(p, pend);
         __builtin_amdgcn_s_waitcnt(0x0F70);
-        const uint32_t done = __hip_atomic_fetch_add(&ctr[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (done == gridDim.x - 1u) {
-            __hip_atomic_store(&ctr[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            for (uint32_t s = 0; s < p.count; ++s)
-                __hip_atomic_store(&ctr[3 + s], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&ctr[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (q_add(&p.ctr[kQExit]) == gridDim.x - 1u) {
+            if (q_load(&p.ctr[kQErr])) {
+                __hip_atomic_store(p.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                q_store(&p.ctr[kQErr], 0u);
+            }
+            q_store(&p.ctr[kQMain], 0u);
+            q_store(&p.ctr[kQHead1], 0u);
+            q_store(&p.ctr[kQReady], 0u);
+            q_store(&p.ctr[kQRes], 0u);
+            q_store(&p.ctr[kQLeft], 0u);
+            for (uint32_t s = 0; s < 2u * p.count; ++s) q_store(&p.ctr[kQRows + s], 0u);
+            q_store(&p.ctr[kQExit], 0u);
         }
     }
 }
 
 template <int MODE>
-__global__ __launch_bounds__(512, 1) void encode_gf8_bs128f_kernel(FusedPlan p) {
+__global__ __launch_bounds__(512, 1) void extend_gf8_bs128q_kernel(QueuePlan p) {
     __shared__ uint32_t lds[(kDmaBytes + kXchBytes) / 4];
-    bs_fused_wave<MODE>(p, lds, (uint32_t)(uintptr_t)lds, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
+    bs_queue_wave<MODE>(p, lds, (uint32_t)(uintptr_t)lds, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
 }
 
-
+#ifdef RSM_DIAG
 // ---------------------------------------------------------------------------
 // Dual launch (DualPlan): bs_uni_wave's persistent pipeline over the union of two
 // independent set lists.  Set t maps to (list, index); with nb == 2 na every group
@@ -783,22 +992,40 @@ hipError_t launch_encode_gf8_bs128(const CodewordSet& cs, hipStream_t st) {
     return hipGetLastError();
 }
 
-#ifdef RSM_DIAG
-// The fused launch needs whole sets per square in both passes (k * S a multiple of
+// The queue launch needs whole sets per square in both passes (k * S a multiple of
 // 2 KiB: every k = 128 square) and the plain row/column CodewordSets to qualify.
-bool bs128_fused_applicable(const CodewordSet& rows, const CodewordSet& cols) {
+bool bs128_queue_applicable(const CodewordSet& rows, const CodewordSet& cols) {
     if (rows.k != 128 || ((uint64_t)rows.k * rows.S) % kSetBytes != 0) return false;
     return bs128_applicable(rows) && bs128_applicable(cols);
 }
 
-hipError_t launch_extend_gf8_bs128_fused(const FusedPlan& p, hipStream_t st) {
-    if (p.total == 0) return hipSuccess;
+// Production: MODE 104 (ds_write_addtid_b32 exchange, the direct half of the next
+// set's loads right after the first exchange).  Measured (profiles/r02g_queue_ab.jsonl,
+// 128 squares per step, 3 streams): 8.80-8.89 us per square against 9.08 with the
+// direct loads after the large layers and 9.52 at the top of the set; Q0 read
+// non-temporal 9.07 (the Infinity-Cache re-read needs the default policy).
+hipError_t launch_extend_gf8_bs128_queue(const QueuePlan& p, hipStream_t st) {
+    const uint32_t total = p.nmain + p.nq1;
+    if (total == 0) return hipSuccess;
     const uint32_t cap = p.rows.grid ? p.rows.grid : 256u;
-    const uint32_t grid = p.total < cap ? p.total : cap;
-    hipLaunchKernelGGL((encode_gf8_bs128f_kernel<40>), dim3(grid), dim3(512), 0, st, p);
+    const uint32_t grid = total < cap ? total : cap;
+#ifdef RSM_DIAG
+    switch (g_diag_mode.load()) {
+        case 2: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<106>), dim3(grid), dim3(512), 0, st, p); break;  // no arithmetic
+        case 4: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<108>), dim3(grid), dim3(512), 0, st, p); break;  // no memory
+        case 140: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<40>), dim3(grid), dim3(512), 0, st, p); break;  // direct loads after the large layers
+        case 168: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<168>), dim3(grid), dim3(512), 0, st, p); break;
+        case 296: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<296>), dim3(grid), dim3(512), 0, st, p); break;
+        case 616: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<616>), dim3(grid), dim3(512), 0, st, p); break;
+        default: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<104>), dim3(grid), dim3(512), 0, st, p); break;
+    }
+#else
+    hipLaunchKernelGGL((extend_gf8_bs128q_kernel<104>), dim3(grid), dim3(512), 0, st, p);
+#endif
     return hipGetLastError();
 }
 
+#ifdef RSM_DIAG
 hipError_t launch_encode_gf8_bs128_dual(const DualPlan& p, hipStream_t st) {
     const uint32_t sets = p.na + p.nb;
     if (sets == 0) return hipSuccess;

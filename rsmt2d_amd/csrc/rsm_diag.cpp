@@ -14,7 +14,7 @@ using namespace rsm;
 
 namespace {
 
-CodewordSet rows_of(uint8_t* d_eds, uint32_t k, uint32_t S, uint32_t count, uint32_t grid) {
+[[maybe_unused]] CodewordSet rows_of(uint8_t* d_eds, uint32_t k, uint32_t S, uint32_t count, uint32_t grid) {
     const uint64_t W = 2ull * k;
     CodewordSet rows{};
     rows.base = rows.out_base = d_eds;
@@ -57,10 +57,11 @@ int rsm_diag_set_bs_row_mode(int mode) {
     return RSM_OK;
 }
 
-// Both passes of `count` in-place k = 128 squares as ONE persistent launch (the
-// row sets of square s + lag interleaved with the column sets of square s).
-// Synchronous: reads back the kernel's stuck-wait flag and fails if it is set.
-int rsm_diag_extend_fused(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size, uint32_t count, uint32_t lag,
+// Both passes of `count` in-place k = 128 squares as ONE persistent launch
+// (extend_gf8_bs128q_kernel, the kernel variant chosen by rsm_diag_set_bs_mode):
+// `delay` squares of row sets lead the Q0-column sets.  Asynchronous on `stream`;
+// rsm_diag_queue_check reports a stuck wait.
+int rsm_diag_extend_fused(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size, uint32_t count, uint32_t delay,
                           void* stream) {
     if (!ctx || !d_eds || k != 128 || validate_chunk_size(share_size) != RSM_OK ||
         ((uint64_t)k * share_size) % 2048 != 0)
@@ -68,30 +69,18 @@ int rsm_diag_extend_fused(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_
     if (count == 0) return RSM_OK;
     if (int rc = use_device(ctx)) return rc;
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-    FusedPlan p{};
-    p.rows = rows_of(static_cast<uint8_t*>(d_eds), k, share_size, count, ctx->cus);
-    p.cols = cols_of(static_cast<uint8_t*>(d_eds), k, share_size, count, ctx->cus);
-    if (!bs128_fused_applicable(p.rows, p.cols)) return fail(RSM_EUNSUPPORTED, "fused extension not applicable");
-    p.count = count;
-    p.lag = lag < 1 ? 1 : (lag > count ? count : lag);
-    p.rn = (uint32_t)((uint64_t)k * share_size / 2048);
-    p.cn = 2 * p.rn;
-    p.total = count * (p.rn + p.cn);
-    StreamScratch& ss = stream_scratch(ctx, st);
-    std::lock_guard<std::mutex> lk(ss.mu);
-    const size_t words = (size_t)count + 3;
+    const int rc = extend_squares_queue(ctx, static_cast<uint8_t*>(d_eds), k, share_size, count, st, delay);
+    return rc == RSM_EUNSUPPORTED ? fail(rc, "queue extension not applicable") : rc;
+}
+
+// Waits for `stream` and reports (and clears) a stuck wait of its queue launches.
+int rsm_diag_queue_check(rsm_ctx* ctx, void* stream) {
+    if (!ctx) return fail(RSM_EINVAL, "rsm_diag_queue_check: bad arguments");
+    if (int rc = use_device(ctx)) return rc;
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
     hipError_t e = hipStreamSynchronize(st);
-    if (e == hipSuccess) e = ss.leaf.ensure(words * 4);  // the stream's scratch doubles as the queue words
-    if (e == hipSuccess) e = hipMemsetAsync(ss.leaf.ptr, 0, words * 4, st);
-    if (e != hipSuccess) return hip_fail(e, "fused extension: queue words");
-    p.ctr = static_cast<uint32_t*>(ss.leaf.ptr);
-    if ((e = launch_extend_gf8_bs128_fused(p, st)) != hipSuccess) return hip_fail(e, "fused extension launch");
-    uint32_t stuck = 0;
-    if ((e = hipMemcpyAsync(&stuck, p.ctr + 2, 4, hipMemcpyDeviceToHost, st)) != hipSuccess ||
-        (e = hipStreamSynchronize(st)) != hipSuccess)
-        return hip_fail(e, "fused extension: error flag");
-    if (stuck) return fail(RSM_EDEVICE, "fused extension: a column set timed out waiting for its rows (output invalid)");
-    return RSM_OK;
+    if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+    return check_queue_reports(ctx, st);
 }
 
 // ONE launch running the row pass of the squares at d_rows_eds and the column pass

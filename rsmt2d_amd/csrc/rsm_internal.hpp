@@ -62,6 +62,8 @@ struct StreamScratch {
     std::mutex mu;
     DevBuf gf16_work, gf16_errs;  // GF(2^16) work arrays / error locators
     DevBuf leaf;                  // DefaultTree leaf digests (device roots)
+    DevBuf queue;                 // work-queue words of the single-launch extension
+    HostBuf qerr;                 // its stuck-wait report (pinned, written by the device)
 };
 
 // Buffers of the ExtendedDataSquare layer (Repair, device roots of an EDS):
@@ -139,6 +141,14 @@ int launch_encode(rsm_ctx* ctx, const CodewordSet& cs, hipStream_t st);
 int launch_decode(rsm_ctx* ctx, const DecodeSet& ds, hipStream_t st);
 int extend_squares(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, uint32_t count, hipStream_t st,
                    int phases = 3);
+// Both passes of `count` k = 128 squares as ONE queue-driven launch
+// (extend_gf8_bs128q_kernel); RSM_EUNSUPPORTED when the shape does not qualify.
+// `delay`: squares of row sets handed out before the first Q0-column set.
+int extend_squares_queue(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, uint32_t count, hipStream_t st,
+                         uint32_t delay = 2);
+// RSM_EDEVICE (and clears the report) when a completed queue launch on `st` (NULL:
+// on any stream of the context) timed out waiting -- its output is invalid.
+int check_queue_reports(rsm_ctx* ctx, hipStream_t st);
 // DefaultTree row + column roots of a device-resident complete [W][W][S] square:
 // d_roots receives 2*W*32 bytes (row roots, then column roots).  RSM_EUNSUPPORTED
 // when W is outside roots_dev_supported().

@@ -85,27 +85,35 @@ hipError_t launch_compare(const uint8_t* a, const uint8_t* b, uint64_t n, uint32
 hipError_t launch_compare_parity(const uint8_t* a, const uint8_t* b, uint32_t k, uint32_t S, uint32_t axis,
                                  const uint32_t* indices, uint32_t count, uint32_t* flags, hipStream_t st);
 
+// One launch that runs both passes of the 2D extension over `count` k = 128
+// squares (kernels_gf8_bs.hip, extend_gf8_bs128q_kernel): row sets and Q0-column
+// sets from one queue head, Q1-column sets from a ready list that the last row set
+// of each square appends to, so the column sets re-read Q0 and Q1 while they are
+// still in the Infinity Cache.  ctr: 224 + 2 * count zeroed words (the kernel
+// leaves them zeroed again); a bounded wait that times out (never, by the
+// deadlock-freedom argument in the kernel, short of a hardware fault) sets *err,
+// a device-visible pinned host word the host checks after the stream completes.
+struct QueuePlan {
+    CodewordSet rows, cols;
+    uint32_t* ctr;
+    uint32_t* err;   // pinned host word (device-visible)
+    uint32_t count;  // squares
+    uint32_t rn, cn; // sets per square: row pass (= Q0-column sets = Q1-column sets), column pass
+    uint32_t delay;  // row sets handed out before the first Q0-column set (<= count * rn)
+    uint32_t nmain;  // 2 * count * rn: row sets + Q0-column sets
+    uint32_t nq1;    // count * rn: Q1-column sets
+    uint32_t margin; // a Q1-column set is claimed while more than this many ready ones are unclaimed
+};
+constexpr uint32_t kQueueFixedWords = 224;
+bool bs128_queue_applicable(const CodewordSet& rows, const CodewordSet& cols);
+hipError_t launch_extend_gf8_bs128_queue(const QueuePlan& p, hipStream_t st);
+
+
 #ifdef RSM_DIAG
 // ---------------------------------------------------------------------------
 // Diagnostic / A-B kernels: compiled only into librsmt2d_hip_diag.so (make diag),
 // never into the product library.
 // ---------------------------------------------------------------------------
-// One launch that runs both passes of the 2D extension over `count` squares
-// (kernels_gf8_bs.hip, encode_gf8_bs128f_kernel): the row sets of square s and
-// the column sets of square s - lag are handed out from one device-wide queue,
-// and a column set waits for its square's row sets (per-square counters), so the
-// column pass re-reads Q0 and Q1 while they are still in the Infinity Cache.
-struct FusedPlan {
-    CodewordSet rows, cols;
-    uint32_t* ctr;   // [0] queue head, [1] exit count, [2] error flag, [3 + s] row sets done of square s
-    uint32_t count;  // squares
-    uint32_t lag;    // squares the column sets trail the row sets by (1 <= lag <= count)
-    uint32_t rn, cn; // sets per square: row pass, column pass
-    uint32_t total;  // count * (rn + cn)
-    uint32_t flags;  // debug: 1 = never prefetch (every item takes the synchronous path)
-    uint32_t* trace; // debug (nullable): trace[item] = workgroup << 8 | iteration << 2 | path
-};
-
 // Two independent codeword batches in one persistent launch (kernels_gf8_bs.hip,
 // encode_gf8_bs128p_kernel): the row pass of one batch of squares and the column
 // pass of another, sets interleaved 1 : 2 when nb == 2 * na so that every CU mixes
@@ -115,10 +123,6 @@ struct DualPlan {
     uint32_t na, nb;  // sets of a, of b
 };
 
-// fused two-pass M = 128 extension; ctr must hold count + 3 zeroed words (the
-// kernel leaves them zeroed again, except the error flag ctr[2])
-bool bs128_fused_applicable(const CodewordSet& rows, const CodewordSet& cols);
-hipError_t launch_extend_gf8_bs128_fused(const FusedPlan& p, hipStream_t st);
 hipError_t launch_encode_gf8_bs128_dual(const DualPlan& p, hipStream_t st);
 // A-B kernel variant of the bit-sliced encode: 40 production, 0/8/24/56 A-B
 // variants, 2 = no arithmetic, 4 = no global memory (wrong output by design)

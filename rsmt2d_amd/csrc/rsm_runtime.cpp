@@ -249,9 +249,96 @@ int launch_decode(rsm_ctx* ctx, const DecodeSet& ds0, hipStream_t st) {
 // which equals the reference's row-encoding of Q2 by linearity of the 2D code
 // (extendeddatasquare.go:204-207; asserted in tests against the oracle, which
 // runs the reference order).
+static CodewordSet rows_set(uint8_t* d_eds, uint32_t k, uint32_t S, uint32_t count) {
+    const uint64_t W = 2ull * k;
+    CodewordSet rows{};
+    rows.base = rows.out_base = d_eds;
+    rows.square_stride = W * W * S;
+    rows.cw_stride = W * S;
+    rows.elem_stride = S;
+    rows.out_offset = (uint64_t)k * S;
+    rows.per_square = k;
+    rows.count = k * count;
+    rows.k = k;
+    rows.S = S;
+    rows.pass = 0;
+    return rows;
+}
+
+static CodewordSet cols_set(uint8_t* d_eds, uint32_t k, uint32_t S, uint32_t count) {
+    const uint64_t W = 2ull * k;
+    CodewordSet cols = rows_set(d_eds, k, S, count);
+    cols.cw_stride = S;
+    cols.elem_stride = W * S;
+    cols.out_offset = (uint64_t)k * W * S;
+    cols.per_square = (uint32_t)W;
+    cols.count = (uint32_t)W * count;
+    cols.pass = 1;
+    return cols;
+}
+
+int check_queue_reports(rsm_ctx* ctx, hipStream_t st) {
+    bool stuck = false;
+    std::lock_guard<std::mutex> lk(ctx->scratch_mu);
+    for (auto& kv : ctx->scratch) {
+        if (st && kv.first != st) continue;
+        volatile uint32_t* w = static_cast<volatile uint32_t*>(kv.second->qerr.ptr);
+        if (w && *w) {
+            *w = 0;
+            stuck = true;
+        }
+    }
+    return stuck ? fail(RSM_EDEVICE, "single-launch extension: a column set timed out waiting for its rows "
+                                     "(that launch's output is invalid)")
+                 : RSM_OK;
+}
+
+int extend_squares_queue(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, uint32_t count, hipStream_t st,
+                         uint32_t delay) {
+    if (field_bits(k) != 8 || count == 0) return RSM_EUNSUPPORTED;
+    QueuePlan p{};
+    p.rows = rows_set(d_eds, k, S, count);
+    p.cols = cols_set(d_eds, k, S, count);
+    p.rows.grid = p.cols.grid = ctx->cus;
+    p.rows.chunks = p.cols.chunks = (S + 255) / 256;
+    if (!bs128_queue_applicable(p.rows, p.cols)) return RSM_EUNSUPPORTED;
+    if (int rc = check_queue_reports(ctx, st)) return rc;
+    p.count = count;
+    p.rn = (uint32_t)((uint64_t)k * S / 2048);
+    p.cn = 2 * p.rn;
+    p.delay = (delay > count ? count : delay) * p.rn;
+    p.nmain = 2 * count * p.rn;
+    p.nq1 = count * p.rn;
+    p.margin = p.rn / 2;
+    StreamScratch& ss = stream_scratch(ctx, st);
+    std::lock_guard<std::mutex> lk(ss.mu);
+    const size_t bytes = (kQueueFixedWords + 2 * (size_t)count) * 4;
+    hipError_t e;
+    if (bytes > ss.queue.cap) {  // zeroed once: every launch leaves its words zeroed
+        if ((e = hipStreamSynchronize(st)) != hipSuccess || (e = ss.queue.ensure(bytes)) != hipSuccess ||
+            (e = hipMemsetAsync(ss.queue.ptr, 0, ss.queue.cap, st)) != hipSuccess)
+            return hip_fail(e, "single-launch extension: queue words");
+    }
+    if (!ss.qerr.ptr) {
+        if ((e = ss.qerr.ensure(64)) != hipSuccess) return hip_fail(e, "single-launch extension: report word");
+        *static_cast<volatile uint32_t*>(ss.qerr.ptr) = 0;
+    }
+    p.ctr = static_cast<uint32_t*>(ss.queue.ptr);
+    p.err = static_cast<uint32_t*>(ss.qerr.ptr);
+    if ((e = launch_extend_gf8_bs128_queue(p, st)) != hipSuccess) return hip_fail(e, "single-launch extension");
+    return RSM_OK;
+}
+
+// Two-phase in-place extension; batches of k = 128 squares run both phases as one
+// queue-driven launch (extend_squares_queue), which re-reads Q0 and Q1 from the
+// Infinity Cache instead of HBM.
 int extend_squares(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, uint32_t count, hipStream_t st,
                    int phases) {
     const uint64_t W = 2ull * k;
+    if (phases == 3 && count >= 2) {
+        const int rc = extend_squares_queue(ctx, d_eds, k, S, count, st);
+        if (rc != RSM_EUNSUPPORTED) return rc;
+    }
     if (phases & 1) {
         CodewordSet rows{};
         rows.base = d_eds;
@@ -827,7 +914,8 @@ int rsm_sync(rsm_ctx* ctx) {
     if (!ctx) return fail(RSM_EINVAL, "rsm_sync: NULL ctx");
     if (int rc = use_device(ctx)) return rc;
     hipError_t e = hipStreamSynchronize(ctx->stream);
-    return e == hipSuccess ? RSM_OK : hip_fail(e, "hipStreamSynchronize");
+    if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+    return check_queue_reports(ctx, nullptr);
 }
 
 // Events: in-loop timing of the production launches (bench.py records one per

@@ -115,6 +115,9 @@ hipError_t launch_decode_gf16(const DecodeSet& ds, const Gf16Dev& g, hipStream_t
 }
 bool bs128_applicable(const CodewordSet&) { return false; }
 hipError_t launch_encode_gf8_bs128(const CodewordSet& cs, hipStream_t st) { return launch_encode_gf8(cs, st); }
+// the single-launch batch path never qualifies here (batches take the two-launch form)
+bool bs128_queue_applicable(const CodewordSet&, const CodewordSet&) { return false; }
+hipError_t launch_extend_gf8_bs128_queue(const QueuePlan&, hipStream_t) { return hipErrorInvalidValue; }
 bool roots_dev_supported(uint32_t W) { return W >= 1 && W <= 2048; }
 hipError_t launch_roots(const uint8_t* d_eds, uint32_t W, uint32_t S, uint32_t squares, uint32_t* d_leaf,
                         uint8_t* d_roots, hipStream_t) {

@@ -145,13 +145,15 @@ def test_product_has_no_diagnostics(lib):
         assert name not in blob, name
     assert not re.search(rb"RSM_[A-Z0-9_]{3,}\x00", blob), re.search(rb"RSM_[A-Z0-9_]{3,}\x00", blob)
     # kernel symbols embedded in the gfx950 code object: only the production modes
-    # of the bit-sliced encode (row pass 104, column pass 184: kernels_gf8_bs.hip),
-    # no diagnostic mode (bits 2 / 4: no arithmetic / no memory), no fused (bs128f)
-    # or dual (bs128p) kernel
+    # of the bit-sliced encode (row pass 104, column pass 184, single-launch queue
+    # extension 104: kernels_gf8_bs.hip), no diagnostic mode (bits 2 / 4: no
+    # arithmetic / no memory), no dual (bs128p) kernel
     modes = set(re.findall(rb"encode_gf8_bs128u_kernelILi(\d+)E", blob))
     assert modes == {b"104", b"184"}, modes
-    assert not any(int(m) & 6 for m in modes)
-    assert b"encode_gf8_bs128f_kernel" not in blob and b"encode_gf8_bs128p_kernel" not in blob
+    qmodes = set(re.findall(rb"extend_gf8_bs128q_kernelILi(\d+)E", blob))
+    assert qmodes == {b"104"}, qmodes
+    assert not any(int(m) & 6 for m in modes | qmodes)
+    assert b"encode_gf8_bs128p_kernel" not in blob
     txt = re.sub(r"/\*.*?\*/", "", open(DIAG_HEADER).read(), flags=re.S)
     for s in set(re.findall(r"\b(rsm_diag_[a-z0-9_]+)\s*\(", txt)):
         assert not hasattr(lib, s), s
@@ -163,7 +165,7 @@ def test_diag_library_is_separate():
     if not os.path.exists(R.DIAG_LIB_PATH):
         pytest.skip("diagnostic library not built")
     blob = open(R.DIAG_LIB_PATH, "rb").read()
-    assert b"encode_gf8_bs128f_kernel" in blob
+    assert set(re.findall(rb"extend_gf8_bs128q_kernelILi(\d+)E", blob)) > {b"104"}  # + A-B / diagnostic modes
     dl = R.diag_library()
     for s in R.DIAG_SIGNATURES:
         assert hasattr(dl, s), s

@@ -37,23 +37,31 @@ def _down(dl, ctx, ptr, n):
     return out
 
 
-@pytest.mark.parametrize("count,S,lag", [(1, 512, 1), (3, 512, 2), (4, 64, 4)])
+@pytest.mark.parametrize("count,S,lag", [(1, 512, 0), (1, 512, 1), (3, 512, 2), (4, 64, 4), (9, 512, 2),
+                                         (40, 512, 0), (2, 1024, 1), (5, 192, 3)])
 def test_fused_matches_two_launch(dl, count, S, lag):
+    """Queue-driven single launch (extend_gf8_bs128q_kernel) == the two-launch
+    production schedule, bit for bit, twice on the same (self-re-zeroed) queue words."""
     k = 128
     n = (2 * k) ** 2 * S * count
     ctx = _ctx(dl)
-    a, b = _buf(dl, ctx, n), _buf(dl, ctx, n)
-    R._check_with(dl, dl.rsm_dev_fill_random(ctx, a, n, 91 + count))
+    src, a, b = _buf(dl, ctx, n), _buf(dl, ctx, n), _buf(dl, ctx, n)
+    R._check_with(dl, dl.rsm_dev_fill_random(ctx, src, n, 91 + count))
     R._check_with(dl, dl.rsm_sync(ctx))
-    R._check_with(dl, dl.rsm_memcpy(ctx, b, a, n, 2))
+    R._check_with(dl, dl.rsm_memcpy(ctx, a, src, n, 2))
     R._check_with(dl, dl.rsm_extend_squares_dev(ctx, a, k, S, count, None))
-    R._check_with(dl, dl.rsm_diag_extend_fused(ctx, b, k, S, count, lag, None))
     R._check_with(dl, dl.rsm_sync(ctx))
-    ga, gb = _down(dl, ctx, a, n), _down(dl, ctx, b, n)
-    assert np.array_equal(ga, gb)
+    ga = _down(dl, ctx, a, n)
     sq = ga[: (2 * k) ** 2 * S].reshape(2 * k, 2 * k, S)
     assert np.array_equal(sq, oracle.extend_square(sq[:k, :k].copy(), nthreads=8))
-    for p in (a, b):
+    for _ in range(2):
+        R._check_with(dl, dl.rsm_memcpy(ctx, b, src, n, 2))
+        R._check_with(dl, dl.rsm_sync(ctx))
+        R._check_with(dl, dl.rsm_diag_extend_fused(ctx, b, k, S, count, lag, None))
+        R._check_with(dl, dl.rsm_diag_queue_check(ctx, None))
+        R._check_with(dl, dl.rsm_sync(ctx))
+        assert np.array_equal(ga, _down(dl, ctx, b, n))
+    for p in (src, a, b):
         dl.rsm_dev_free(ctx, p)
     dl.rsm_ctx_destroy(ctx)
 

@@ -113,7 +113,10 @@ def test_pass_grid_caps_do_not_change_results(lib, cap):
     for p in (0, 1):
         R._check(lib.rsm_ctx_set_pass_grid(ctx, p, cap, ctypes.byref(prev) if p == 0 else None))
     try:
-        R._check(lib.rsm_extend_squares_dev(ctx, b.ptr, k, S, B, None))
+        # the two-launch form (row pass, column pass): the single-launch batch path
+        # always runs on every CU
+        R._check(lib.rsm_extend_squares_phase_dev(ctx, b.ptr, k, S, B, 1, None))
+        R._check(lib.rsm_extend_squares_phase_dev(ctx, b.ptr, k, S, B, 2, None))
         R._check(lib.rsm_sync(ctx))
     finally:
         for p in (0, 1):
@@ -122,6 +125,70 @@ def test_pass_grid_caps_do_not_change_results(lib, cap):
     for i in range(B):
         assert np.array_equal(got[i], oracle.extend_square(got[i, :k, :k].copy(), nthreads=8))
     assert lib.rsm_ctx_set_pass_grid(ctx, 2, 0, None) == R.RSM_EINVAL
+
+
+@pytest.mark.parametrize("S,count", [(512, 2), (512, 3), (512, 17), (64, 9), (1024, 4), (512, 70)])
+def test_single_launch_batch_matches_two_launch(lib, S, count):
+    """Batches of k = 128 squares run as ONE queue-driven launch (row sets, Q0-column
+    sets, Q1-column sets from a ready list: extend_gf8_bs128q_kernel); bit-exact with
+    the two-launch form, twice on the same (self-re-zeroed) queue words, and the
+    first / last square against the oracle."""
+    ctx = R.device_context(0)
+    k = 128
+    W = 2 * k
+    n = W * W * S * count
+    src, a, b = (R.DeviceBuffer(n) for _ in range(3))
+    src.fill_random(900 + count)
+    R._check(lib.rsm_sync(ctx))
+    R._check(lib.rsm_memcpy(ctx, a.ptr, src.ptr, n, 2))
+    R._check(lib.rsm_extend_squares_phase_dev(ctx, a.ptr, k, S, count, 1, None))
+    R._check(lib.rsm_extend_squares_phase_dev(ctx, a.ptr, k, S, count, 2, None))
+    R._check(lib.rsm_sync(ctx))
+    want = a.download(n)
+    for _ in range(2):
+        R._check(lib.rsm_memcpy(ctx, b.ptr, src.ptr, n, 2))
+        R._check(lib.rsm_extend_squares_dev(ctx, b.ptr, k, S, count, None))
+        R._check(lib.rsm_sync(ctx))
+        assert np.array_equal(b.download(n), want)
+    sq = want.reshape(count, W, W, S)
+    for i in (0, count - 1):
+        assert np.array_equal(sq[i], oracle.extend_square(sq[i, :k, :k].copy(), nthreads=8))
+
+
+def test_single_launch_batches_on_three_streams(lib):
+    """Three streams each run single-launch batches on their own buffer (each stream
+    owns its queue words), several rounds; every square equals the two-launch result."""
+    ctx = R.device_context(0)
+    k, S, B = 128, 512, 6
+    W = 2 * k
+    n = W * W * S * B
+    src = [R.DeviceBuffer(n) for _ in range(3)]
+    work = [R.DeviceBuffer(n) for _ in range(3)]
+    for i, b in enumerate(src):
+        b.fill_random(77 + i)
+    R._check(lib.rsm_sync(ctx))
+    want = []
+    for i in range(3):
+        R._check(lib.rsm_memcpy(ctx, work[i].ptr, src[i].ptr, n, 2))
+        R._check(lib.rsm_extend_squares_phase_dev(ctx, work[i].ptr, k, S, B, 1, None))
+        R._check(lib.rsm_extend_squares_phase_dev(ctx, work[i].ptr, k, S, B, 2, None))
+        R._check(lib.rsm_sync(ctx))
+        want.append(work[i].download(n))
+    st = [ctypes.c_void_p() for _ in range(3)]
+    for s in st:
+        R._check(lib.rsm_stream_create(ctx, ctypes.byref(s)))
+    for _ in range(3):
+        for i in range(3):
+            R._check(lib.rsm_memcpy(ctx, work[i].ptr, src[i].ptr, n, 2))
+        for i in range(3):
+            R._check(lib.rsm_extend_squares_dev(ctx, work[i].ptr, k, S, B, st[i]))
+        for s in st:
+            R._check(lib.rsm_stream_sync(s))
+        R._check(lib.rsm_sync(ctx))  # also reports a stuck queue wait on any stream
+        for i in range(3):
+            assert np.array_equal(work[i].download(n), want[i])
+    for s in st:
+        R._check(lib.rsm_stream_destroy(ctx, s))
 
 
 @pytest.mark.parametrize("k,S,count", [(128, 512, 5), (16, 64, 3), (256, 128, 2)])
