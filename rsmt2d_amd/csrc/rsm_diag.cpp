@@ -69,7 +69,10 @@ int rsm_diag_extend_fused(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_
     if (count == 0) return RSM_OK;
     if (int rc = use_device(ctx)) return rc;
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-    const int rc = extend_squares_queue(ctx, static_cast<uint8_t*>(d_eds), k, share_size, count, st, delay);
+    // delay bits 0-7: squares; bits 8-15 (if non-zero): the Q1 claim margin + 1
+    const uint32_t m = (delay >> 8) & 0xFFu;
+    const int rc = extend_squares_queue(ctx, static_cast<uint8_t*>(d_eds), k, share_size, count, st, delay & 0xFFu,
+                                        m ? m - 1 : ~0u);
     return rc == RSM_EUNSUPPORTED ? fail(rc, "queue extension not applicable") : rc;
 }
 

@@ -145,7 +145,7 @@ int extend_squares(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, uint32_
 // (extend_gf8_bs128q_kernel); RSM_EUNSUPPORTED when the shape does not qualify.
 // `delay`: squares of row sets handed out before the first Q0-column set.
 int extend_squares_queue(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, uint32_t count, hipStream_t st,
-                         uint32_t delay = 2);
+                         uint32_t delay = 2, uint32_t margin = ~0u);
 // RSM_EDEVICE (and clears the report) when a completed queue launch on `st` (NULL:
 // on any stream of the context) timed out waiting -- its output is invalid.
 int check_queue_reports(rsm_ctx* ctx, hipStream_t st);

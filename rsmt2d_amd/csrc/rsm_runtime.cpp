@@ -294,7 +294,7 @@ int check_queue_reports(rsm_ctx* ctx, hipStream_t st) {
 }
 
 int extend_squares_queue(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, uint32_t count, hipStream_t st,
-                         uint32_t delay) {
+                         uint32_t delay, uint32_t margin) {
     if (field_bits(k) != 8 || count == 0) return RSM_EUNSUPPORTED;
     QueuePlan p{};
     p.rows = rows_set(d_eds, k, S, count);
@@ -309,7 +309,7 @@ int extend_squares_queue(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, u
     p.delay = (delay > count ? count : delay) * p.rn;
     p.nmain = 2 * count * p.rn;
     p.nq1 = count * p.rn;
-    p.margin = p.rn / 2;
+    p.margin = margin == ~0u ? p.rn / 2 : margin;
     StreamScratch& ss = stream_scratch(ctx, st);
     std::lock_guard<std::mutex> lk(ss.mu);
     const size_t bytes = (kQueueFixedWords + 2 * (size_t)count) * 4;
