@@ -7,10 +7,11 @@ Metric (BASELINE.json): GiB/s of device-resident 2D RS encode, k=128 square,
 A "step" = ComputeExtendedDataSquare's arithmetic (erasureExtendSquare,
 extendeddatasquare.go:154-227) over one batch of `--batch` independent squares
 already resident in HBM (the EDS buffer holds each ODS in its top-left quadrant,
-as the Go EDS aliases its input).  c2 default: 128 squares (4 GiB of EDS) per step
+as the Go EDS aliases its input).  c2 default: 256 squares (8 GiB of EDS) per step
 as ONE queue-driven launch (both passes, extend_gf8_bs128q_kernel), steps rotating
-over 3 streams and 3 buffers (12 GiB), so no step finds its squares in the 256 MiB
-Infinity Cache.
+over 3 streams and 3 buffers (24 GiB of the 288 GB), so no step finds its squares in
+the 256 MiB Infinity Cache.  (Per launch the schedule pays ~64 us of start-up and tail:
+8.84 / 8.68 / 8.59 us per square at 128 / 192 / 256 squares, profiles/r02g_queue_ab.jsonl.)
 value = ODS bytes encoded per second over all ranks (GiB/s).
 
 N > 1 GPUs (one process per GPU, torch.distributed): every rank encodes its own
@@ -503,7 +504,7 @@ def main():
     # k = 128: one queue-driven launch per step (both passes; rsm_extend_squares_dev
     # takes it for batches of >= 2 squares) unless --two-launch
     single = k == 128 and not a.two_launch and not a.one_stream
-    B = a.batch or (128 if single else max(1, (1 << 30) // sq_bytes))
+    B = a.batch or (256 if single else max(1, (1 << 30) // sq_bytes))
     nstreams = 1 if a.one_stream else (a.streams or (3 if single else 2))
     L = R.library()
     ctx = R.device_context(local)
