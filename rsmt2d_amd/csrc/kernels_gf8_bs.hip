@@ -529,9 +529,11 @@ __device__ __forceinline__ void bs_queue_wave(const QueuePlan& p, uint32_t* lds,
     // the first exchange, 128 the same for row sets only (column sets after the large
     // layers), 256 with the LDS-DMA half at the top of the set; default after the
     // large layers.  MODE 512: Q0 read non-temporal by both its readers (A/B).
+    // MODE 1024: after the byte->plane transposes; 2048: after the small IFFT layers
+    // (both before the first exchange).  MODE 4096: Q1 read with the default policy.
     constexpr bool ADDTID = (MODE & 8) != 0, ARITH = !(MODE & 2), EARLY = (MODE & 256) != 0,
-                   NTQ0 = (MODE & 512) != 0;
-    constexpr int DPOS = EARLY ? 0 : (MODE & 64) ? 1 : (MODE & 128) ? 3 : 2;
+                   NTQ0 = (MODE & 512) != 0, NTQ1 = !(MODE & 4096);
+    constexpr int DPOS = EARLY ? 0 : (MODE & 1024) ? 4 : (MODE & 2048) ? 5 : (MODE & 64) ? 1 : (MODE & 128) ? 3 : 2;
     const bool MEM = !(MODE & 4) || p.rows.S == 1;  // runtime-false in mode 4 (keeps the code alive)
     const uint32_t lane = threadIdx.x & 63u;
     const bool t0 = threadIdx.x == 0;
@@ -549,13 +551,13 @@ __device__ __forceinline__ void bs_queue_wave(const QueuePlan& p, uint32_t* lds,
     auto issue_dma = [&](uint32_t row, uint32_t q1, const SetAddr& a) {
         if (!MEM) return;
         if (row) issue_dma_rt<NTQ0>(p.rows, a, lds_base, A);
-        else if (q1) issue_dma_rt<true>(p.cols, a, lds_base, A);
+        else if (q1) issue_dma_rt<NTQ1>(p.cols, a, lds_base, A);
         else issue_dma_rt<NTQ0>(p.cols, a, lds_base, A);
     };
     auto issue_direct = [&](uint32_t row, uint32_t q1, const SetAddr& a) {
         if (!MEM) return;
         if (row) issue_direct_rt<NTQ0>(p.rows, a, A, P);
-        else if (q1) issue_direct_rt<true>(p.cols, a, A, P);
+        else if (q1) issue_direct_rt<NTQ1>(p.cols, a, A, P);
         else issue_direct_rt<NTQ0>(p.cols, a, A, P);
     };
 
@@ -631,14 +633,16 @@ __device__ __forceinline__ void bs_queue_wave(const QueuePlan& p, uint32_t* lds,
                 if constexpr (DPOS == 0) issue_direct(nrow, nxt & kQ1, an);
             }
             // direct loads issued since the previous set's stores, at the publish point
-            const bool dearly = pre && (DPOS <= 1 || (DPOS == 3 && nrow));
+            const bool dearly = pre && (DPOS <= 1 || DPOS >= 4 || (DPOS == 3 && nrow));
             // no claim in a workgroup's last set (nothing would take the item)
             if (t0) cand = more ? q_claim(p, qc) : kNone;
 
-            if constexpr (ARITH) {
-                bs8::sfor<16>([&](auto J) { bs8::transpose8_dev(X[decltype(J)::value]); });
-                bs8::small_ifft_all(X, A);
-            }
+            if constexpr (ARITH) bs8::sfor<16>([&](auto J) { bs8::transpose8_dev(X[decltype(J)::value]); });
+            if constexpr (DPOS == 4)
+                if (pre) issue_direct(nrow, nxt & kQ1, an);
+            if constexpr (ARITH) bs8::small_ifft_all(X, A);
+            if constexpr (DPOS == 5)
+                if (pre) issue_direct(nrow, nxt & kQ1, an);
             bs8::sfor<8>([&](auto Pp) { xch_to_large<decltype(Pp)::value, ADDTID>(X, e_small, s_small, e_large); });
             if constexpr (DPOS == 1 || DPOS == 3)
                 if (pre && (DPOS == 1 || nrow)) issue_direct(nrow, nxt & kQ1, an);
@@ -999,28 +1003,38 @@ bool bs128_queue_applicable(const CodewordSet& rows, const CodewordSet& cols) {
     return bs128_applicable(rows) && bs128_applicable(cols);
 }
 
-// Production: MODE 104 (ds_write_addtid_b32 exchange, the direct half of the next
-// set's loads right after the first exchange).  Measured (profiles/r02g_queue_ab.jsonl,
-// 128 squares per step, 3 streams): 8.80-8.89 us per square against 9.08 with the
-// direct loads after the large layers and 9.52 at the top of the set; Q0 read
-// non-temporal 9.07 (the Infinity-Cache re-read needs the default policy).
+// Production: MODE 2088 (ds_write_addtid_b32 exchange, the direct half of the next
+// set's loads after the small IFFT layers, just before the first exchange).  Measured
+// (profiles/r02g_queue_ab.jsonl, 3 streams, same box): 256 squares per step 8.43 us
+// per square against 8.57-8.59 right after the first exchange (MODE 104) and 8.73 right
+// after the transposes; at 128 squares 104 gave 8.80-8.89 against 9.08 after the large
+// layers and 9.52 at the top of the set; Q0 read non-temporal +3 %, Q1 read with the
+// default policy +3 % (the Infinity-Cache re-read of Q0 needs the default policy, the
+// last read of Q1 is best non-temporal).
 hipError_t launch_extend_gf8_bs128_queue(const QueuePlan& p, hipStream_t st) {
     const uint32_t total = p.nmain + p.nq1;
     if (total == 0) return hipSuccess;
     const uint32_t cap = p.rows.grid ? p.rows.grid : 256u;
     const uint32_t grid = total < cap ? total : cap;
 #ifdef RSM_DIAG
+    // diagnostic codes: 2 / 4 no arithmetic / no memory (wrong output by design);
+    // 104 direct loads right after the first exchange, 140 after the large layers,
+    // 168 rows early / columns late, 296 at the top of the set, 616 = 104 + Q0
+    // non-temporal, 1064 after the transposes, 4200 = 104 + Q1 default policy
     switch (g_diag_mode.load()) {
-        case 2: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<106>), dim3(grid), dim3(512), 0, st, p); break;  // no arithmetic
-        case 4: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<108>), dim3(grid), dim3(512), 0, st, p); break;  // no memory
-        case 140: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<40>), dim3(grid), dim3(512), 0, st, p); break;  // direct loads after the large layers
+        case 2: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<2090>), dim3(grid), dim3(512), 0, st, p); break;
+        case 4: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<2092>), dim3(grid), dim3(512), 0, st, p); break;
+        case 104: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<104>), dim3(grid), dim3(512), 0, st, p); break;
+        case 140: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<40>), dim3(grid), dim3(512), 0, st, p); break;
         case 168: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<168>), dim3(grid), dim3(512), 0, st, p); break;
         case 296: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<296>), dim3(grid), dim3(512), 0, st, p); break;
         case 616: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<616>), dim3(grid), dim3(512), 0, st, p); break;
-        default: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<104>), dim3(grid), dim3(512), 0, st, p); break;
+        case 1064: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<1064>), dim3(grid), dim3(512), 0, st, p); break;
+        case 4200: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<4200>), dim3(grid), dim3(512), 0, st, p); break;
+        default: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<2088>), dim3(grid), dim3(512), 0, st, p); break;
     }
 #else
-    hipLaunchKernelGGL((extend_gf8_bs128q_kernel<104>), dim3(grid), dim3(512), 0, st, p);
+    hipLaunchKernelGGL((extend_gf8_bs128q_kernel<2088>), dim3(grid), dim3(512), 0, st, p);
 #endif
     return hipGetLastError();
 }
