@@ -775,11 +775,17 @@ __device__ __forceinline__ void bs_queue_wave(const QueuePlan& p, uint32_t* lds,
     }
     // drain: every wave's stores, then the last row set's signal and the exit count;
     // the last workgroup out re-zeroes the queue for the next launch on these words
+    // (all its threads: 2 * count words)
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     if (t0) {
         if (pend != kNone) q_signal(p, pend);
         __builtin_amdgcn_s_waitcnt(0x0F70);
-        if (q_add(&p.ctr[kQExit]) == gridDim.x - 1u) {
+        lds[0] = q_add(&p.ctr[kQExit]) == gridDim.x - 1u ? 1u : 0u;
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (__builtin_amdgcn_readfirstlane(lds[0])) {
+        for (uint32_t s = threadIdx.x; s < 2u * p.count; s += blockDim.x) q_store(&p.ctr[kQRows + s], 0u);
+        if (t0) {
             if (q_load(&p.ctr[kQErr])) {
                 __hip_atomic_store(p.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 q_store(&p.ctr[kQErr], 0u);
@@ -789,7 +795,6 @@ __device__ __forceinline__ void bs_queue_wave(const QueuePlan& p, uint32_t* lds,
             q_store(&p.ctr[kQReady], 0u);
             q_store(&p.ctr[kQRes], 0u);
             q_store(&p.ctr[kQLeft], 0u);
-            for (uint32_t s = 0; s < 2u * p.count; ++s) q_store(&p.ctr[kQRows + s], 0u);
             q_store(&p.ctr[kQExit], 0u);
         }
     }

@@ -28,6 +28,7 @@ ctx = ctypes.c_void_p()
 chk(D.rsm_ctx_create(0, ctypes.byref(ctx)))
 ctx = ctx.value
 STEPS = int(os.environ.get("QAB_STEPS", "100"))
+EVENTS = os.environ.get("QAB_EVENTS", "0") == "1"  # a HIP event either side of every timed launch (as bench.py)
 
 
 def run(cfg, steps=STEPS, warmup=6):
@@ -63,22 +64,31 @@ def run(cfg, steps=STEPS, warmup=6):
             chk(D.rsm_stream_sync(s))
 
     n = [0]
+    evs = []
 
-    def step():
+    def step(timed=False):
         i = n[0]
         n[0] += 1
         st = streams[i % ns]
+        if timed and EVENTS:
+            e0, e1 = ctypes.c_void_p(), ctypes.c_void_p()
+            chk(D.rsm_event_create(ctx, ctypes.byref(e0)))
+            chk(D.rsm_event_create(ctx, ctypes.byref(e1)))
+            evs.append((e0, e1))
+            chk(D.rsm_event_record(ctx, e0, st))
         if kind == "two":
             chk(D.rsm_extend_squares_dev(ctx, bufs[i % nb], k, S, B, st))
         else:
             chk(D.rsm_diag_extend_fused(ctx, bufs[i % nb], k, S, B, delay, st))
+        if timed and EVENTS:
+            chk(D.rsm_event_record(ctx, evs[-1][1], st))
 
     for _ in range(warmup):
         step()
     sync()
     t0 = time.perf_counter()
     for _ in range(steps):
-        step()
+        step(True)
     sync()
     dt = (time.perf_counter() - t0) / steps
     ok = True
@@ -94,13 +104,16 @@ def run(cfg, steps=STEPS, warmup=6):
         chk(D.rsm_memcpy(ctx, got.ctypes.data, last + j * SQ, SQ, 1))
         got = got.reshape(W, W, S)
         ok &= bool(np.array_equal(got, oracle.extend_square(got[:k, :k].copy(), nthreads=16)))
+    for e0, e1 in evs:
+        D.rsm_event_destroy(e0)
+        D.rsm_event_destroy(e1)
     for s in streams[1:]:
         chk(D.rsm_stream_destroy(ctx, s))
     for p in bufs:
         chk(D.rsm_dev_free(ctx, p))
     us_sq = dt / B * 1e6
     algo = 4 * k * k * S
-    return {"cfg": cfg, "us_per_step": round(dt * 1e6, 2), "us_per_square": round(us_sq, 3),
+    return {"cfg": cfg, "events": EVENTS, "us_per_step": round(dt * 1e6, 2), "us_per_square": round(us_sq, 3),
             "step_frac": round(algo / (us_sq * 1e-6) / 8e12, 4), "ok": ok}
 
 
