@@ -282,6 +282,9 @@ int check_queue_reports(rsm_ctx* ctx, hipStream_t st) {
     std::lock_guard<std::mutex> lk(ctx->scratch_mu);
     for (auto& kv : ctx->scratch) {
         if (st && kv.first != st) continue;
+        // the stream's lock: extend_squares_queue allocates the word under it (lock
+        // order scratch_mu -> StreamScratch::mu, as everywhere else)
+        std::lock_guard<std::mutex> lk2(kv.second->mu);
         volatile uint32_t* w = static_cast<volatile uint32_t*>(kv.second->qerr.ptr);
         if (w && *w) {
             *w = 0;
