@@ -417,43 +417,56 @@ __global__ __launch_bounds__(64) void decode_gf8_kernel(DecodeSet ds) {
 }
 
 // ---------------------------------------------------------------------------
-// Split decoder for M = 128 (65 <= k <= 128, n = 256 points): one 4-wave
-// workgroup per (codeword, 256-byte chunk), 2048 waves for a 256-row sweep
-// instead of 512 single waves (2 per CU, VALU issue-bound at one wave per SIMD).
-//   S layout: wave w holds points e = 64w + j (j = 0..63): decoder IFFT layers
-//             d = 1..32 and FFT layers 32..1 (twiddles depend on w: one
+// Split decoder for M = 128 (65 <= k <= 128, n = 256 points): one NW-wave
+// workgroup per (codeword, 256-byte chunk), PW = 256 / NW points per wave.
+//   S layout: wave w holds points e = PW w + j (j < PW): decoder IFFT layers
+//             d < PW and FFT layers PW/2..1 (twiddles depend on w: one
 //             compile-time variant per wave, selected by a wave-uniform branch);
-//   L layout: wave w holds e = 4h + w (h = 0..63): IFFT layers 64, 128, the
-//             formal derivative and FFT layers 128, 64 (twiddles independent of w).
+//   L layout: wave w holds e = NW h + w (h < PW): IFFT layers PW..128, the formal
+//             derivative and FFT layers 128..PW (twiddles independent of w).
 // The derivative (closed form out[e] = in[e] ^ XOR_{t: e_t = 0} in[e + 2^t], see
-// derivative_half) needs, in L, the partners across bits 0 and 1 from the other
-// waves: all waves publish their post-IFFT points to LDS once, then each adds the
-// (original) partner values.  LDS: [256 points][64 lanes] dwords = 64 KiB, so two
-// workgroups share a CU.
+// derivative_half) needs, in L, the partners across the low log2(NW) bits from
+// the other waves: all waves publish their post-IFFT points to LDS once, then each
+// adds the (original) partner values.  LDS: [256 points][64 lanes] dwords = 64 KiB,
+// so two workgroups share a CU.  Production NW = 16 (8 waves per SIMD: the
+// shift/and/perm/xor chains of the byte-table multiplies need the latency cover;
+// c3 sweep 42.5 / 33.7 / 32.0 us at NW = 4 / 8 / 16).
 // ---------------------------------------------------------------------------
-template <int W>
-__device__ __forceinline__ void split_ifft_low(uint32_t (&v)[64]) { ifft_layers<64, 64 * W - 1>(v); }
-template <int W>
-__device__ __forceinline__ void split_fft_low(uint32_t (&v)[64]) { fft_layers<64, 64 * W - 1>(v); }
+template <int PW, int W>
+__device__ __forceinline__ void split_ifft_low(uint32_t (&v)[PW]) { ifft_layers<PW, PW * W - 1>(v); }
+template <int PW, int W>
+__device__ __forceinline__ void split_fft_low(uint32_t (&v)[PW]) { fft_layers<PW, PW * W - 1>(v); }
 
-// L layout: points 4h + w: the layer joining e and e + 64 pairs h and h + 16 (block
-// start b = 128 * (h >> 5)), the layer joining e and e + 128 pairs h and h + 32.
-__device__ __forceinline__ void split_ifft_high(uint32_t (&v)[64]) {
-    constexpr unsigned L64a = kGf8.skew[0 + 64 - 1], L64b = kGf8.skew[128 + 64 - 1], L128 = kGf8.skew[128 - 1];
-    static_for<16>([&](auto H) {
-        constexpr int h = decltype(H)::value;
-        ifft2<L64a>(v[h], v[h + 16]);
-        ifft2<L64b>(v[h + 32], v[h + 48]);
+// wave-uniform dispatch of the per-wave twiddle variant
+template <int NW, int PW, bool FFT>
+__device__ __forceinline__ void split_low(uint32_t (&v)[PW], uint32_t w) {
+    static_for<NW>([&](auto Wc) {
+        constexpr int W = decltype(Wc)::value;
+        if (w == (uint32_t)W) {
+            if constexpr (FFT) split_fft_low<PW, W>(v);
+            else split_ifft_low<PW, W>(v);
+        }
     });
-    static_for<32>([&](auto H) { ifft2<L128>(v[decltype(H)::value], v[decltype(H)::value + 32]); });
 }
-__device__ __forceinline__ void split_fft_high(uint32_t (&v)[64]) {
-    constexpr unsigned L64a = kGf8.skew[0 + 64 - 1], L64b = kGf8.skew[128 + 64 - 1], L128 = kGf8.skew[128 - 1];
-    static_for<32>([&](auto H) { fft2<L128>(v[decltype(H)::value], v[decltype(H)::value + 32]); });
-    static_for<16>([&](auto H) {
-        constexpr int h = decltype(H)::value;
-        fft2<L64a>(v[h], v[h + 16]);
-        fft2<L64b>(v[h + 32], v[h + 48]);
+
+// L layout, layer d >= PW: e = NW h + w, so the partner e + d is register h + d / NW
+// of the same wave; block start 2d * floor(e / 2d) = 2d * floor(h / (2d / NW)).
+template <int NW, int PW, bool FFT>
+__device__ __forceinline__ void split_high(uint32_t (&v)[PW]) {
+    static_for<8>([&](auto LG) {
+        constexpr int d = FFT ? (128 >> decltype(LG)::value) : (1 << decltype(LG)::value);
+        if constexpr (d >= PW && d <= 128) {
+            constexpr int sd = d / NW;
+            static_for<PW>([&](auto H) {
+                constexpr int h = decltype(H)::value;
+                if constexpr (((h / sd) & 1) == 0) {
+                    constexpr int b = 2 * d * (h / (2 * sd));
+                    constexpr unsigned L = kGf8.skew[b + d - 1];
+                    if constexpr (FFT) fft2<L>(v[h], v[h + sd]);
+                    else ifft2<L>(v[h], v[h + sd]);
+                }
+            });
+        }
     });
 }
 
@@ -466,13 +479,22 @@ __device__ __forceinline__ uint32_t gf8_mul_tab(uint32_t y, const PermTab& t) {
                 __builtin_amdgcn_perm(t.c, t.c, sc));
 }
 
+// bits [o, o + 64) of the 256-bit presence mask (zeros past the end)
+__device__ __forceinline__ uint64_t pres_bits(const uint64_t (&pres)[4], uint32_t o) {
+    const uint32_t q = o >> 6, r = o & 63u;
+    const uint64_t lo = q < 4u ? pres[q] >> r : 0ull;
+    const uint64_t hi = (r && q + 1u < 4u) ? pres[q + 1u] << (64u - r) : 0ull;
+    return lo | hi;
+}
+
 // per-point multiply tables of one codeword: [0] scale by err[e] (all-zero for an
 // absent point, so its bytes -- whatever the buffer holds -- enter as 0), [1]
 // reveal by 255 - err[e].  Written once by wave 0; every wave reads them with
 // uniform LDS broadcasts instead of a dependent scalar table load per point.
-template <bool ZC>
+template <int NW, bool ZC>
 __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t task, uint32_t (&xch)[256][64],
                                                   PermTab (&ptab)[2][256]) {
+    constexpr int PW = 256 / NW, HALF = NW / 2;
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t chunks = ds.chunks;
@@ -484,9 +506,9 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
     const uint64_t cell0 = ds.axis == 0 ? (uint64_t)vec * Wd : (uint64_t)vec;
     const uint64_t cell_step = ds.axis == 0 ? 1u : (uint64_t)Wd;
 
-    // This wave's points e = 64w + j are 64 consecutive cell positions: recovery
-    // (parity) i = e for w < 2, original (data) i = e - 128 for w >= 2; point j is
-    // valid when i < k.  From HBM their loads go out first (independent of the
+    // This wave's points e = PW w + j are PW consecutive cell positions: recovery
+    // (parity) i = e for w < NW/2, original (data) i = e - 128 for w >= NW/2; point j
+    // is valid when i < k.  From HBM their loads go out first (independent of the
     // presence mask and the error locator, whose latency they overlap; an absent
     // point's bytes are multiplied by zero).  Zero-copy (ZC: inputs from host-mapped
     // memory over PCIe), only the present points are read: the presence mask comes
@@ -496,15 +518,15 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(ds.base);
     const bool mirror = ds.mirror != nullptr;  // rebuilt cells also written there
     const __amdgpu_buffer_rsrc_t ri = make_rsrc(ZC ? ds.in_base : ds.base);
-    const uint32_t ib = (w & 1u) * 64u;
-    const uint32_t p0 = (w < 2u ? k : 0u) + ib;
-    const uint32_t nvalid = ib >= k ? 0u : (k - ib >= 64u ? 64u : k - ib);
+    const uint32_t ib = (w % HALF) * PW;
+    const uint32_t p0 = (w < HALF ? k : 0u) + ib;
+    const uint32_t nvalid = ib >= k ? 0u : (k - ib >= (uint32_t)PW ? (uint32_t)PW : k - ib);
     const uint32_t pbase = (uint32_t)((cell0 + (uint64_t)p0 * cell_step) * ds.S);
     const uint32_t pstep = (uint32_t)(cell_step * ds.S);
     const uint64_t valid = nvalid == 64u ? ~0ull : ((1ull << nvalid) - 1ull);
-    uint32_t v[64];
+    uint32_t v[PW];
     auto load_points = [&](uint64_t mask) {
-        static_for<64>([&](auto J) {
+        static_for<PW>([&](auto J) {
             constexpr int j = decltype(J)::value;
             const uint32_t so = ((mask >> j) & 1ull) ? pbase + (uint32_t)j * pstep : kOob;
             v[j] = __builtin_amdgcn_raw_buffer_load_b32(ri, off, so, 0);
@@ -520,26 +542,26 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
         pres[g] = __ballot(p);
     }
     auto present = [&](uint32_t e) -> bool { return (pres[e >> 6] >> (e & 63u)) & 1u; };
-    const uint64_t have = w < 2u ? (pres[(k + ib) >> 6] >> ((k + ib) & 63u)) | (((k + ib) & 63u) ? pres[((k + ib) >> 6) + 1] << (64u - ((k + ib) & 63u)) : 0ull)
-                                 : pres[ib >> 6];
-    if constexpr (ZC) load_points(valid & have);
+    const uint64_t have = pres_bits(pres, w < HALF ? k + ib : ib) & valid;
+    if constexpr (ZC) load_points(have);
 
-    // error locator (log domain), as decode_gf8_kernel: entries 4 lane .. 4 lane + 3
-    uint32_t er[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const uint32_t i = lane * 4u + j;
-        uint32_t x = 0;
-        if (i < k) x = present(k + i) ? 0u : 1u;
-        else if (i < 128u) x = 1u;
-        else if (i < 128u + k) x = present(i - 128u) ? 0u : 1u;
-        er[j] = x;
-    }
-    fwht256(er, lane);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) er[j] = (er[j] * d_gf8.logwalsh[lane * 4u + j]) % 255u;
-    fwht256(er, lane);
+    // error locator (log domain), as decode_gf8_kernel: entries 4 lane .. 4 lane + 3;
+    // wave 0 alone (it builds the per-point tables every wave reads)
     if (w == 0) {
+        uint32_t er[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t i = lane * 4u + j;
+            uint32_t x = 0;
+            if (i < k) x = present(k + i) ? 0u : 1u;
+            else if (i < 128u) x = 1u;
+            else if (i < 128u + k) x = present(i - 128u) ? 0u : 1u;
+            er[j] = x;
+        }
+        fwht256(er, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) er[j] = (er[j] * d_gf8.logwalsh[lane * 4u + j]) % 255u;
+        fwht256(er, lane);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint32_t e = lane * 4u + j;  // point e: a present, valid input?
@@ -550,63 +572,60 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
         }
     }
     if constexpr (ZC) {  // the present cells also land in the device square
-        const uint64_t keep = valid & have;
-        static_for<64>([&](auto J) {
+        static_for<PW>([&](auto J) {
             constexpr int j = decltype(J)::value;
-            const uint32_t so = ((keep >> j) & 1ull) ? pbase + (uint32_t)j * pstep : kOob;
+            const uint32_t so = ((have >> j) & 1ull) ? pbase + (uint32_t)j * pstep : kOob;
             __builtin_amdgcn_raw_buffer_store_b32(v[j], rs, off, so, 0);
         });
     }
     __syncthreads();
 
     // 1. S layout: scale every point by the error locator (absent -> 0)
-    static_for<64>([&](auto J) {
+    static_for<PW>([&](auto J) {
         constexpr int j = decltype(J)::value;
-        v[j] = gf8_mul_tab(v[j], ptab[0][64u * w + j]);
+        v[j] = gf8_mul_tab(v[j], ptab[0][PW * w + j]);
     });
-    // 2. IFFT layers 1..32 (per-wave twiddles)
-    if (w == 0) split_ifft_low<0>(v);
-    else if (w == 1) split_ifft_low<1>(v);
-    else if (w == 2) split_ifft_low<2>(v);
-    else split_ifft_low<3>(v);
+    // 2. IFFT layers 1..PW/2 (per-wave twiddles)
+    split_low<NW, PW, false>(v, w);
     // 3. S -> L
-    static_for<64>([&](auto J) { xch[64u * w + decltype(J)::value][lane] = v[decltype(J)::value]; });
+    static_for<PW>([&](auto J) { xch[PW * w + decltype(J)::value][lane] = v[decltype(J)::value]; });
     __syncthreads();
-    static_for<64>([&](auto H) { v[decltype(H)::value] = xch[4u * decltype(H)::value + w][lane]; });
+    static_for<PW>([&](auto H) { v[decltype(H)::value] = xch[NW * decltype(H)::value + w][lane]; });
     __syncthreads();
-    // 4. IFFT layers 64, 128; formal derivative
-    split_ifft_high(v);
-    static_for<64>([&](auto H) { xch[4u * decltype(H)::value + w][lane] = v[decltype(H)::value]; });
+    // 4. IFFT layers PW..128; formal derivative
+    split_high<NW, PW, false>(v);
+    static_for<PW>([&](auto H) { xch[NW * decltype(H)::value + w][lane] = v[decltype(H)::value]; });
     __syncthreads();
-    static_for<64>([&](auto H) {  // partners across bits 2..7: same wave, registers h + 2^s
+    static_for<PW>([&](auto H) {  // partners across the high bits: same wave, registers h + 2^t
         constexpr int h = decltype(H)::value;
-        static_for<6>([&](auto T) {
+        static_for<8>([&](auto T) {
             constexpr int t = decltype(T)::value;
-            if constexpr (((h >> t) & 1) == 0) v[h] ^= v[h + (1 << t)];
+            if constexpr ((1 << t) < PW && ((h >> t) & 1) == 0) v[h] ^= v[h + (1 << t)];
         });
     });
-    if ((w & 1u) == 0)  // bit 0 of the point is 0: add point e + 1 (wave w + 1)
-        static_for<64>([&](auto H) { v[decltype(H)::value] ^= xch[4u * decltype(H)::value + w + 1][lane]; });
-    if ((w & 2u) == 0)  // bit 1 is 0: add point e + 2 (wave w + 2)
-        static_for<64>([&](auto H) { v[decltype(H)::value] ^= xch[4u * decltype(H)::value + w + 2][lane]; });
-    // 5. FFT layers 128, 64; L -> S
-    split_fft_high(v);
+    static_for<8>([&](auto B) {  // partners across the low bits: wave w + 2^b (bit b of e is 0)
+        constexpr int bit = 1 << decltype(B)::value;
+        if constexpr (bit < NW)
+            if ((w & (uint32_t)bit) == 0)
+                static_for<PW>([&](auto H) {
+                    v[decltype(H)::value] ^= xch[NW * decltype(H)::value + w + bit][lane];
+                });
+    });
+    // 5. FFT layers 128..PW; L -> S
+    split_high<NW, PW, true>(v);
     __syncthreads();
-    static_for<64>([&](auto H) { xch[4u * decltype(H)::value + w][lane] = v[decltype(H)::value]; });
+    static_for<PW>([&](auto H) { xch[NW * decltype(H)::value + w][lane] = v[decltype(H)::value]; });
     __syncthreads();
-    static_for<64>([&](auto J) { v[decltype(J)::value] = xch[64u * w + decltype(J)::value][lane]; });
-    // 6. FFT layers 32..1; reveal the missing points of this wave
-    if (w == 0) split_fft_low<0>(v);
-    else if (w == 1) split_fft_low<1>(v);
-    else if (w == 2) split_fft_low<2>(v);
-    else split_fft_low<3>(v);
+    static_for<PW>([&](auto J) { v[decltype(J)::value] = xch[PW * w + decltype(J)::value][lane]; });
+    // 6. FFT layers PW/2..1; reveal the missing points of this wave
+    split_low<NW, PW, true>(v, w);
     const uint64_t reveal = valid & ~have;
     const __amdgpu_buffer_rsrc_t rm = make_rsrc(mirror ? ds.mirror : ds.base);
     uint32_t sbase = pbase, sstep = pstep;
     asm volatile("" : "+s"(sbase), "+s"(sstep));
-    static_for<64>([&](auto J) {
+    static_for<PW>([&](auto J) {
         constexpr int j = decltype(J)::value;
-        const uint32_t e = 64u * w + j;
+        const uint32_t e = PW * w + j;
         const uint32_t so = ((reveal >> j) & 1ull) ? sbase + (uint32_t)j * sstep : kOob;
         const uint32_t x = gf8_mul_tab(v[j], ptab[1][e]);
         __builtin_amdgcn_raw_buffer_store_b32(x, rs, off, so, 0);
@@ -614,20 +633,24 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
     });
 }
 
+constexpr int kSplitWaves = 16;
+
 // one workgroup per task (device-resident square)
-__global__ __launch_bounds__(256, 2) void decode_gf8_split_kernel(DecodeSet ds) {
+template <int NW>
+__global__ __launch_bounds__(64 * NW, NW / 2) void decode_gf8_split_kernel(DecodeSet ds) {
     __shared__ uint32_t xch[256][64];
     __shared__ PermTab ptab[2][256];
-    decode_split_task<false>(ds, blockIdx.x, xch, ptab);
+    decode_split_task<NW, false>(ds, blockIdx.x, xch, ptab);
 }
 
 // zero-copy form: a capped grid loops over the tasks
-__global__ __launch_bounds__(256, 2) void decode_gf8_split_zc_kernel(DecodeSet ds) {
+template <int NW>
+__global__ __launch_bounds__(64 * NW, NW / 2) void decode_gf8_split_zc_kernel(DecodeSet ds) {
     __shared__ uint32_t xch[256][64];
     __shared__ PermTab ptab[2][256];
     const uint32_t tasks = ds.count * ds.chunks;
     for (uint32_t task = blockIdx.x; task < tasks; task += gridDim.x) {
-        decode_split_task<true>(ds, __builtin_amdgcn_readfirstlane(task), xch, ptab);
+        decode_split_task<NW, true>(ds, __builtin_amdgcn_readfirstlane(task), xch, ptab);
         __syncthreads();  // LDS (xch, ptab) is reused by the next task
     }
 }
@@ -683,14 +706,16 @@ static hipError_t launch_dec(const DecodeSet& ds, hipStream_t st) {
 }
 
 hipError_t launch_decode_gf8(const DecodeSet& ds, hipStream_t st) {
-    if (ceil_pow2(ds.k) == 128) {  // split form: 4 waves per (codeword, 256 B chunk)
+    if (ceil_pow2(ds.k) == 128) {  // split form: kSplitWaves waves per (codeword, 256 B chunk)
         const uint64_t tasks = (uint64_t)ds.count * ds.chunks;
         if (tasks == 0) return hipSuccess;
         if (ds.in_base) {
+            // zero-copy: PCIe-bound; 4 waves (8 would spill the loop's extra registers)
             const uint32_t grid = ds.grid && ds.grid < tasks ? ds.grid : (uint32_t)tasks;
-            hipLaunchKernelGGL(decode_gf8_split_zc_kernel, dim3(grid), dim3(256), 0, st, ds);
+            hipLaunchKernelGGL(decode_gf8_split_zc_kernel<4>, dim3(grid), dim3(256), 0, st, ds);
         } else {
-            hipLaunchKernelGGL(decode_gf8_split_kernel, dim3((uint32_t)tasks), dim3(256), 0, st, ds);
+            constexpr int NW = kSplitWaves;
+            hipLaunchKernelGGL(decode_gf8_split_kernel<NW>, dim3((uint32_t)tasks), dim3(64 * NW), 0, st, ds);
         }
         return hipGetLastError();
     }
