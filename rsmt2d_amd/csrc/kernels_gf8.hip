@@ -533,6 +533,12 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
         });
     };
     if constexpr (!ZC) load_points(valid);
+    // wave 0's error-locator weights, loaded with the points (off the critical path)
+    uint32_t lw[4] = {0, 0, 0, 0};
+    if (w == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) lw[j] = d_gf8.logwalsh[lane * 4u + j];
+    }
 
     uint64_t pres[4];
 #pragma unroll
@@ -560,7 +566,7 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
         }
         fwht256(er, lane);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) er[j] = (er[j] * d_gf8.logwalsh[lane * 4u + j]) % 255u;
+        for (int j = 0; j < 4; ++j) er[j] = (er[j] * lw[j]) % 255u;
         fwht256(er, lane);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
