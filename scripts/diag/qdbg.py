@@ -1,3 +1,12 @@
+"""Locates wrong cells of the single-launch queue extension (diagnostic library).
+
+For a few (count, delay) shapes: extends with the two-launch form and with
+rsm_diag_extend_fused twice on the same queue words, and prints, per quadrant, the
+rows/columns that differ and whether the differing cells still hold the untouched
+source bytes (a set never processed) or something else (a set processed from stale
+inputs).  Written while finding the round-2g dropped-claim bug.
+usage: python3 scripts/diag/qdbg.py   (on a GPU box)
+"""
 import ctypes, sys, os
 sys.path.insert(0, os.getcwd())
 import numpy as np
