@@ -533,7 +533,10 @@ __device__ __forceinline__ void bs_queue_wave(const QueuePlan& p, uint32_t* lds,
     // (both before the first exchange).  MODE 4096: Q1 read with the default policy.
     constexpr bool ADDTID = (MODE & 8) != 0, ARITH = !(MODE & 2), EARLY = (MODE & 256) != 0,
                    NTQ0 = (MODE & 512) != 0, NTQ1 = !(MODE & 4096);
-    constexpr int DPOS = EARLY ? 0 : (MODE & 1024) ? 4 : (MODE & 2048) ? 5 : (MODE & 64) ? 1 : (MODE & 128) ? 3 : 2;
+    // MODE 8192 (with 2048): row sets after the small IFFT layers, column sets right
+    // after the first exchange; 16384 (with 2048): the other way round (A/B)
+    constexpr int DPOS = (MODE & 8192) ? 6 : (MODE & 16384) ? 7 : EARLY ? 0 : (MODE & 1024) ? 4 : (MODE & 2048) ? 5
+                       : (MODE & 64) ? 1 : (MODE & 128) ? 3 : 2;
     const bool MEM = !(MODE & 4) || p.rows.S == 1;  // runtime-false in mode 4 (keeps the code alive)
     const uint32_t lane = threadIdx.x & 63u;
     const bool t0 = threadIdx.x == 0;
@@ -633,7 +636,7 @@ __device__ __forceinline__ void bs_queue_wave(const QueuePlan& p, uint32_t* lds,
                 if constexpr (DPOS == 0) issue_direct(nrow, nxt & kQ1, an);
             }
             // direct loads issued since the previous set's stores, at the publish point
-            const bool dearly = pre && (DPOS <= 1 || DPOS >= 4 || (DPOS == 3 && nrow));
+            const bool dearly = pre && (DPOS <= 1 || DPOS >= 4 || (DPOS == 3 && nrow));  // all issued by the publish point
             // no claim in a workgroup's last set (nothing would take the item)
             if (t0) cand = more ? q_claim(p, qc) : kNone;
 
@@ -643,9 +646,13 @@ __device__ __forceinline__ void bs_queue_wave(const QueuePlan& p, uint32_t* lds,
             if constexpr (ARITH) bs8::small_ifft_all(X, A);
             if constexpr (DPOS == 5)
                 if (pre) issue_direct(nrow, nxt & kQ1, an);
+            if constexpr (DPOS == 6 || DPOS == 7)
+                if (pre && ((DPOS == 6) == (nrow != 0))) issue_direct(nrow, nxt & kQ1, an);
             bs8::sfor<8>([&](auto Pp) { xch_to_large<decltype(Pp)::value, ADDTID>(X, e_small, s_small, e_large); });
             if constexpr (DPOS == 1 || DPOS == 3)
                 if (pre && (DPOS == 1 || nrow)) issue_direct(nrow, nxt & kQ1, an);
+            if constexpr (DPOS == 6 || DPOS == 7)
+                if (pre && ((DPOS == 6) != (nrow != 0))) issue_direct(nrow, nxt & kQ1, an);
             if constexpr (ARITH) bs8::large_ifft_fft(X);
 
             // publish the row set stored at the end of the previous set (its stores
@@ -1008,11 +1015,12 @@ bool bs128_queue_applicable(const CodewordSet& rows, const CodewordSet& cols) {
     return bs128_applicable(rows) && bs128_applicable(cols);
 }
 
-// Production: MODE 2088 (ds_write_addtid_b32 exchange, the direct half of the next
-// set's loads after the small IFFT layers, just before the first exchange).  Measured
-// (profiles/r02g_queue_ab.jsonl, 3 streams, same box): 256 squares per step 8.43 us
-// per square against 8.57-8.59 right after the first exchange (MODE 104) and 8.73 right
-// after the transposes; at 128 squares 104 gave 8.80-8.89 against 9.08 after the large
+// Production: MODE 18472 (ds_write_addtid_b32 exchange; the direct half of the next
+// set's loads after the small IFFT layers for a column set, right after the first
+// exchange for a row set).  Measured (profiles/r02g_queue_ab.jsonl, 3 streams, same
+// box): 256 squares per step 8.53 us per square against 8.59-8.60 with both after the
+// small IFFT layers (MODE 2088), 8.68-8.76 the other way round; 2088 against 104 (both
+// right after the first exchange) 8.43 vs 8.57-8.59, 8.73 right after the transposes; at 128 squares 104 gave 8.80-8.89 against 9.08 after the large
 // layers and 9.52 at the top of the set; Q0 read non-temporal +3 %, Q1 read with the
 // default policy +3 % (the Infinity-Cache re-read of Q0 needs the default policy, the
 // last read of Q1 is best non-temporal).
@@ -1025,10 +1033,12 @@ hipError_t launch_extend_gf8_bs128_queue(const QueuePlan& p, hipStream_t st) {
     // diagnostic codes: 2 / 4 no arithmetic / no memory (wrong output by design);
     // 104 direct loads right after the first exchange, 140 after the large layers,
     // 168 rows early / columns late, 296 at the top of the set, 616 = 104 + Q0
-    // non-temporal, 1064 after the transposes, 4200 = 104 + Q1 default policy
+    // non-temporal, 1064 after the transposes, 2088 after the small IFFT layers,
+    // 4200 = 104 + Q1 default policy, 10280 rows after the small IFFT / columns after
+    // the exchange
     switch (g_diag_mode.load()) {
-        case 2: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<2090>), dim3(grid), dim3(512), 0, st, p); break;
-        case 4: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<2092>), dim3(grid), dim3(512), 0, st, p); break;
+        case 2: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<18474>), dim3(grid), dim3(512), 0, st, p); break;
+        case 4: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<18476>), dim3(grid), dim3(512), 0, st, p); break;
         case 104: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<104>), dim3(grid), dim3(512), 0, st, p); break;
         case 140: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<40>), dim3(grid), dim3(512), 0, st, p); break;
         case 168: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<168>), dim3(grid), dim3(512), 0, st, p); break;
@@ -1036,10 +1046,12 @@ hipError_t launch_extend_gf8_bs128_queue(const QueuePlan& p, hipStream_t st) {
         case 616: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<616>), dim3(grid), dim3(512), 0, st, p); break;
         case 1064: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<1064>), dim3(grid), dim3(512), 0, st, p); break;
         case 4200: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<4200>), dim3(grid), dim3(512), 0, st, p); break;
-        default: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<2088>), dim3(grid), dim3(512), 0, st, p); break;
+        case 10280: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<10280>), dim3(grid), dim3(512), 0, st, p); break;
+        case 2088: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<2088>), dim3(grid), dim3(512), 0, st, p); break;
+        default: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<18472>), dim3(grid), dim3(512), 0, st, p); break;
     }
 #else
-    hipLaunchKernelGGL((extend_gf8_bs128q_kernel<2088>), dim3(grid), dim3(512), 0, st, p);
+    hipLaunchKernelGGL((extend_gf8_bs128q_kernel<18472>), dim3(grid), dim3(512), 0, st, p);
 #endif
     return hipGetLastError();
 }
