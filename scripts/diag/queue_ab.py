@@ -1,7 +1,7 @@
 """Single-launch queue schedule vs the production two-launch schedule, c2 (k=128, S=512).
 
-Configurations "kind,B,streams,delay": kind "two" = production rsm_extend_squares_dev
-(row pass + column pass), kind "queue" = rsm_diag_extend_fused (extend_gf8_bs128q_kernel,
+Configurations "kind,B,streams,delay": kind "two" = the round-1 two-launch schedule
+(rsm_extend_squares_phase_dev row pass + column pass), kind "queue" = rsm_diag_extend_fused (extend_gf8_bs128q_kernel,
 diagnostic library).  Steps of B squares rotate over 2 buffers and `streams` streams;
 the first and last square of the last step are checked against the oracle, and the
 queue's stuck-wait word is checked.  One JSON line per configuration.
@@ -76,8 +76,9 @@ def run(cfg, steps=STEPS, warmup=6):
             chk(D.rsm_event_create(ctx, ctypes.byref(e1)))
             evs.append((e0, e1))
             chk(D.rsm_event_record(ctx, e0, st))
-        if kind == "two":
-            chk(D.rsm_extend_squares_dev(ctx, bufs[i % nb], k, S, B, st))
+        if kind == "two":  # the two launches explicitly (rsm_extend_squares_dev takes the queue path)
+            chk(D.rsm_extend_squares_phase_dev(ctx, bufs[i % nb], k, S, B, 1, st))
+            chk(D.rsm_extend_squares_phase_dev(ctx, bufs[i % nb], k, S, B, 2, st))
         else:
             chk(D.rsm_diag_extend_fused(ctx, bufs[i % nb], k, S, B, delay, st))
         if timed and EVENTS:
