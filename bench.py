@@ -543,7 +543,11 @@ def main():
         nstep[0] += 1
         st, b = streams[i % len(streams)], bufs[i % len(bufs)].ptr
         if ev is None:
-            R._check(L.rsm_extend_squares_dev(ctx, b, k, S, B, st))
+            if single:
+                R._check(L.rsm_extend_squares_dev(ctx, b, k, S, B, st))
+            else:  # the two launches (rsm_extend_squares_dev would take the queue path)
+                R._check(L.rsm_extend_squares_phase_dev(ctx, b, k, S, B, 1, st))
+                R._check(L.rsm_extend_squares_phase_dev(ctx, b, k, S, B, 2, st))
             return
         if single:
             # the production step: ONE launch (both passes), an event either side
