@@ -669,7 +669,10 @@ def main():
             sets = (W if col_dom else k) * B * S // 2048
         grid_threads = min(sets, 256) * 512  # persistent grid: one 512-thread workgroup per CU
         for row in json.load(open(pmc_path)).get("launches", []):
-            if want in row["kernel"] and row["grid_threads"] == grid_threads:
+            # persistent launches of every batch size share one grid: accept the row
+            # only if it is plausibly this batch (0.9x - 2x the algorithmic bytes)
+            if want in row["kernel"] and row["grid_threads"] == grid_threads and \
+                    0.9 <= row["traffic_bytes"] / dominant[1] <= 2.0:
                 traffic = int(row["traffic_bytes"])
     us = lambda x: round(x * 1e6, 2)
     out = {
