@@ -101,7 +101,8 @@ int rsm_host_free(rsm_ctx* ctx, void* p);
  * library's HIP runtime; NULL = the context stream); asynchronous.  Batches of
  * >= 2 squares with k = 128 run both passes as ONE queue-driven launch; its
  * bounded waits cannot time out short of a hardware fault, and if one did, the
- * next rsm_sync (or the next extension on that stream) returns RSM_EDEVICE. */
+ * stream's next rsm_stream_check (rsm_sync for the context stream), its
+ * rsm_stream_destroy or the next extension on that stream returns RSM_EDEVICE. */
 int rsm_extend_squares_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size, uint32_t count,
                            void* stream);
 /* One phase of the above: phase 1 = row pass (Q0 -> Q1), phase 2 = column pass
@@ -179,6 +180,9 @@ int rsm_memcpy(rsm_ctx* ctx, void* dst, const void* src, uint64_t bytes, int kin
 /* SplitMix64 byte stream (seeded synthetic shares), asynchronous on the ctx stream. */
 int rsm_dev_fill_random(rsm_ctx* ctx, void* d, uint64_t bytes, uint64_t seed);
 int rsm_sync(rsm_ctx* ctx);
+/* *equal = 1 iff the device buffers a and b (bytes a multiple of 16) are equal,
+ * compared on the device (a kernel on `stream`, NULL = context stream); synchronous. */
+int rsm_dev_equal(rsm_ctx* ctx, const void* a, const void* b, uint64_t bytes, void* stream, int* equal);
 /* Extra HIP streams on the context's device, for callers that pipeline independent
  * batches (e.g. step n's column pass beside step n+1's row pass on another
  * stream).  Each stream owns its device scratch (GF(2^16) work arrays, leaf
@@ -186,6 +190,10 @@ int rsm_sync(rsm_ctx* ctx);
 int rsm_stream_create(rsm_ctx* ctx, void** out);
 int rsm_stream_destroy(rsm_ctx* ctx, void* stream);
 int rsm_stream_sync(void* stream);
+/* Waits for `stream` (NULL = context stream) and returns RSM_EDEVICE (clearing it)
+ * if a queue-driven extension on it reported a stuck wait; rsm_sync does the same
+ * for the context stream only. */
+int rsm_stream_check(rsm_ctx* ctx, void* stream);
 /* HIP events on the context's device, for timing launches inside a caller's loop
  * (NULL stream = context stream).  rsm_event_elapsed_ms waits for `end`. */
 int rsm_event_create(rsm_ctx* ctx, void** out);

@@ -158,6 +158,8 @@ SIGNATURES = {
     "rsm_stream_create": (_I32, [_VP, ctypes.POINTER(_VP)]),
     "rsm_stream_destroy": (_I32, [_VP, _VP]),
     "rsm_stream_sync": (_I32, [_VP]),
+    "rsm_stream_check": (_I32, [_VP, _VP]),
+    "rsm_dev_equal": (_I32, [_VP, _VP, _VP, _U64, _VP, ctypes.POINTER(ctypes.c_int)]),
     "rsm_time_extend": (_I32, [_VP, _VP, _U32, _U32, _U32, _U32, ctypes.POINTER(ctypes.c_float),
                                ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
     "rsm_default_tree_root": (_I32, [_VP, _I32, _U32, _VP, _U32, _U32, _VP, _VP]),
@@ -422,13 +424,31 @@ def NewDefaultTree(axis: int = Row, index: int = 0):
 
 
 class _NmtTree(Tree):
-    """Host Tree of the erasured NMT (Push collects, Root hashes via rsm_nmt_tree_root)."""
+    """Host Tree of the erasured NMT (Push validates and collects, Root hashes via
+    rsm_nmt_tree_root).  Push reports the wrapper's errors where the reference does
+    (nmtwrapper_test.go:103-108: share or axis index past 2*squareSize, data shorter
+    than the namespace) and the NMT's namespace push-order error (celestiaorg/nmt
+    v0.24.3 Push: namespaces must not decrease; the parity namespace 0xFF.. is the
+    largest)."""
 
     def __init__(self, params: "NmtParams", axis: int, index: int):
         self._p, self._axis, self._index, self._leaves = params, axis, index, []
+        self._last_ns = None
 
     def Push(self, data: bytes):
-        self._leaves.append(bytes(data))
+        ns, n = self._p.namespace_size, int(self._p.square_size)
+        share = len(self._leaves)
+        if self._index + 1 > 2 * n or share + 1 > 2 * n:
+            raise RSMError(RSM_EINVAL, f"pushed past predetermined square size: boundary at {2 * n} index at "
+                                       f"{self._index} {share}")
+        data = bytes(data)
+        if len(data) < ns:
+            raise RSMError(RSM_EINVAL, "data is too short to contain namespace ID")
+        nid = data[:ns] if (share < n and self._index < n) else b"\xff" * ns
+        if self._last_ns is not None and nid < self._last_ns:
+            raise RSMError(RSM_EINVAL, "pushed data has to be lexicographically ordered by namespace IDs")
+        self._last_ns = nid
+        self._leaves.append(data)
 
     def Root(self) -> bytes:
         keep, ptrs, _ = _bufs(self._leaves) if self._leaves else ([], None, None)

@@ -485,6 +485,10 @@ __device__ __forceinline__ uint32_t q_take(const QueuePlan& p, QClaim& c, bool w
     const uint32_t q = it & ~kQ1;
     if (wait) {
         sq = q_wait(p, kQ1 | q);
+        if (sq == kNone) {  // stuck (error word set): take nothing, leave
+            sq = 0u;
+            return kNone;
+        }
     } else {
         sq = q_ready(p, q);
         if (sq == kNone) {
@@ -497,14 +501,15 @@ __device__ __forceinline__ uint32_t q_take(const QueuePlan& p, QClaim& c, bool w
     return kQ1 | q;
 }
 
-// Bounded wait for Q1 item `it`; returns its square.
+// Bounded wait for Q1 item `it`; returns its square, or kNone when the wait timed
+// out (the error word is set; the caller skips the set -- no loads, no stores -- so
+// a stuck wait corrupts no square, and the launch still drains).
 __device__ __forceinline__ uint32_t q_wait(const QueuePlan& p, uint32_t it) {
     uint32_t s = kNone;
     for (uint32_t n = 0; (s = q_ready(p, it & ~kQ1)) == kNone; ++n) {
         if (n >= kSpinLimit) {
             q_store(&p.ctr[kQErr], 1u);
-            s = 0u;
-            break;
+            return kNone;
         }
         __builtin_amdgcn_s_sleep(4);
     }
@@ -533,6 +538,9 @@ __device__ __forceinline__ void bs_queue_wave(const QueuePlan& p, uint32_t* lds,
     // (both before the first exchange).  MODE 4096: Q1 read with the default policy.
     constexpr bool ADDTID = (MODE & 8) != 0, ARITH = !(MODE & 2), EARLY = (MODE & 256) != 0,
                    NTQ0 = (MODE & 512) != 0, NTQ1 = !(MODE & 4096);
+    // diagnostics (wrong output by design): 32768 no LDS exchange, 65536 no byte<->plane
+    // transposes, 131072 no butterflies
+    constexpr bool XCH = !(MODE & 32768), TRP = ARITH && !(MODE & 65536), BFL = ARITH && !(MODE & 131072);
     // MODE 8192 (with 2048): row sets after the small IFFT layers, column sets right
     // after the first exchange; 16384 (with 2048): the other way round (A/B)
     constexpr int DPOS = (MODE & 8192) ? 6 : (MODE & 16384) ? 7 : EARLY ? 0 : (MODE & 1024) ? 4 : (MODE & 2048) ? 5
@@ -640,20 +648,20 @@ __device__ __forceinline__ void bs_queue_wave(const QueuePlan& p, uint32_t* lds,
             // no claim in a workgroup's last set (nothing would take the item)
             if (t0) cand = more ? q_claim(p, qc) : kNone;
 
-            if constexpr (ARITH) bs8::sfor<16>([&](auto J) { bs8::transpose8_dev(X[decltype(J)::value]); });
+            if constexpr (TRP) bs8::sfor<16>([&](auto J) { bs8::transpose8_dev(X[decltype(J)::value]); });
             if constexpr (DPOS == 4)
                 if (pre) issue_direct(nrow, nxt & kQ1, an);
-            if constexpr (ARITH) bs8::small_ifft_all(X, A);
+            if constexpr (BFL) bs8::small_ifft_all(X, A);
             if constexpr (DPOS == 5)
                 if (pre) issue_direct(nrow, nxt & kQ1, an);
             if constexpr (DPOS == 6 || DPOS == 7)
                 if (pre && ((DPOS == 6) == (nrow != 0))) issue_direct(nrow, nxt & kQ1, an);
-            bs8::sfor<8>([&](auto Pp) { xch_to_large<decltype(Pp)::value, ADDTID>(X, e_small, s_small, e_large); });
+            if constexpr (XCH) bs8::sfor<8>([&](auto Pp) { xch_to_large<decltype(Pp)::value, ADDTID>(X, e_small, s_small, e_large); });
             if constexpr (DPOS == 1 || DPOS == 3)
                 if (pre && (DPOS == 1 || nrow)) issue_direct(nrow, nxt & kQ1, an);
             if constexpr (DPOS == 6 || DPOS == 7)
                 if (pre && ((DPOS == 6) != (nrow != 0))) issue_direct(nrow, nxt & kQ1, an);
-            if constexpr (ARITH) bs8::large_ifft_fft(X);
+            if constexpr (BFL) bs8::large_ifft_fft(X);
 
             // publish the row set stored at the end of the previous set (its stores
             // were issued before this set's loads: wait for them only); the counter
@@ -695,8 +703,8 @@ __device__ __forceinline__ void bs_queue_wave(const QueuePlan& p, uint32_t* lds,
                 qc.qh = q_load(&p.ctr[kQHead1]);
             }
             if (pre && (DPOS == 2 || (DPOS == 3 && !nrow))) issue_direct(nrow, nxt & kQ1, an);
-            bs8::sfor<8>([&](auto Pp) { xch_to_small<decltype(Pp)::value, ADDTID>(X, e_large, s_large, e_small); });
-            if constexpr (ARITH) bs8::small_fft_all(X, A);
+            if constexpr (XCH) bs8::sfor<8>([&](auto Pp) { xch_to_small<decltype(Pp)::value, ADDTID>(X, e_large, s_large, e_small); });
+            if constexpr (BFL) bs8::small_fft_all(X, A);
             if (t0) {
                 asm volatile("" : "+v"(sig), "+v"(rv));
                 if (sig_sq != kNone) {
@@ -737,7 +745,7 @@ __device__ __forceinline__ void bs_queue_wave(const QueuePlan& p, uint32_t* lds,
                 const bool rs = crow != 0;
                 bs8::sfor<16>([&](auto J) {
                     constexpr int j = decltype(J)::value;
-                    if constexpr (ARITH) bs8::transpose8_dev(X[j]);
+                    if constexpr (TRP) bs8::transpose8_dev(X[j]);
                     const uint32_t so = sym_off(16u * A + j, k, oo, es);
                     v4u x, y;
                     x.x = X[j][0]; x.y = X[j][1]; x.z = X[j][2]; x.w = X[j][3];
@@ -766,6 +774,7 @@ __device__ __forceinline__ void bs_queue_wave(const QueuePlan& p, uint32_t* lds,
                 pend = kNone;
                 asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
                 nsq = __builtin_amdgcn_readfirstlane(lds[3]);
+                if (nsq == kNone) break;  // stuck wait: skip the set, drain
                 q_item(p, nxt, nsq, nrow, nset);
                 an = addr(nrow, nset);
                 issue_dma(nrow, nxt & kQ1, an);
@@ -1048,6 +1057,11 @@ hipError_t launch_extend_gf8_bs128_queue(const QueuePlan& p, hipStream_t st) {
         case 4200: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<4200>), dim3(grid), dim3(512), 0, st, p); break;
         case 10280: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<10280>), dim3(grid), dim3(512), 0, st, p); break;
         case 2088: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<2088>), dim3(grid), dim3(512), 0, st, p); break;
+        case 32768: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<18472 | 32768>), dim3(grid), dim3(512), 0, st, p); break;
+        case 65536: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<18472 | 65536>), dim3(grid), dim3(512), 0, st, p); break;
+        case 131072: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<18472 | 131072>), dim3(grid), dim3(512), 0, st, p); break;
+        case 98304: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<18472 | 98304>), dim3(grid), dim3(512), 0, st, p); break;
+        case 32772: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<18476 | 32768>), dim3(grid), dim3(512), 0, st, p); break;
         default: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<18472>), dim3(grid), dim3(512), 0, st, p); break;
     }
 #else

@@ -116,6 +116,7 @@ namespace rsm {
 // Lane pool: blocks while all kMaxLanes lanes are busy.
 Lane* acquire_lane(rsm_ctx* ctx, int* rc);
 void release_lane(rsm_ctx* ctx, Lane* l);
+int acquire_lanes(rsm_ctx* ctx, int n, Lane** out);
 struct LaneGuard {
     rsm_ctx* ctx;
     Lane* lane;

@@ -110,6 +110,34 @@ Lane* acquire_lane(rsm_ctx* ctx, int* rc) {
     }
 }
 
+// n lanes in one step: waits (holding none) until n are free or can be created, so
+// callers that each need several lanes never deadlock holding part of a set.
+int acquire_lanes(rsm_ctx* ctx, int n, Lane** out) {
+    if (n <= 0 || (size_t)n > rsm_ctx::kMaxLanes) return fail(RSM_EINVAL, "acquire_lanes: bad lane count %d", n);
+    std::unique_lock<std::mutex> lk(ctx->lane_mu);
+    ctx->lane_cv.wait(lk, [&] {
+        return ctx->free_lanes.size() + (rsm_ctx::kMaxLanes - ctx->lanes.size()) >= (size_t)n;
+    });
+    int got = 0;
+    while (got < n && !ctx->free_lanes.empty()) {
+        out[got++] = ctx->free_lanes.back();
+        ctx->free_lanes.pop_back();
+    }
+    while (got < n) {
+        auto l = std::make_unique<Lane>();
+        hipError_t e = hipStreamCreateWithFlags(&l->stream, hipStreamNonBlocking);
+        if (e != hipSuccess) {
+            for (int i = 0; i < got; ++i) ctx->free_lanes.push_back(out[i]);
+            lk.unlock();
+            ctx->lane_cv.notify_all();
+            return hip_fail(e, "hipStreamCreate (lane)");
+        }
+        ctx->lanes.push_back(std::move(l));
+        out[got++] = ctx->lanes.back().get();
+    }
+    return RSM_OK;
+}
+
 void release_lane(rsm_ctx* ctx, Lane* l) {
     {
         std::lock_guard<std::mutex> lk(ctx->lane_mu);
@@ -666,24 +694,35 @@ int rsm_extend_squares_host(rsm_ctx* ctx, const uint8_t* ods, uint32_t k, uint32
     if (int rc = use_device(ctx)) return rc;
     constexpr int kLanes = 3;
     const int nl = (int)std::min<uint32_t>(count, kLanes);
-    std::unique_ptr<LaneGuard> g[kLanes];
-    for (int i = 0; i < nl; ++i) {
-        g[i] = std::make_unique<LaneGuard>(ctx);
-        if (!g[i]->lane) return g[i]->rc;
-    }
+    Lane* lanes[kLanes] = {};
+    // all lanes in one step (a caller holding some while waiting for more could
+    // deadlock against other multi-lane callers); released on every return path,
+    // after their streams have drained
+    if (int rc = acquire_lanes(ctx, nl, lanes)) return rc;
+    struct Release {
+        rsm_ctx* ctx;
+        Lane** l;
+        int n;
+        ~Release() {
+            for (int i = 0; i < n; ++i) {
+                (void)hipStreamSynchronize(l[i]->stream);
+                release_lane(ctx, l[i]);
+            }
+        }
+    } rel{ctx, lanes, nl};
     const size_t S = share_size, W = 2ull * k, ods_b = (size_t)k * k * S, eds_b = W * W * S;
     hipError_t e;
     for (int i = 0; i < nl; ++i)
-        if ((e = g[i]->lane->dev.ensure(eds_b)) != hipSuccess) return hip_fail(e, "hipMalloc");
+        if ((e = lanes[i]->dev.ensure(eds_b)) != hipSuccess) return hip_fail(e, "hipMalloc");
     for (uint32_t i = 0; i < count; ++i) {
-        Lane& L = *g[i % nl]->lane;
+        Lane& L = *lanes[i % nl];
         if (int rc = host_square(ctx, ods + i * ods_b, (size_t)k * S, eds + i * eds_b, static_cast<uint8_t*>(L.dev.ptr),
                                  k, share_size, L.stream))
             return rc;
         fill_q0(ods + i * ods_b, eds + i * eds_b, k, share_size);
     }
     for (int i = 0; i < nl; ++i)
-        if ((e = hipStreamSynchronize(g[i]->lane->stream)) != hipSuccess) return hip_fail(e, "extend (host batch)");
+        if ((e = hipStreamSynchronize(lanes[i]->stream)) != hipSuccess) return hip_fail(e, "extend (host batch)");
     return RSM_OK;
 }
 
@@ -899,12 +938,47 @@ int rsm_stream_destroy(rsm_ctx* ctx, void* stream) {
     if (int rc = use_device(ctx)) return rc;
     hipStream_t st = static_cast<hipStream_t>(stream);
     (void)hipStreamSynchronize(st);
+    // the stream's stuck-wait report is read before its scratch (which holds the
+    // report word) is released, so a failed launch is never lost
+    const int rep = check_queue_reports(ctx, st);
     {
         std::lock_guard<std::mutex> lk(ctx->scratch_mu);
         ctx->scratch.erase(st);  // its scratch dies with it
     }
     hipError_t e = hipStreamDestroy(st);
+    if (rep != RSM_OK) return rep;
     return e == hipSuccess ? RSM_OK : hip_fail(e, "hipStreamDestroy");
+}
+
+// Device-side equality of two device buffers (a compare kernel on `stream`, then
+// one word back): checks of large device-resident results without downloading them.
+int rsm_dev_equal(rsm_ctx* ctx, const void* a, const void* b, uint64_t bytes, void* stream, int* equal) {
+    if (!ctx || !a || !b || !equal || bytes % 16 != 0) return fail(RSM_EINVAL, "rsm_dev_equal: bad arguments");
+    *equal = 0;
+    if (int rc = use_device(ctx)) return rc;
+    LaneGuard g(ctx);
+    if (!g.lane) return g.rc;
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    hipError_t e;
+    uint32_t word = 1;
+    if ((e = g.lane->aux.ensure(64)) != hipSuccess ||
+        (e = hipMemsetAsync(g.lane->aux.ptr, 0, 4, st)) != hipSuccess ||
+        (e = launch_compare(static_cast<const uint8_t*>(a), static_cast<const uint8_t*>(b), bytes,
+                            static_cast<uint32_t*>(g.lane->aux.ptr), st)) != hipSuccess ||
+        (e = hipMemcpyAsync(&word, g.lane->aux.ptr, 4, hipMemcpyDeviceToHost, st)) != hipSuccess ||
+        (e = hipStreamSynchronize(st)) != hipSuccess)
+        return hip_fail(e, "rsm_dev_equal");
+    *equal = word == 0;
+    return RSM_OK;
+}
+
+int rsm_stream_check(rsm_ctx* ctx, void* stream) {
+    if (!ctx) return fail(RSM_EINVAL, "rsm_stream_check: NULL ctx");
+    if (int rc = use_device(ctx)) return rc;
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    hipError_t e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+    return check_queue_reports(ctx, st);
 }
 
 int rsm_stream_sync(void* stream) {
@@ -918,7 +992,9 @@ int rsm_sync(rsm_ctx* ctx) {
     if (int rc = use_device(ctx)) return rc;
     hipError_t e = hipStreamSynchronize(ctx->stream);
     if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
-    return check_queue_reports(ctx, nullptr);
+    // only the stream this call has drained: a report word of another stream may
+    // belong to a launch still running there (rsm_stream_check reports those)
+    return check_queue_reports(ctx, ctx->stream);
 }
 
 // Events: in-loop timing of the production launches (bench.py records one per

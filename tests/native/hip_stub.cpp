@@ -10,6 +10,7 @@
 #include <atomic>
 #include <cstdlib>
 #include <cstring>
+#include <vector>
 
 #include "../../rsmt2d_amd/csrc/gf16.hpp"
 #include "../../rsmt2d_amd/csrc/rsm_kernels.hpp"
@@ -22,9 +23,16 @@ std::atomic<int> g_streams{0};
 }  // namespace
 
 extern "C" {
+#ifdef RSM_STUB_ORACLE
+static thread_local int t_device = 0;  // G host "devices" for the multi-GPU check
+hipError_t hipGetDeviceCount(int* n) { *n = 8; return hipSuccess; }
+hipError_t hipSetDevice(int d) { if (d < 0 || d >= 8) return hipErrorInvalidDevice; t_device = d; return hipSuccess; }
+hipError_t hipGetDevice(int* d) { *d = t_device; return hipSuccess; }
+#else
 hipError_t hipGetDeviceCount(int* n) { *n = 1; return hipSuccess; }
 hipError_t hipSetDevice(int) { return hipSuccess; }
 hipError_t hipGetDevice(int* d) { *d = 0; return hipSuccess; }
+#endif
 hipError_t hipDeviceGetAttribute(int* v, hipDeviceAttribute_t, int) { *v = 256; return hipSuccess; }
 hipError_t hipDeviceSynchronize(void) { return hipSuccess; }
 hipError_t hipGetLastError(void) { return hipSuccess; }
@@ -84,6 +92,32 @@ static void touch_codewords(const CodewordSet& cs, bool gf16) {
     }
 }
 
+#ifdef RSM_STUB_ORACLE
+// multi_check (tests/test_multi_cpu.py): "kernels" that compute the real parity
+// with the C oracle, so the product's host code above them (CodewordSet
+// construction, the multi-GPU exchange) is checked bit for bit on the CPU.
+}  // namespace rsm
+extern "C" int leo_encode(unsigned k, size_t S, const uint8_t* const* data, uint8_t* const* parity);
+namespace rsm {
+static hipError_t oracle_codewords(const CodewordSet& cs) {
+    std::vector<const uint8_t*> d(cs.k);
+    std::vector<uint8_t*> p(cs.k);
+    for (uint32_t q = 0; q < cs.count; ++q) {
+        const uint64_t rel = cs.indices ? (uint64_t)cs.indices[q] * cs.cw_stride
+                                        : (uint64_t)(q / cs.per_square) * cs.square_stride +
+                                              (uint64_t)(q % cs.per_square) * cs.cw_stride;
+        uint8_t* out = cs.out_base ? cs.out_base : cs.base;
+        for (uint32_t e = 0; e < cs.k; ++e) {
+            d[e] = cs.base + rel + (uint64_t)e * cs.elem_stride;
+            p[e] = out + rel + cs.out_offset + (uint64_t)e * cs.elem_stride;
+        }
+        if (leo_encode(cs.k, cs.S, d.data(), p.data()) != 0) return hipErrorInvalidValue;
+    }
+    return hipSuccess;
+}
+hipError_t launch_encode_gf8(const CodewordSet& cs, hipStream_t) { return oracle_codewords(cs); }
+hipError_t launch_encode_gf16(const CodewordSet& cs, const Gf16Dev&, hipStream_t) { return oracle_codewords(cs); }
+#else
 hipError_t launch_encode_gf8(const CodewordSet& cs, hipStream_t) {
     touch_codewords(cs, false);
     return hipSuccess;
@@ -93,6 +127,7 @@ hipError_t launch_encode_gf16(const CodewordSet& cs, const Gf16Dev& g, hipStream
     touch_codewords(cs, true);
     return hipSuccess;
 }
+#endif
 static void touch_decode(const DecodeSet& ds) {
     const uint64_t W = 2ull * ds.k;
     for (uint32_t i = 0; i < ds.count; ++i) {

@@ -263,3 +263,14 @@ def test_repair_half_of_each_row_byzantine_k128(lib, rng):
     # progress (it inserts verified rows before meeting the byzantine one)
     after = eds.Flattened()
     assert all(a == b for a, b in zip(before, after) if a is not None)
+
+
+def test_cannot_repair_square_with_bad_roots(lib):  # extendeddatacrossword_test.go:165-183
+    """Roots taken from the original, then one cell of the (complete) square
+    replaced: Repair must fail (the pre-repair check finds row 0 / column 0
+    inconsistent with its committed root)."""
+    original = example_eds()
+    rr, cr = _roots(original)
+    original.setCell(0, 0, CORRUPT)
+    with pytest.raises(R.RSMError):
+        original.Repair(rr, cr)

@@ -136,3 +136,45 @@ def test_nmt_repair(k):
     h2 = R.ImportExtendedDataSquare(bad, codec, ctor)
     with pytest.raises(R.ErrByzantineData):
         h2.Repair(rr, cr)
+
+
+def _nmt_eds(values, ns=1, share=512):
+    """createTestEdsWithNMT (extendeddatacrossword_test.go:788-804): a 2x2 ODS of
+    constant shares, erasured NMT with `ns`-byte namespaces."""
+    data = [bytes([v]) * share for v in values]
+    return R.ComputeExtendedDataSquare(data, R.NewLeoRSCodec(), R.newErasuredNamespacedMerkleTreeConstructor(2, ns))
+
+
+ONE, TWO, THREE = (bytes([v]) * SHARE for v in (1, 2, 3))
+ALL_BUT = lambda keep: [(r, c) for r in range(4) for c in range(4) if (r, c) not in keep]
+
+
+@pytest.mark.parametrize("name,cells,axis", [
+    ("no corruption", {}, None),
+    # row 0 = [two, one, parity...] complete, everything else erased: row 0's tree
+    # push fails on the namespace order -> ErrByzantineData{Row, 0}
+    ("rows with unordered shares", {**{(0, 0): TWO, (0, 1): ONE}, **{rc: None for rc in ALL_BUT(
+        {(0, 0), (0, 1), (0, 2), (0, 3)})}}, R.Row),
+    # column 0 = [three, one, parity...] complete, the rest erased -> {Col, 0}
+    ("columns with unordered shares", {**{(0, 0): THREE, (1, 0): ONE}, **{rc: None for rc in ALL_BUT(
+        {(0, 0), (1, 0), (2, 0), (3, 0)})}}, R.Col),
+])
+def test_corrupted_eds_byzantine_unordered_shares(name, cells, axis):
+    """TestCorruptedEdsReturnsErrByzantineData_UnorderedShares
+    (extendeddatacrossword_test.go:490-602): the DA header of the ODS {1,2,3,4}
+    with 1-byte namespaces; a corrupted copy whose only complete vector has its
+    shares out of namespace order must fail Repair with ErrByzantineData on exactly
+    that axis, index 0."""
+    header = _nmt_eds([1, 2, 3, 4])
+    rr, cr = header.RowRoots(), header.ColRoots()
+    eds = _nmt_eds([1, 2, 3, 4])
+    for (r, c), v in cells.items():
+        eds.setCell(r, c, v)
+    if axis is None:
+        eds.Repair(rr, cr)
+        assert eds.Flattened() == header.Flattened()
+        return
+    with pytest.raises(R.ErrByzantineData) as ei:
+        eds.Repair(rr, cr)
+    assert ei.value.Axis == axis and ei.value.Index == 0
+

@@ -191,6 +191,68 @@ def test_single_launch_batches_on_three_streams(lib):
         R._check(lib.rsm_stream_destroy(ctx, s))
 
 
+def test_single_launch_at_bench_scale(lib):
+    """The bench's exact configuration (bench.py c2: k = 128, S = 512, 256 squares per
+    launch, launches on 3 streams over 3 buffers, running concurrently): EVERY square
+    of every launch equals the two-launch result, compared on the device
+    (rsm_dev_equal), over several rounds.  The parity quadrants are re-poisoned
+    before every launch, so a Q1-column set that read a stale or unfinished Q1 (the
+    inter-workgroup hand-off of extend_gf8_bs128q_kernel) could not match by
+    accident; the two-launch references are themselves oracle-checked at their
+    first and last square.  Reference: extendeddatasquare.go:154-227."""
+    ctx = R.device_context(0)
+    k, S, B, NS = 128, 512, 256, 3
+    W = 2 * k
+    sq = W * W * S
+    n = sq * B
+    seeds = [0xBE5C0 + i for i in range(NS)]
+    ref = [R.DeviceBuffer(n) for _ in range(NS)]
+    work = [R.DeviceBuffer(n) for _ in range(NS)]
+    st = [ctypes.c_void_p() for _ in range(NS)]
+    try:
+        for i in range(NS):
+            ref[i].fill_random(seeds[i])
+            R._check(lib.rsm_sync(ctx))
+            R._check(lib.rsm_extend_squares_phase_dev(ctx, ref[i].ptr, k, S, B, 1, None))
+            R._check(lib.rsm_extend_squares_phase_dev(ctx, ref[i].ptr, k, S, B, 2, None))
+            R._check(lib.rsm_sync(ctx))
+            for j in (0, B - 1):
+                got = ref[i].download(sq, j * sq).reshape(W, W, S)
+                assert np.array_equal(got, oracle.extend_square(got[:k, :k].copy(), nthreads=8)), (i, j)
+        for s in st:
+            R._check(lib.rsm_stream_create(ctx, ctypes.byref(s)))
+        eq = ctypes.c_int()
+        for rnd in range(4):
+            for i in range(NS):  # Q0 = the reference input, Q1..Q3 = garbage
+                work[i].fill_random(seeds[i] if rnd % 2 == 0 else seeds[(i + 1) % NS] ^ 0x55)
+                R._check(lib.rsm_sync(ctx))
+                if rnd % 2:
+                    # restore the ODS quadrant of every square from the reference
+                    _restore_ods(lib, ctx, work[i], ref[i], k, S, B)
+            for i in range(NS):
+                R._check(lib.rsm_extend_squares_dev(ctx, work[i].ptr, k, S, B, st[i]))
+            for i in range(NS):
+                R._check(lib.rsm_stream_check(ctx, st[i]))  # also reports a stuck queue wait
+            for i in range(NS):
+                R._check(lib.rsm_dev_equal(ctx, work[i].ptr, ref[i].ptr, n, None, ctypes.byref(eq)))
+                assert eq.value == 1, (rnd, i)
+    finally:
+        for s in st:
+            if s.value:
+                R._check(lib.rsm_stream_destroy(ctx, s))
+        for b in ref + work:
+            b.free()
+
+
+def _restore_ods(lib, ctx, dst, src, k, S, B):
+    """Q0 of every square of src into dst (device to device, one copy per ODS row)."""
+    W = 2 * k
+    for b in range(B):
+        for r in range(k):
+            off = (b * W + r) * W * S
+            R._check(lib.rsm_memcpy(ctx, dst.ptr + off, src.ptr + off, k * S, 2))
+
+
 @pytest.mark.parametrize("k,S,count", [(128, 512, 5), (16, 64, 3), (256, 128, 2)])
 def test_pinned_host_batch(lib, k, S, count):
     """rsm_extend_squares_host over pinned arenas: three lanes overlap H2D,

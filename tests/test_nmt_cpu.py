@@ -81,3 +81,23 @@ def test_buffered_constructor_interface():
     assert c.params.square_size == 67 and c.params.namespace_size == 29 and c.params.ignore_max_namespace == 1
     with pytest.raises(ValueError):
         R.newErasuredNamespacedMerkleTreeConstructor(0)
+
+
+def test_nmt_push_validates_like_the_wrapper():
+    """The host tree reports the wrapper's Push errors at Push
+    (nmtwrapper_test.go:103-108, nmtwrapper.go Push)."""
+    t = R.newErasuredNamespacedMerkleTreeConstructor(2, 1)(R.Row, 0)
+    t.Push(bytes([1]) * 8)
+    with pytest.raises(R.RSMError, match="lexicographically"):
+        t.Push(bytes([0]) * 8)  # namespace 0 after 1 (both in Q0)
+    t = R.newErasuredNamespacedMerkleTreeConstructor(2, 29)(R.Row, 0)
+    with pytest.raises(R.RSMError, match="too short"):
+        t.Push(b"\1" * 28)
+    t = R.newErasuredNamespacedMerkleTreeConstructor(2, 1)(R.Row, 4)
+    with pytest.raises(R.RSMError, match="past predetermined"):
+        t.Push(b"\1" * 8)
+    t = R.newErasuredNamespacedMerkleTreeConstructor(1, 1)(R.Row, 0)
+    t.Push(b"\1" * 8)
+    t.Push(b"\1" * 8)  # parity namespace 0xFF >= 1
+    with pytest.raises(R.RSMError, match="past predetermined"):
+        t.Push(b"\1" * 8)
