@@ -50,6 +50,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-c5", action="store_true", help="skip the config-5 (sharded 512x512 square) line")
     p.add_argument("--no-c3", action="store_true", help="skip the config-3 (Repair) timings")
+    p.add_argument("--no-c4", action="store_true", help="skip the config-4 (k=256, S=2048, GF(2^16)) line")
+    p.add_argument("--no-gf16-repair", action="store_true", help="skip the k=256/512 Repair timings")
     p.add_argument("--no-roots", action="store_true", help="skip the extension + Merkle roots timing")
     p.add_argument("--no-extras", action="store_true", help="skip host-path and Codec-latency lines")
     p.add_argument("--dist", action="store_true",
@@ -83,29 +85,46 @@ def cpu_info():
 
 
 def cpu_baseline(k, S, seconds):
-    """AVX2 restatement of the reference path (oracle/libleopard_simd.so: the C oracle
-    with klauspost's pshufb nibble-table GF(2^8) rows), multithreaded over codewords
-    with the reference's two-phase schedule.  Not the reference: its Go/klauspost
-    code cannot run here."""
+    """The reference path restated on the host CPU (oracle/leopard_oracle.c with
+    klauspost's fastest x86 leopard8 technique where the CPU has it: AVX-512 rows,
+    GF2P8AFFINEQB multiplies, fused butterflies -- libleopard_gfni.so; else the AVX2
+    pshufb build), multithreaded over codewords with the reference's two-phase
+    schedule, writing into a reused EDS buffer (no page faults in the timed loop).
+    Threads: this job's CPU share on the GPU box (16 per GPU: the harness sizes every
+    worker pool to it; os.cpu_count() reports the whole machine); the single-thread
+    rate is reported beside it.  Not the reference: its Go/klauspost code cannot run
+    here."""
     import numpy as np
     import oracle
-    threads = min(16, os.cpu_count() or 1)
+    ncpu = os.cpu_count() or 1
+    threads = min(16, ncpu)
+    gfni = oracle.gfni_supported() and k <= 128
+    ext = oracle.extend_square_gfni if gfni else oracle.extend_square_simd if k <= 128 else None
     ods = oracle.splitmix64_bytes(k * k * S).reshape(k, k, S)
-    ext = oracle.extend_square_simd if k <= 128 else oracle.extend_square
-    ext(ods, nthreads=threads)  # warm
-    n, t0 = 0, time.perf_counter()
-    while True:
-        ext(ods, nthreads=threads)
-        n += 1
-        dt = time.perf_counter() - t0
-        if dt >= seconds:
-            break
-    model, ncpu = cpu_info()
+    out = np.empty((2 * k, 2 * k, S), np.uint8)
+
+    def rate(nth, secs):
+        run = (lambda: ext(ods, nthreads=nth, out=out)) if ext else (lambda: oracle.extend_square(ods, nthreads=nth))
+        run()  # warm
+        n, t0 = 0, time.perf_counter()
+        while True:
+            run()
+            n += 1
+            dt = time.perf_counter() - t0
+            if dt >= secs:
+                return n, dt
+
+    n, dt = rate(threads, seconds)
+    n1, dt1 = rate(1, max(2.0, seconds / 4))
+    model, _ = cpu_info()
+    tech = ("AVX-512 + GFNI (GF2P8AFFINEQB multiplies, fused butterflies)" if gfni
+            else "AVX2 pshufb nibble tables" if ext else "scalar tables")
     return {"value": round(n * k * k * S / dt / 2**30, 4), "unit": "GiB/s", "cores": threads,
             "kind": "port", "cpu_model": model, "host_cpus": ncpu,
-            "sample": f"{n} squares k={k} S={S} ({dt:.1f} s) through oracle/leopard_oracle.c built with LEO_SIMD "
-                      f"(AVX2 pshufb nibble-table rows, restatement of klauspost leopard8, not the reference), "
-                      f"{threads} threads over codewords; the Go reference cannot run here"}
+            "single_thread_GiB_s": round(n1 * k * k * S / dt1 / 2**30, 4),
+            "sample": f"{n} squares k={k} S={S} ({dt:.1f} s) through oracle/leopard_oracle.c ({tech}; restatement "
+                      f"of klauspost leopard8, not the reference), {threads} threads over codewords = this job's CPU "
+                      f"share of the {ncpu}-CPU host; single thread: {n1} squares in {dt1:.1f} s"}
 
 
 def pct(xs, q):
@@ -348,10 +367,11 @@ def bench_c5(world, rank, local, dist, steps, L, R):
     return out
 
 
-def bench_c3(local, L, R, repeats=5):
+def bench_c3(local, L, R, repeats=5, k=128, S=512):
     """Config 3: k=128, S=512, exactly k of the 2k cells of every
     row erased (BenchmarkRepair's scheme, extendeddatacrossword_test.go:443-453),
-    honest DefaultTree roots.  Two timings:
+    honest DefaultTree roots; also run at k = 256 and 512 (GF(2^16), BenchmarkRepair's
+    larger ODS sizes).  Two timings:
       decode_sweep -- the device decode of all 2k rows alone (rsm_decode_vectors_dev
                       over a device-resident EDS + presence mask, HIP-synchronised);
       repair       -- (*ExtendedDataSquare).Repair end to end as BenchmarkRepair
@@ -362,10 +382,9 @@ def bench_c3(local, L, R, repeats=5):
     Replicas only: Repair is not sharded."""
     import ctypes
     import numpy as np
-    k, S = 128, 512
     W = 2 * k
     ctx = R.device_context(local)
-    rng = np.random.default_rng(0xC3)
+    rng = np.random.default_rng(0xC3 + k)
     # original EDS from the device extension of a seeded ODS
     buf = R.DeviceBuffer(W * W * S, local)
     buf.fill_random(0xC3)
@@ -402,7 +421,7 @@ def bench_c3(local, L, R, repeats=5):
     R._check(L.rsm_sync(ctx))
     if not np.array_equal(buf.download(W * W * S).reshape(W, W, S), full):
         raise SystemExit("bench c3: device decode sweep differs from the original EDS")
-    n_sw = 50
+    n_sw = 50 if k <= 128 else 10
     t0 = time.perf_counter()
     for _ in range(n_sw):
         sweep()
@@ -433,7 +452,8 @@ def bench_c3(local, L, R, repeats=5):
         L.rsm_eds_free(h)
     t_rep = sorted(times)[len(times) // 2]
     algo = W * W * S  # present shares read + missing shares written
-    return {"workload": "c3: k=128, S=512, 128 of 256 cells erased in every row (BenchmarkRepair scheme)",
+    return {"workload": f"{'c3: ' if k == 128 else ''}k={k}, S={S}, {k} of {W} cells erased in every row "
+                        f"(BenchmarkRepair scheme, GF(2^{8 if k <= 128 else 16}))",
             "decode_sweep_us": round(t_sweep * 1e6, 2),
             "decode_sweep_GB_s": round(algo / t_sweep / 1e9, 1),
             "decode_sweep_frac": round(algo / t_sweep / 1e9 / HBM_PEAK_GBS, 4),
@@ -442,6 +462,92 @@ def bench_c3(local, L, R, repeats=5):
             "note": "repair = rsm_eds_repair end to end on a host EDS (zero-copy decode sweeps: present cells "
                     "read over PCIe, rebuilt cells written back; device column re-encode check; device "
                     "DefaultTree roots of all 512 vectors); median of samples"}
+
+
+def bench_single_square(local, L, R, k=128, S=512, reps=200):
+    """What a cgo ComputeExtendedDataSquare of ONE square gets (extendeddatasquare.go:
+    50-77) from device memory: rsm_extend_squares_dev with count = 1 (the single-launch
+    queue kernel over the square's 96 sets), launches back to back on one stream, so
+    each one's device time is its latency.  Oracle-checked."""
+    import ctypes
+    import numpy as np
+    import oracle
+    ctx = R.device_context(local)
+    W = 2 * k
+    buf = R.DeviceBuffer(W * W * S, local)
+    buf.fill_random(0x55)
+    R._check(L.rsm_extend_squares_dev(ctx, buf.ptr, k, S, 1, None))
+    R._check(L.rsm_sync(ctx))
+    got = buf.download(W * W * S).reshape(W, W, S)
+    if not np.array_equal(got, oracle.extend_square(got[:k, :k].copy(), nthreads=8)):
+        raise SystemExit("bench single square: GPU EDS differs from the oracle")
+    e0, e1 = ctypes.c_void_p(), ctypes.c_void_p()
+    R._check(L.rsm_event_create(ctx, ctypes.byref(e0)))
+    R._check(L.rsm_event_create(ctx, ctypes.byref(e1)))
+    R._check(L.rsm_event_record(ctx, e0, None))
+    for _ in range(reps):
+        R._check(L.rsm_extend_squares_dev(ctx, buf.ptr, k, S, 1, None))
+    R._check(L.rsm_event_record(ctx, e1, None))
+    ms = ctypes.c_float()
+    R._check(L.rsm_event_elapsed_ms(e0, e1, ctypes.byref(ms)))
+    t_dev = ms.value / reps / 1e3
+    lat = []
+    for _ in range(50):  # host-observed: launch + completion of one square
+        t0 = time.perf_counter()
+        R._check(L.rsm_extend_squares_dev(ctx, buf.ptr, k, S, 1, None))
+        R._check(L.rsm_sync(ctx))
+        lat.append(time.perf_counter() - t0)
+    for e in (e0, e1):
+        L.rsm_event_destroy(e)
+    buf.free()
+    return {"workload": f"one k={k} S={S} square, device-resident (count = 1)",
+            "single_square_us": round(t_dev * 1e6, 2), "host_observed_us_p50": round(pct(lat, 0.5) * 1e6, 1),
+            "frac": round(4 * k * k * S / t_dev / 1e9 / HBM_PEAK_GBS, 4),
+            "note": "device time per launch of back-to-back launches on one stream; host_observed = "
+                    "rsm_extend_squares_dev + rsm_sync round trip"}
+
+
+def bench_c4(local, L, R, steps, B=2):
+    """Config 4: 256x256 -> 512x512 squares of 2048 B shares (GF(2^16), enc16_kernel<256>),
+    device-resident, B squares (1 GiB of EDS) per step, steps alternating over two
+    buffers so no step finds its squares in the 256 MiB Infinity Cache."""
+    import ctypes
+    import numpy as np
+    import oracle
+    k, S = 256, 2048
+    W = 2 * k
+    sq = W * W * S
+    ctx = R.device_context(local)
+    bufs = [R.DeviceBuffer(B * sq, local) for _ in range(2)]
+    for i, b in enumerate(bufs):
+        b.fill_random(0xC4 + i)
+    R._check(L.rsm_sync(ctx))
+    for b in bufs:
+        R._check(L.rsm_extend_squares_dev(ctx, b.ptr, k, S, B, None))
+    R._check(L.rsm_sync(ctx))
+    got = bufs[0].download(sq).reshape(W, W, S)
+    if not np.array_equal(got, oracle.extend_square(got[:k, :k].copy(), nthreads=16)):
+        raise SystemExit("bench c4: GPU EDS differs from the oracle")
+    n = max(4, min(steps, 20))
+    e0, e1 = ctypes.c_void_p(), ctypes.c_void_p()
+    R._check(L.rsm_event_create(ctx, ctypes.byref(e0)))
+    R._check(L.rsm_event_create(ctx, ctypes.byref(e1)))
+    R._check(L.rsm_event_record(ctx, e0, None))
+    for i in range(n):
+        R._check(L.rsm_extend_squares_dev(ctx, bufs[i % 2].ptr, k, S, B, None))
+    R._check(L.rsm_event_record(ctx, e1, None))
+    ms = ctypes.c_float()
+    R._check(L.rsm_event_elapsed_ms(e0, e1, ctypes.byref(ms)))
+    dt = ms.value / n / 1e3
+    for e in (e0, e1):
+        L.rsm_event_destroy(e)
+    for b in bufs:
+        b.free()
+    algo = 4 * k * k * S * B
+    return {"workload": "c4: 256x256->512x512 squares, 2048 B shares, GF(2^16)", "squares_per_step": B,
+            "ms_per_square": round(dt / B * 1e3, 4), "ods_GiB_s": round(k * k * S * B / dt / 2**30, 3),
+            "frac": round(algo / dt / 1e9 / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_square": 4 * k * k * S,
+            "kernel": "enc16_kernel<256> (row pass, column pass)"}
 
 
 def bench_roots(local, L, R, buf, k, S, B, steps):
@@ -600,11 +706,13 @@ def main():
     # per-launch durations of THIS timed run (events on the launch streams)
     rows, cols, spans = [], [], []
     ms = ctypes.c_float()
-    # union of the timed launches (first launch's start event to the last one's end
-    # event, on the device clock): concurrent launches on different streams share
-    # the CUs, so their individual spans overlap
-    R._check(L.rsm_event_elapsed_ms(events[0][0], events[-1][2], ctypes.byref(ms)))
-    union_s = ms.value / 1e3
+    # union of the timed launches on the device clock: from the first launch's start
+    # event to the LATEST end event of any step (with several streams an earlier
+    # launch on another stream can end after the last-enqueued one)
+    union_s = 0.0
+    for ev in events:
+        R._check(L.rsm_event_elapsed_ms(events[0][0], ev[2], ctypes.byref(ms)))
+        union_s = max(union_s, ms.value / 1e3)
     for ev in events:
         if not single:
             R._check(L.rsm_event_elapsed_ms(ev[0], ev[1], ctypes.byref(ms)))
@@ -650,7 +758,7 @@ def main():
         # the step IS one launch of the dominant kernel; with 3 streams the launches
         # run concurrently (each on a share of the CUs), so the kernel's rate is the
         # algorithmic bytes of all timed launches over their union on the device clock
-        dominant = ("extend_gf8_bs128q_kernel (one launch: both passes)", algo_step, union_s / a.steps)
+        dominant = ("extend_gf8_bs128s_kernel (one launch: both passes)", algo_step, union_s / a.steps)
     else:
         dominant = ((kname + " column pass", col_bytes, t_col) if col_dom else (kname + " row pass", row_bytes, t_row))
     ach = dominant[1] / dominant[2] / 1e9
@@ -662,7 +770,7 @@ def main():
     pmc_path = os.path.join(ROOT, "profiles", "pmc_latest.json")
     if bitsliced and os.path.exists(pmc_path):
         if single:
-            want = "extend_gf8_bs128q_kernel<18472>"
+            want = "extend_gf8_bs128s_kernel<0>"
             sets = 3 * k * B * S // 2048
         else:
             want = "encode_gf8_bs128u_kernel<%d, %d>" % ((184, 1) if col_dom else (104, 0))
@@ -695,7 +803,9 @@ def main():
                    "streams": len(streams), "row_pass_grid": row_grid or None},
         "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": dominant[0], "avg_launch_us": us(t_span if single else dominant[2]),
+                     "kernel": dominant[0],
+                     **({"union_us_per_launch": us(union_s / a.steps),
+                         "concurrent_span_us": us(t_span)} if single else {"avg_launch_us": us(dominant[2])}),
                      "bytes_per_launch": dominant[1],
                      "source": (f"HIP events around every launch of the {a.steps} timed steps; {len(streams)} "
                                 "concurrent launches share the CUs, so achieved = bytes of all timed launches / "
@@ -730,8 +840,14 @@ def main():
         b.free()
     for st in streams[1:]:
         R._check(L.rsm_stream_destroy(ctx, st))
+    if rank == 0 and world == 1 and k == 128:
+        out["single_square"] = bench_single_square(local, L, R)
+        if not a.no_c4:
+            out["c4"] = bench_c4(local, L, R, a.steps)
     if rank == 0 and world == 1 and not a.no_c3:
         out["c3"] = bench_c3(local, L, R)
+        if not a.no_gf16_repair:
+            out["repair_gf16"] = [bench_c3(local, L, R, repeats=3, k=kk) for kk in (256, 512)]
     if not a.no_c5:
         out["c5"] = bench_c5(world, rank, local, dist, a.steps, L, R)
     if rank == 0:

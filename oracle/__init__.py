@@ -137,13 +137,56 @@ def simd_lib() -> ctypes.CDLL:
     return _simd
 
 
-def extend_square_simd(ods: np.ndarray, nthreads: int = 1) -> np.ndarray:
+def extend_square_simd(ods: np.ndarray, nthreads: int = 1, out: np.ndarray = None) -> np.ndarray:
     ods = np.ascontiguousarray(ods, dtype=np.uint8)
     k, _, S = ods.shape
-    eds = np.empty((2 * k, 2 * k, S), dtype=np.uint8)
+    eds = out if out is not None else np.empty((2 * k, 2 * k, S), dtype=np.uint8)
+    assert eds.shape == (2 * k, 2 * k, S) and eds.dtype == np.uint8 and eds.flags.c_contiguous
     rc = simd_lib().leo_extend_square(k, S, ods.ctypes.data, eds.ctypes.data, int(nthreads))
     if rc != 0:
         raise ValueError(f"leo_extend_square (simd) failed rc={rc}")
+    return eds
+
+
+_gfni = None
+
+
+def gfni_supported() -> bool:
+    """GFNI + AVX-512BW on this host (the GPU box's EPYC 9575F has both)."""
+    try:
+        flags = open("/proc/cpuinfo").read()
+    except OSError:
+        return False
+    return " gfni" in flags and " avx512bw" in flags
+
+
+def gfni_lib() -> ctypes.CDLL:
+    """libleopard_gfni.so: the restatement with AVX-512 rows, GF2P8AFFINEQB multiplies
+    and fused GF(2^8) butterflies (LEO_GFNI) -- bench.py's cpu_baseline only, checked
+    against the scalar oracle in tests/test_oracle.py (klauspost's fastest x86
+    leopard8 technique, restated; not the reference)."""
+    global _gfni
+    with _lock:
+        if _gfni is None:
+            path = os.path.join(_HERE, "libleopard_gfni.so")
+            if not os.path.exists(path):
+                build()
+            L = ctypes.CDLL(path)
+            L.leo_extend_square.argtypes = [ctypes.c_uint, ctypes.c_size_t, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_int]
+            L.leo_extend_square.restype = ctypes.c_int
+            _gfni = L
+    return _gfni
+
+
+def extend_square_gfni(ods: np.ndarray, nthreads: int = 1, out: np.ndarray = None) -> np.ndarray:
+    ods = np.ascontiguousarray(ods, dtype=np.uint8)
+    k, _, S = ods.shape
+    eds = out if out is not None else np.empty((2 * k, 2 * k, S), dtype=np.uint8)
+    assert eds.shape == (2 * k, 2 * k, S) and eds.dtype == np.uint8 and eds.flags.c_contiguous
+    rc = gfni_lib().leo_extend_square(k, S, ods.ctypes.data, eds.ctypes.data, int(nthreads))
+    if rc != 0:
+        raise ValueError(f"leo_extend_square (gfni) failed rc={rc}")
     return eds
 
 

@@ -44,6 +44,9 @@ static uint8_t mul8[ORD8][ORD8]; /* mul8[logm][x] = mulLog8(x, logm) */
 #ifdef LEO_SIMD
 static uint8_t nib8[ORD8][2][16];
 #endif
+#ifdef LEO_GFNI
+static uint64_t aff8[ORD8]; /* GF2P8AFFINEQB matrix of x -> mulLog8(x, logm) */
+#endif
 
 /* ------------------------------------------------------------------------- */
 /* GF(2^16): klauspost leopard.go / catid LeopardFF16.cpp                      */
@@ -214,6 +217,21 @@ static void init_nib8(void) {
         }
 }
 static void init_all(void) { init8(); init16(); init_nib8(); }
+#elif defined(LEO_GFNI)
+/* row i of the bit matrix (byte 7 - i of the qword): input bit j feeds output bit i
+ * iff bit i of mulLog8(1 << j, logm) is set */
+static void init_aff8(void) {
+    for (unsigned lm = 0; lm < ORD8; ++lm) {
+        uint64_t a = 0;
+        for (unsigned i = 0; i < 8; ++i) {
+            unsigned row = 0;
+            for (unsigned j = 0; j < 8; ++j) row |= ((mul8[lm][1u << j] >> i) & 1u) << j;
+            a |= (uint64_t)row << (8 * (7 - i));
+        }
+        aff8[lm] = a;
+    }
+}
+static void init_all(void) { init8(); init16(); init_aff8(); }
 #else
 static void init_all(void) { init8(); init16(); }
 #endif
@@ -224,7 +242,48 @@ static void ensure_init(void) { pthread_once(&g_once, init_all); }
 /* A GF16 work row is S bytes; per 64-byte block, symbol t (t<32) is          */
 /* lo = row[64b+t], hi = row[64b+32+t]  (klauspost refMulAdd layout, A.6).   */
 /* ------------------------------------------------------------------------- */
-#ifndef LEO_SIMD
+#if defined(LEO_GFNI)
+/* LEO_GFNI (libleopard_gfni.so, the bench's cpu_baseline only): AVX-512 rows with
+ * GF(2^8) multiply-by-constant as one GF2P8AFFINEQB per 64 bytes -- the instruction
+ * klauspost/reedsolomon's AVX-512 GFNI leopard8 path uses -- and the butterflies
+ * fused into one pass over x and y (a restatement, not the reference). */
+#include <immintrin.h>
+static inline void xor_row(uint8_t *restrict dst, const uint8_t *restrict src, size_t n) {
+    for (size_t i = 0; i < n; i += 64)
+        _mm512_storeu_si512(dst + i, _mm512_xor_si512(_mm512_loadu_si512(dst + i), _mm512_loadu_si512(src + i)));
+}
+static inline void muladd8(uint8_t *restrict dst, const uint8_t *restrict src, unsigned lm, size_t n) {
+    const __m512i a = _mm512_set1_epi64((long long)aff8[lm]);
+    for (size_t i = 0; i < n; i += 64)
+        _mm512_storeu_si512(dst + i, _mm512_xor_si512(_mm512_loadu_si512(dst + i),
+                                                      _mm512_gf2p8affine_epi64_epi8(_mm512_loadu_si512(src + i), a, 0)));
+}
+static inline void mul8_row(uint8_t *restrict dst, const uint8_t *restrict src, unsigned lm, size_t n) {
+    const __m512i a = _mm512_set1_epi64((long long)aff8[lm]);
+    for (size_t i = 0; i < n; i += 64)
+        _mm512_storeu_si512(dst + i, _mm512_gf2p8affine_epi64_epi8(_mm512_loadu_si512(src + i), a, 0));
+}
+/* fused GF(2^8) butterflies: IFFT_DIT2 y ^= x; x ^= y*L -- FFT_DIT2 x ^= y*L; y ^= x */
+static inline void ifft2_8(uint8_t *restrict x, uint8_t *restrict y, unsigned lm, size_t n) {
+    const __m512i a = _mm512_set1_epi64((long long)aff8[lm]);
+    for (size_t i = 0; i < n; i += 64) {
+        const __m512i xv = _mm512_loadu_si512(x + i);
+        const __m512i yv = _mm512_xor_si512(_mm512_loadu_si512(y + i), xv);
+        _mm512_storeu_si512(y + i, yv);
+        _mm512_storeu_si512(x + i, _mm512_xor_si512(xv, _mm512_gf2p8affine_epi64_epi8(yv, a, 0)));
+    }
+}
+static inline void fft2_8(uint8_t *restrict x, uint8_t *restrict y, unsigned lm, size_t n) {
+    const __m512i a = _mm512_set1_epi64((long long)aff8[lm]);
+    for (size_t i = 0; i < n; i += 64) {
+        const __m512i yv = _mm512_loadu_si512(y + i);
+        const __m512i xv = _mm512_xor_si512(_mm512_loadu_si512(x + i), _mm512_gf2p8affine_epi64_epi8(yv, a, 0));
+        _mm512_storeu_si512(x + i, xv);
+        _mm512_storeu_si512(y + i, _mm512_xor_si512(yv, xv));
+    }
+}
+#define LEO_FUSED8 1
+#elif !defined(LEO_SIMD)
 static inline void xor_row(uint8_t *restrict dst, const uint8_t *restrict src, size_t n) {
     for (size_t i = 0; i < n; ++i) dst[i] ^= src[i];
 }
@@ -312,11 +371,17 @@ static inline unsigned skew_at(const field_t *f, long idx) {
 
 /* IFFT_DIT2: y ^= x; x ^= y*L   (L == MOD => zero multiplier: XOR half only) */
 static inline void ifft2(const field_t *f, uint8_t *x, uint8_t *y, unsigned L) {
+#ifdef LEO_FUSED8
+    if (!f->gf16 && L != f->mod) { ifft2_8(x, y, L, f->n); return; }
+#endif
     xor_row(y, x, f->n);
     if (L != f->mod) muladd(f, x, y, L);
 }
 /* FFT_DIT2: x ^= y*L; y ^= x */
 static inline void fft2(const field_t *f, uint8_t *x, uint8_t *y, unsigned L) {
+#ifdef LEO_FUSED8
+    if (!f->gf16 && L != f->mod) { fft2_8(x, y, L, f->n); return; }
+#endif
     if (L != f->mod) muladd(f, x, y, L);
     xor_row(y, x, f->n);
 }
@@ -555,7 +620,7 @@ int leo_extend_square(unsigned k, size_t S, const uint8_t *ods, uint8_t *eds, in
     ensure_init();
     if (k == 0 || S == 0 || (S % 64) != 0) return -1;
     size_t W = 2 * (size_t)k;
-    memset(eds, 0, W * W * S);
+    /* every cell outside Q0 is written by the encodes below */
     for (unsigned r = 0; r < k; ++r)
         memcpy(eds + (size_t)r * W * S, ods + (size_t)r * k * S, (size_t)k * S);
     if (nthreads < 1) nthreads = 1;

@@ -224,4 +224,66 @@ RSM_HD void large_ifft_fft(uint32_t (&X)[16][8]) {
     });
 }
 
+// ---------------------------------------------------------------------------
+// Half-split schedule (production queue kernel since round 3).  Symbol bit 6
+// splits the 128-point transform into two halves that are independent in every
+// layer except the merged middle pair, so each phase below works on one half
+// (registers 8G..8G+7) while the other half's LDS exchange is in flight.
+//   small layout S': wave A, register j: e = (j & 7) + 8A + 64 (j >> 3)
+//                    (bits 0-2 in registers, 3-5 the wave, bit 6 the half)
+//   large layout L : wave w, register h: e = w + 8h (as above)
+// The exchange of half G is a transpose: wave u's register 8G + v goes to wave v's
+// register 8G + u (both directions).
+template <int A, int G>
+RSM_HD void small_ifft_h(uint32_t (&X)[16][8]) {
+    sfor<3>([&](auto LG) {
+        constexpr int d = 1 << decltype(LG)::value;
+        sfor<8 / (2 * d)>([&](auto B) {
+            constexpr int b = decltype(B)::value * 2 * d;
+            constexpr unsigned L = kGf8.skew[kOffEnc + 8 * A + 64 * G + b + d];
+            sfor<d>([&](auto Q) {
+                ifft2<L>(X[8 * G + b + decltype(Q)::value], X[8 * G + b + decltype(Q)::value + d]);
+            });
+        });
+    });
+}
+template <int A, int G>
+RSM_HD void small_fft_h(uint32_t (&X)[16][8]) {
+    sfor<3>([&](auto LG) {
+        constexpr int d = 4 >> decltype(LG)::value;
+        sfor<8 / (2 * d)>([&](auto B) {
+            constexpr int b = decltype(B)::value * 2 * d;
+            constexpr unsigned L = kGf8.skew[-1 + 8 * A + 64 * G + b + d];
+            sfor<d>([&](auto Q) {
+                fft2<L>(X[8 * G + b + decltype(Q)::value], X[8 * G + b + decltype(Q)::value + d]);
+            });
+        });
+    });
+}
+template <int G>
+RSM_HD void large_ifft_h(uint32_t (&X)[16][8]) {  // IFFT d = 8, 16, 32 on h in [8G, 8G + 8)
+    sfor<3>([&](auto LG) {
+        constexpr int dh = 1 << decltype(LG)::value;
+        sfor<8 / (2 * dh)>([&](auto B) {
+            constexpr int hb = 8 * G + decltype(B)::value * 2 * dh;
+            constexpr unsigned L = kGf8.skew[kOffEnc + 8 * hb + 8 * dh];
+            sfor<dh>([&](auto Q) { ifft2<L>(X[hb + decltype(Q)::value], X[hb + decltype(Q)::value + dh]); });
+        });
+    });
+}
+RSM_HD void large_mid(uint32_t (&X)[16][8]) {
+    sfor<8>([&](auto Q) { mid2<kMidLog>(X[decltype(Q)::value], X[decltype(Q)::value + 8]); });
+}
+template <int G>
+RSM_HD void large_fft_h(uint32_t (&X)[16][8]) {  // FFT d = 32, 16, 8 on h in [8G, 8G + 8)
+    sfor<3>([&](auto LG) {
+        constexpr int dh = 4 >> decltype(LG)::value;
+        sfor<8 / (2 * dh)>([&](auto B) {
+            constexpr int hb = 8 * G + decltype(B)::value * 2 * dh;
+            constexpr unsigned L = kGf8.skew[-1 + 8 * hb + 8 * dh];
+            sfor<dh>([&](auto Q) { fft2<L>(X[hb + decltype(Q)::value], X[hb + decltype(Q)::value + dh]); });
+        });
+    });
+}
+
 }  // namespace rsm::bs8

@@ -47,9 +47,81 @@ static void emit(const char* name, bool ifft) {
     printf(" \"=&v\"(t0), \"=&v\"(t1), \"=&v\"(t2)\n        : \"s\"(A) : \"scc\");\n}\n");
 }
 
+// Half-split schedule (bs8.hpp small_ifft_h / small_fft_h): the small layers of ONE
+// half G in layout S' (register j of wave A holds e = (j & 7) + 8A + 64 (j >> 3)),
+// operands %0..%63 = X[8G + b][i] (operand 8b + i), %64..%66 temporaries, %67 = A.
+static void emit_half(const char* name, bool ifft, int G) {
+    const int kOffEnc = 127;
+    printf("RSM_BS8_DEV void %s(uint32_t (&X)[16][8], uint32_t A) {\n    uint32_t t0, t1, t2;\n    asm volatile(\n",
+           name);
+    for (int a = 0; a < 7; ++a) printf("        \"s_cmp_eq_u32 %%67, %d\\n\\ts_cbranch_scc1 .L%s%d_%%=\\n\\t\"\n", a, name, a);
+    printf("        \"s_branch .L%s7_%%=\\n\\t\"\n", name);
+    auto bfly = [&](int kind, unsigned L, int xs, int ys, std::vector<std::string>& out) {
+        auto map = [&](int c) { return c < 8 ? 8 * xs + c : c < 16 ? 8 * ys + (c - 8) : 64 + (c - 16); };
+        for (const Op& o : butterfly_ops(kind, L)) out.push_back(op_asm(o, map));
+    };
+    for (int a = 0; a < 8; ++a) {
+        std::vector<std::string> ins;
+        if (ifft) {
+            for (int d = 1; d <= 4; d <<= 1)
+                for (int b = 0; b < 8; b += 2 * d)
+                    for (int q = 0; q < d; ++q) bfly(0, kGf8.skew[kOffEnc + 8 * a + 64 * G + b + d], b + q, b + q + d, ins);
+        } else {
+            for (int d = 4; d >= 1; d >>= 1)
+                for (int b = 0; b < 8; b += 2 * d)
+                    for (int q = 0; q < d; ++q) bfly(1, kGf8.skew[-1 + 8 * a + 64 * G + b + d], b + q, b + q + d, ins);
+        }
+        printf("        \".L%s%d_%%=:\\n\\t\"\n", name, a);
+        for (const auto& s : ins) printf("        \"%s\\n\\t\"\n", s.c_str());
+        if (a < 7) printf("        \"s_branch .L%send_%%=\\n\\t\"\n", name);
+    }
+    printf("        \".L%send_%%=:\"\n        :", name);
+    for (int j = 8 * G; j < 8 * G + 8; ++j)
+        for (int i = 0; i < 8; ++i) printf(" \"+v\"(X[%d][%d]),", j, i);
+    printf(" \"=&v\"(t0), \"=&v\"(t1), \"=&v\"(t2)\n        : \"s\"(A) : \"scc\");\n}\n");
+}
+
+// Half-split exchange (kernels_gf8_bs.hip, bs_split_wave): half G is a transpose,
+// wave u's register 8G + v -> wave v's register 8G + u, through LDS entries
+//   (plane p, destination v, source u) at ((p * 8 + v) * 4 + u / 2) * 512 + lane * 8 + (u % 2) * 4
+// (a reader's two sources u, u + 1 share one ds_read_b64; the writers' lanes are 8 B
+// apart: a 2-way bank overlap that costs ds_write_b32 nothing).
+// xch_write_hG: 64 ds_write_b32, no wait (the caller waits and keeps X live until then);
+//   %0..%63 = X[8G + v][p] (operand 8v + p), %64 = lds + lane*8 + (u&1)*4 + (u>>1)*512, %65 = %64 + 65536.
+// xch_read_hG: 32 ds_read_b64 then lgkmcnt(0); outputs %0..%31 = T[s/2][p] (the pair
+//   X[8G + s][p], X[8G + s + 1][p]), %32 = lds + lane*8 + u*2048, %33 = %32 + 65536.
+static void emit_xch(int G) {
+    printf("RSM_BS8_DEV void xch_write_h%d(uint32_t (&X)[16][8], uint32_t va, uint32_t vb) {\n    asm volatile(\n", G);
+    for (int p = 0; p < 8; ++p)
+        for (int v = 0; v < 8; ++v)
+            printf("        \"ds_write_b32 %%%d, %%%d offset:%d\\n\\t\"\n", p < 4 ? 64 : 65, 8 * v + p, ((p % 4) * 8 + v) * 2048);
+    printf("        :");
+    for (int v = 0; v < 8; ++v)
+        for (int p = 0; p < 8; ++p) printf(" \"+v\"(X[%d][%d])%s", 8 * G + v, p, (v == 7 && p == 7) ? "" : ",");
+    printf("\n        : \"v\"(va), \"v\"(vb) : \"memory\");\n}\n");
+    printf("RSM_BS8_DEV void xch_read_h%d(uint32_t (&X)[16][8], uint32_t ra, uint32_t rb) {\n"
+           "    uint64_t T[4][8];\n    asm volatile(\n", G);
+    for (int p = 0; p < 8; ++p)
+        for (int s2 = 0; s2 < 4; ++s2)
+            printf("        \"ds_read_b64 %%%d, %%%d offset:%d\\n\\t\"\n", 8 * s2 + p, p < 4 ? 32 : 33, (p % 4) * 16384 + s2 * 512);
+    printf("        \"s_waitcnt lgkmcnt(0)\"\n        :");
+    for (int s2 = 0; s2 < 4; ++s2)
+        for (int p = 0; p < 8; ++p) printf(" \"=&v\"(T[%d][%d])%s", s2, p, (s2 == 3 && p == 7) ? "" : ",");
+    printf("\n        : \"v\"(ra), \"v\"(rb) : \"memory\");\n");
+    printf("    for (int s2 = 0; s2 < 4; ++s2)\n        for (int p = 0; p < 8; ++p) {\n"
+           "            X[%d + 2 * s2][p] = (uint32_t)T[s2][p];\n            X[%d + 2 * s2 + 1][p] = (uint32_t)(T[s2][p] >> 32);\n"
+           "        }\n}\n", 8 * G, 8 * G);
+}
+
 int main() {
     printf("// GENERATED by gen/gen_bs8_small.cpp -- do not edit.\n");
+    emit_xch(0);
+    emit_xch(1);
     emit("small_ifft_all", true);
     emit("small_fft_all", false);
+    emit_half("small_ifft_h0_all", true, 0);
+    emit_half("small_ifft_h1_all", true, 1);
+    emit_half("small_fft_h0_all", false, 0);
+    emit_half("small_fft_h1_all", false, 1);
     return 0;
 }

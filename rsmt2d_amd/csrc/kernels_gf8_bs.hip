@@ -816,6 +816,382 @@ __device__ __forceinline__ void bs_queue_wave(const QueuePlan& p, uint32_t* lds,
     }
 }
 
+// ---------------------------------------------------------------------------
+// Half-split schedule (production since round 3): the same queue, hand-off and
+// per-set arithmetic as bs_queue_wave, with the set's 128 symbols split by bit 6
+// into two halves that are independent in every layer but the merged middle pair
+// (bs8.hpp, "Half-split schedule").  Each LDS exchange moves one half while the
+// VALU works on the other, so the exchange (a quarter of the set's time when the
+// waves wait for it: profiles/r03_qab.jsonl) overlaps arithmetic:
+//   top   X[h0] <- P (direct loads of the previous set); direct loads of the NEXT
+//         set's h0 -> P; transposes + small IFFT h0; X[h1] <- R (LDS-DMA landed)
+//   write h0 -> R            || transposes + small IFFT h1
+//   read  h0 (layout L)      ;  write h1 -> R || large IFFT h0
+//   read  h1                 ;  large IFFT h1, middle pair, large FFT h0
+//   write h0 -> R            || large FFT h1
+//   read  h0 (layout S')     ;  write h1 -> R || small FFT h0, planes -> bytes, stores h0
+//   read  h1                 ;  LDS-DMA of the NEXT set's h1 -> R || small FFT h1,
+//                               planes -> bytes, stores h1
+// LDS: R = [0, 128 KiB) (one half's exchange, or the landing zone of the next set's
+// h1); the queue slot words at 128 KiB.  Loads of symbol e of the set: h0 registers
+// j < 8 hold e = j + 8A, h1 registers e = (j - 8) + 8A + 64.
+constexpr uint32_t kRBytes = 128u * 1024u;
+constexpr uint32_t kSlotW = kRBytes / 4;
+
+__device__ __forceinline__ uint32_t e_split(uint32_t A, int j) {
+    return (uint32_t)(j & 7) + 8u * A + 64u * (uint32_t)(j >> 3);
+}
+
+// h1 (registers 8..15) of a set by LDS-DMA into wave A's 16 KiB of R
+template <bool NT>
+__device__ __forceinline__ void split_dma_h1(const CodewordSet& cs, const SetAddr& a, uint32_t lds_base, uint32_t A) {
+    const uint32_t k = cs.k, es = (uint32_t)cs.elem_stride;
+    bs8::sfor<8>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        const uint32_t so = sym_off(e_split(A, 8 + j), k, 0, es);
+        const uint32_t l = __builtin_amdgcn_readfirstlane(lds_base + A * 16384u + j * 2048u);
+        dma16<NT>(l, a.off[0], a.rs, so);
+        dma16<NT>(l + 1024u, a.off[1], a.rs, so);
+    });
+}
+// h0 (registers 0..7) of a set into P (direct loads)
+template <bool NT>
+__device__ __forceinline__ void split_direct_h0(const CodewordSet& cs, const SetAddr& a, uint32_t A,
+                                                uint32_t (&P)[8][8]) {
+    const uint32_t k = cs.k, es = (uint32_t)cs.elem_stride;
+    const __amdgpu_buffer_rsrc_t rs = as_rsrc(a.rs);
+    bs8::sfor<8>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        const uint32_t so = sym_off(e_split(A, j), k, 0, es);
+        const v4u x = __builtin_amdgcn_raw_buffer_load_b128(rs, a.off[0], so, NT ? 2 : 0);
+        const v4u y = __builtin_amdgcn_raw_buffer_load_b128(rs, a.off[1], so, NT ? 2 : 0);
+        P[j][0] = x.x; P[j][1] = x.y; P[j][2] = x.z; P[j][3] = x.w;
+        P[j][4] = y.x; P[j][5] = y.y; P[j][6] = y.z; P[j][7] = y.w;
+    });
+}
+// planes -> bytes and the 16 stores of half G (Q1 write-through, Q2/Q3 non-temporal)
+template <int G, bool TRP, bool MEM_ON>
+__device__ __forceinline__ void split_store_h(uint32_t (&X)[16][8], const SetAddr& a, uint32_t A, uint32_t k,
+                                              uint32_t oo, uint32_t es, bool row, bool mem) {
+    const __amdgpu_buffer_rsrc_t ro = as_rsrc(a.ro);
+    bs8::sfor<8>([&](auto J) {
+        constexpr int j = 8 * G + decltype(J)::value;
+        if constexpr (TRP) bs8::transpose8_dev(X[j]);
+        const uint32_t so = sym_off(e_split(A, j), k, oo, es);
+        v4u x, y;
+        x.x = X[j][0]; x.y = X[j][1]; x.z = X[j][2]; x.w = X[j][3];
+        y.x = X[j][4]; y.y = X[j][5]; y.z = X[j][6]; y.w = X[j][7];
+        if (!MEM_ON || !mem) {
+        } else if (row) {
+            __builtin_amdgcn_raw_buffer_store_b128(x, ro, a.off[0], so, 16);
+            __builtin_amdgcn_raw_buffer_store_b128(y, ro, a.off[1], so, 16);
+        } else {
+            __builtin_amdgcn_raw_buffer_store_b128(x, ro, a.off[0], so, 2);
+            __builtin_amdgcn_raw_buffer_store_b128(y, ro, a.off[1], so, 2);
+        }
+        asm volatile("s_nop 2" ::: "memory");  // store-data hazard, see bs_uni_wave
+    });
+}
+// keep half G's registers allocated until the LDS writes that read them are done
+template <int G>
+__device__ __forceinline__ void keep_half(uint32_t (&X)[16][8]) {
+#pragma unroll
+    for (int v = 0; v < 8; ++v)
+        asm volatile("" : : "v"(X[8 * G + v][0]), "v"(X[8 * G + v][1]), "v"(X[8 * G + v][2]), "v"(X[8 * G + v][3]),
+                     "v"(X[8 * G + v][4]), "v"(X[8 * G + v][5]), "v"(X[8 * G + v][6]), "v"(X[8 * G + v][7]));
+}
+#define RSM_LDS_SYNC asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
+
+template <int MODE>
+__device__ __forceinline__ void bs_split_wave(const QueuePlan& p, uint32_t* lds, uint32_t lds_base, uint32_t A) {
+    // diagnostics (wrong output by design): 2 no arithmetic, 4 no global memory,
+    // 32768 no LDS exchange
+    constexpr bool ARITH = !(MODE & 2), XCH = !(MODE & 32768), NTQ0 = false, NTQ1 = true;
+    // A/B: 65536 = h0's small FFT and stores after the next set's LDS-DMA issue (a
+    // longer DMA lead, the last exchange write not overlapped)
+    constexpr bool LATE0 = (MODE & 65536) != 0;
+    const bool MEM = !(MODE & 4) || p.rows.S == 1;  // runtime-false in mode 4 (keeps the code alive)
+    const uint32_t lane = threadIdx.x & 63u;
+    const bool t0 = threadIdx.x == 0;
+    const uint32_t dread = lds_base + A * 16384u + lane * 16u;
+    const uint32_t xw = lds_base + lane * 8u + (A & 1u) * 4u + (A >> 1) * 512u, xr = lds_base + lane * 8u + A * 2048u;
+    uint32_t* slot = lds + kSlotW;
+    uint32_t X[16][8];
+    uint32_t P[8][8];
+    QClaim qc;
+
+    auto addr = [&](uint32_t row, uint32_t set) { return set_addr(row ? p.rows : p.cols, set, lane); };
+    auto issue_dma = [&](uint32_t row, uint32_t q1, const SetAddr& a) {
+        if (!MEM) return;
+        if (row) split_dma_h1<NTQ0>(p.rows, a, lds_base, A);
+        else if (q1) split_dma_h1<NTQ1>(p.cols, a, lds_base, A);
+        else split_dma_h1<NTQ0>(p.cols, a, lds_base, A);
+    };
+    auto issue_direct = [&](uint32_t row, uint32_t q1, const SetAddr& a) {
+        if (!MEM) return;
+        if (row) split_direct_h0<NTQ0>(p.rows, a, A, P);
+        else if (q1) split_direct_h0<NTQ1>(p.cols, a, A, P);
+        else split_direct_h0<NTQ0>(p.cols, a, A, P);
+    };
+
+    // prologue: the first two items, taken synchronously; the first one loaded
+    if (t0) {
+        uint32_t sq0 = 0, sq1 = 0, r0 = 1, r1 = 1;
+        const uint32_t c0 = q_take(p, qc, true, sq0, r0);
+        const uint32_t c1 = c0 == kNone ? kNone : q_take(p, qc, false, sq1, r1);
+        slot[0] = c0;
+        slot[1] = sq0;
+        slot[4] = c1;
+        slot[5] = sq1;
+        slot[6] = r1;
+        qc.rc = q_load(&p.ctr[kQReady]);
+        qc.qh = q_load(&p.ctr[kQHead1]);
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    uint32_t cur = __builtin_amdgcn_readfirstlane(slot[0]);
+    const uint32_t csq = __builtin_amdgcn_readfirstlane(slot[1]);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    uint32_t pend = kNone;  // square of a stored-but-unsignalled row set
+    if (cur != kNone) {
+        uint32_t crow, cset;
+        q_item(p, cur, csq, crow, cset);
+        {
+            const SetAddr a = addr(crow, cset);
+            issue_dma(crow, cur & kQ1, a);
+            issue_direct(crow, cur & kQ1, a);
+        }
+        if (t0) {
+            slot[0] = slot[4];
+            slot[1] = slot[5];
+            slot[2] = slot[6];
+        }
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        // thread 0, carried across the loop (as bs_queue_wave)
+        uint32_t cand = kNone, nn = kNone, nnsq = 0, nst = 0, rv = 0, sig = 0, sig_sq = kNone;
+        for (;;) {
+            // ---- top: h0 from P; the next item; its h0 direct loads ----
+            bs8::sfor<8>([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                bs8::sfor<8>([&](auto I) { X[j][decltype(I)::value] = P[j][decltype(I)::value]; });
+            });
+            const uint32_t nxt = __builtin_amdgcn_readfirstlane(slot[0]);
+            uint32_t nsq = __builtin_amdgcn_readfirstlane(slot[1]);
+            const uint32_t rdy = __builtin_amdgcn_readfirstlane(slot[2]);
+            const bool more = nxt != kNone;
+            const bool pre = more && rdy;
+            uint32_t nrow = 0, nset = 0;
+            SetAddr an{};
+            if (pre) {
+                q_item(p, nxt, nsq, nrow, nset);
+                an = addr(nrow, nset);
+                issue_direct(nrow, nxt & kQ1, an);
+            }
+            // no claim in a workgroup's last set (nothing would take the item)
+            if (t0) cand = more ? q_claim(p, qc) : kNone;
+            if constexpr (ARITH) {
+                bs8::sfor<8>([&](auto J) { bs8::transpose8_dev(X[decltype(J)::value]); });
+                bs8::small_ifft_h0_all(X, A);
+            }
+            // ---- h1 from the LDS-DMA landing zone (issued at the end of the last set) ----
+            // ops issued after it: the previous set's h1 stores (16; LATE0: and its h0
+            // stores, 16) and, if pre, this set's direct loads (16)
+            if constexpr (LATE0) {
+                if (pre) asm volatile("s_waitcnt vmcnt(48)\n\ts_barrier" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(32)\n\ts_barrier" ::: "memory");
+            } else {
+                if (pre) asm volatile("s_waitcnt vmcnt(32)\n\ts_barrier" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+            }
+            {
+                v4u g[8];
+                bs8::sfor<2>([&](auto Hh) {
+                    constexpr int hh = decltype(Hh)::value;
+                    ds_r16x8<8192 * hh, 1024>(dread, g);
+                    bs8::sfor<4>([&](auto J) {
+                        constexpr int j = 8 + 4 * hh + decltype(J)::value;
+                        const v4u x = g[2 * (j & 3)], y = g[2 * (j & 3) + 1];
+                        X[j][0] = x.x; X[j][1] = x.y; X[j][2] = x.z; X[j][3] = x.w;
+                        X[j][4] = y.x; X[j][5] = y.y; X[j][6] = y.z; X[j][7] = y.w;
+                    });
+                });
+            }
+            asm volatile("s_barrier" ::: "memory");  // every wave has read R
+            // ---- S' -> L, half 0 || small layers of h1 ----
+            if constexpr (XCH) bs8::xch_write_h0(X, xw, xw + 65536u);
+            if constexpr (ARITH) {
+                bs8::sfor<8>([&](auto J) { bs8::transpose8_dev(X[8 + decltype(J)::value]); });
+                bs8::small_ifft_h1_all(X, A);
+            }
+            RSM_LDS_SYNC;
+            keep_half<0>(X);
+            if constexpr (XCH) bs8::xch_read_h0(X, xr, xr + 65536u);
+            asm volatile("s_barrier" ::: "memory");
+            // ---- S' -> L, half 1 || large IFFT of h0 ----
+            if constexpr (XCH) bs8::xch_write_h1(X, xw, xw + 65536u);
+            if constexpr (ARITH) bs8::large_ifft_h<0>(X);
+            RSM_LDS_SYNC;
+            keep_half<1>(X);
+            if constexpr (XCH) bs8::xch_read_h1(X, xr, xr + 65536u);
+            asm volatile("s_barrier" ::: "memory");
+            if constexpr (ARITH) {
+                bs8::large_ifft_h<1>(X);
+                bs8::large_mid(X);
+                bs8::large_fft_h<0>(X);
+            }
+            // publish the row set stored at the end of the previous set: ops issued
+            // since its last stores = this set's direct loads (16, if pre)
+            if (pend != kNone) {
+                if (pre) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+                if (t0) {
+                    sig = q_add(&p.ctr[kQRows + pend]);
+                    sig_sq = pend;
+                }
+                pend = kNone;
+            }
+            // the claim (issued at the top of the set) becomes the next-next item; a Q1
+            // item's readiness is loaded now and read after the next exchange
+            asm volatile("" : "+v"(cand));
+            if (t0) {
+                nnsq = 0u;
+                nst = 0u;
+                uint32_t it = cand;
+                if (it != kNone && it != kQExitCheck && !(it & kQ1) && it >= p.nmain) {
+                    qc.main_done = 1u;
+                    it = qc.res != kNone ? qc.res : kQExitCheck;
+                }
+                if (it == kQExitCheck) it = q_leave_or_claim(p);
+                if (it == kNone || ((it & kQ1) && (it & ~kQ1) >= p.nq1)) {
+                    nn = kNone;
+                } else {
+                    nn = it;
+                    if (it & kQ1) {
+                        nst = 1u;
+                        rv = q_load(&p.ctr[kQRows + p.count + (it & ~kQ1) / p.rn]);
+                    }
+                }
+                qc.rc = q_load(&p.ctr[kQReady]);
+                qc.qh = q_load(&p.ctr[kQHead1]);
+            }
+            // ---- L -> S', half 0 || large FFT of h1 ----
+            if constexpr (XCH) bs8::xch_write_h0(X, xw, xw + 65536u);
+            if constexpr (ARITH) bs8::large_fft_h<1>(X);
+            if (t0) {
+                asm volatile("" : "+v"(sig), "+v"(rv));
+                if (sig_sq != kNone) {
+                    if (sig == p.rn - 1u) q_publish(p, sig_sq);
+                    sig_sq = kNone;
+                }
+                uint32_t r = 1u;
+                if (nst == 1u) {
+                    if (rv != 0u) {
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                        nnsq = rv - 1u;
+                        if (nn == qc.res) qc.res = kNone;
+                    } else {
+                        // not published yet: keep it in reserve and take a main item
+                        qc.res = nn;
+                        uint32_t u = p.nmain;
+                        if (!qc.main_done) u = q_add(&p.ctr[kQMain]);
+                        if (u < p.nmain) {
+                            nn = u;
+                        } else {
+                            qc.main_done = 1u;
+                            qc.res = kNone;
+                            r = 0u;  // main sequence exhausted: the slow path waits for it
+                        }
+                    }
+                }
+                slot[0] = nn;
+                slot[1] = nnsq;
+                slot[2] = r;
+            }
+            RSM_LDS_SYNC;
+            keep_half<0>(X);
+            if constexpr (XCH) bs8::xch_read_h0(X, xr, xr + 65536u);
+            asm volatile("s_barrier" ::: "memory");
+            // ---- L -> S', half 1 || small FFT, bytes and stores of h0 ----
+            const SetAddr a = addr(crow, cset);
+            const uint32_t k = p.rows.k;
+            const uint32_t oo = (uint32_t)(crow ? p.rows.out_offset : p.cols.out_offset);
+            const uint32_t es = (uint32_t)(crow ? p.rows.elem_stride : p.cols.elem_stride);
+            if constexpr (XCH) bs8::xch_write_h1(X, xw, xw + 65536u);
+            if constexpr (!LATE0) {
+                if constexpr (ARITH) bs8::small_fft_h0_all(X, A);
+                split_store_h<0, ARITH, true>(X, a, A, k, oo, es, crow != 0, MEM);
+            }
+            RSM_LDS_SYNC;
+            keep_half<1>(X);
+            if constexpr (XCH) bs8::xch_read_h1(X, xr, xr + 65536u);
+            asm volatile("s_barrier" ::: "memory");  // R free: the next set's h1 may land
+            if (pre) issue_dma(nrow, nxt & kQ1, an);
+            if constexpr (LATE0) {
+                if constexpr (ARITH) bs8::small_fft_h0_all(X, A);
+                split_store_h<0, ARITH, true>(X, a, A, k, oo, es, crow != 0, MEM);
+            }
+            if constexpr (ARITH) bs8::small_fft_h1_all(X, A);
+            split_store_h<1, ARITH, true>(X, a, A, k, oo, es, crow != 0, MEM);
+            if (crow) pend = cset / p.rn;
+            if (!more) break;
+            if (!pre) {
+                // slow path (main sequence exhausted, next Q1 set not ready): publish our
+                // own row set first, wait, then load the next set synchronously
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+                if (t0) {
+                    if (pend != kNone) q_signal(p, pend);
+                    slot[3] = q_wait(p, nxt);
+                }
+                pend = kNone;
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+                nsq = __builtin_amdgcn_readfirstlane(slot[3]);
+                if (nsq == kNone) break;  // stuck wait: skip the set, drain
+                q_item(p, nxt, nsq, nrow, nset);
+                an = addr(nrow, nset);
+                issue_dma(nrow, nxt & kQ1, an);
+                issue_direct(nrow, nxt & kQ1, an);
+                __builtin_amdgcn_s_waitcnt(0x0F70);
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            }
+            cur = nxt;
+            crow = nrow;
+            cset = nset;
+        }
+    }
+    // drain: every wave's stores, then the last row set's signal and the exit count;
+    // the last workgroup out re-zeroes the queue for the next launch on these words
+    // (all its threads: 2 * count words)
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (t0) {
+        if (pend != kNone) q_signal(p, pend);
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        slot[0] = q_add(&p.ctr[kQExit]) == gridDim.x - 1u ? 1u : 0u;
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (__builtin_amdgcn_readfirstlane(slot[0])) {
+        for (uint32_t s = threadIdx.x; s < 2u * p.count; s += blockDim.x) q_store(&p.ctr[kQRows + s], 0u);
+        if (t0) {
+            if (q_load(&p.ctr[kQErr])) {
+                __hip_atomic_store(p.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                q_store(&p.ctr[kQErr], 0u);
+            }
+            q_store(&p.ctr[kQMain], 0u);
+            q_store(&p.ctr[kQHead1], 0u);
+            q_store(&p.ctr[kQReady], 0u);
+            q_store(&p.ctr[kQRes], 0u);
+            q_store(&p.ctr[kQLeft], 0u);
+            q_store(&p.ctr[kQExit], 0u);
+        }
+    }
+}
+#undef RSM_LDS_SYNC
+
+template <int MODE>
+__global__ __launch_bounds__(512, 1) void extend_gf8_bs128s_kernel(QueuePlan p) {
+    __shared__ uint32_t lds[(kDmaBytes + kXchBytes) / 4];
+    bs_split_wave<MODE>(p, lds, (uint32_t)(uintptr_t)lds, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
+}
+
 template <int MODE>
 __global__ __launch_bounds__(512, 1) void extend_gf8_bs128q_kernel(QueuePlan p) {
     __shared__ uint32_t lds[(kDmaBytes + kXchBytes) / 4];
@@ -1046,6 +1422,15 @@ hipError_t launch_extend_gf8_bs128_queue(const QueuePlan& p, hipStream_t st) {
     // 4200 = 104 + Q1 default policy, 10280 rows after the small IFFT / columns after
     // the exchange
     switch (g_diag_mode.load()) {
+        // half-split schedule (production) and its diagnostic variants
+        case 40: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<0>), dim3(grid), dim3(512), 0, st, p); break;
+        case 50002: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<2>), dim3(grid), dim3(512), 0, st, p); break;
+        case 50004: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<4>), dim3(grid), dim3(512), 0, st, p); break;
+        case 50768: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<32768>), dim3(grid), dim3(512), 0, st, p); break;
+        case 50772: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<32772>), dim3(grid), dim3(512), 0, st, p); break;
+        case 65536: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<65536>), dim3(grid), dim3(512), 0, st, p); break;
+        // round-2 schedule (bs_queue_wave) for A/B
+        case 18472: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<18472>), dim3(grid), dim3(512), 0, st, p); break;
         case 2: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<18474>), dim3(grid), dim3(512), 0, st, p); break;
         case 4: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<18476>), dim3(grid), dim3(512), 0, st, p); break;
         case 104: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<104>), dim3(grid), dim3(512), 0, st, p); break;
@@ -1062,10 +1447,10 @@ hipError_t launch_extend_gf8_bs128_queue(const QueuePlan& p, hipStream_t st) {
         case 131072: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<18472 | 131072>), dim3(grid), dim3(512), 0, st, p); break;
         case 98304: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<18472 | 98304>), dim3(grid), dim3(512), 0, st, p); break;
         case 32772: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<18476 | 32768>), dim3(grid), dim3(512), 0, st, p); break;
-        default: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<18472>), dim3(grid), dim3(512), 0, st, p); break;
+        default: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<0>), dim3(grid), dim3(512), 0, st, p); break;
     }
 #else
-    hipLaunchKernelGGL((extend_gf8_bs128q_kernel<18472>), dim3(grid), dim3(512), 0, st, p);
+    hipLaunchKernelGGL((extend_gf8_bs128s_kernel<0>), dim3(grid), dim3(512), 0, st, p);
 #endif
     return hipGetLastError();
 }

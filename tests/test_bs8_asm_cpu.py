@@ -111,3 +111,32 @@ def test_small_layer_blocks(gf, name, inverse):
                                                            ref[b + q], ref[b + q + d], mul)
         for j in range(16):
             assert unplanes(regs[8 * j:8 * j + 8]).tobytes() == ref[j].tobytes(), (name, A, j)
+
+
+@pytest.mark.parametrize("G", [0, 1])
+@pytest.mark.parametrize("name,inverse", [("small_ifft_h%d_all", True), ("small_fft_h%d_all", False)])
+def test_half_split_small_layer_blocks(gf, name, inverse, G):
+    """The half-split schedule's small layers (layout S': register b of half G of
+    wave A holds e = b + 8A + 64G; d = 1, 2, 4 on b; bs8.hpp small_ifft_h)."""
+    mul, skew = gf
+    name = name % G
+    text = open(os.path.join(CSRC, "bs8_small.inc")).read()
+    fn = re.search(r"void %s\(.*?\{(.*?)\n\}" % name, text, re.S).group(1)
+    parts = re.split(r"\.L%s(\d)_%%=:" % name, fn)
+    bodies = {int(parts[i]): parts[i + 1] for i in range(1, len(parts), 2)}
+    assert sorted(bodies) == list(range(8))
+    rng = np.random.default_rng(10 + G)
+    for A, body in bodies.items():
+        sym = [rng.integers(0, 256, 32, dtype=np.uint8) for _ in range(8)]
+        regs = sum((planes(s) for s in sym), []) + [int(v) for v in rng.integers(0, 2**32, 3)]
+        execute(parse(body), regs)
+        ref = [s.copy() for s in sym]
+        for d in ((1, 2, 4) if inverse else (4, 2, 1)):
+            for b in range(0, 8, 2 * d):
+                e0 = 8 * A + 64 * G + b + d
+                L = skew[127 + e0] if inverse else skew[-1 + e0]
+                for q in range(d):
+                    ref[b + q], ref[b + q + d] = butterfly("ifft2_asm" if inverse else "fft2_asm", L,
+                                                           ref[b + q], ref[b + q + d], mul)
+        for j in range(8):
+            assert unplanes(regs[8 * j:8 * j + 8]).tobytes() == ref[j].tobytes(), (name, A, j)

@@ -28,7 +28,11 @@ def bs8_host(tmp_path_factory):
     return exe
 
 
+@pytest.mark.parametrize("split", [0, 1])
 @pytest.mark.parametrize("k,S", [(128, 512), (65, 64), (100, 192), (127, 1024)])
-def test_bitsliced_encode_matches_oracle(bs8_host, k, S):
-    r = subprocess.run([bs8_host, str(k), str(S), str(k * 7919 + S)], capture_output=True, text=True)
+def test_bitsliced_encode_matches_oracle(bs8_host, k, S, split):
+    """split 0: the two-launch kernel's schedule (small layout e = 16A + j); split 1:
+    the half-split schedule of the queue kernel (layout S', e = (j & 7) + 8A + 64 (j >> 3),
+    per-half small / large layers, transpose exchange per half)."""
+    r = subprocess.run([bs8_host, str(k), str(S), str(k * 7919 + S), str(split)], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr

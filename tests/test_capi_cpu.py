@@ -145,14 +145,16 @@ def test_product_has_no_diagnostics(lib):
         assert name not in blob, name
     assert not re.search(rb"RSM_[A-Z0-9_]{3,}\x00", blob), re.search(rb"RSM_[A-Z0-9_]{3,}\x00", blob)
     # kernel symbols embedded in the gfx950 code object: only the production modes
-    # of the bit-sliced encode (row pass 104, column pass 184, single-launch queue
-    # extension 18472: kernels_gf8_bs.hip), no diagnostic mode (bits 2 / 4: no
-    # arithmetic / no memory), no dual (bs128p) kernel
+    # of the bit-sliced encode (row pass 104, column pass 184, the single-launch
+    # half-split queue extension 0: kernels_gf8_bs.hip), no diagnostic mode (bits
+    # 2 / 4 / 32768: no arithmetic / no memory / no exchange), no round-2 queue
+    # kernel (diag A/B only), no dual (bs128p) kernel
     modes = set(re.findall(rb"encode_gf8_bs128u_kernelILi(\d+)E", blob))
     assert modes == {b"104", b"184"}, modes
-    qmodes = set(re.findall(rb"extend_gf8_bs128q_kernelILi(\d+)E", blob))
-    assert qmodes == {b"18472"}, qmodes
-    assert not any(int(m) & 6 for m in modes | qmodes)
+    smodes = set(re.findall(rb"extend_gf8_bs128s_kernelILi(\d+)E", blob))
+    assert smodes == {b"0"}, smodes
+    assert b"extend_gf8_bs128q_kernel" not in blob
+    assert not any(int(m) & (6 | 32768) for m in modes | smodes)
     assert b"encode_gf8_bs128p_kernel" not in blob
     txt = re.sub(r"/\*.*?\*/", "", open(DIAG_HEADER).read(), flags=re.S)
     for s in set(re.findall(r"\b(rsm_diag_[a-z0-9_]+)\s*\(", txt)):
@@ -165,7 +167,8 @@ def test_diag_library_is_separate():
     if not os.path.exists(R.DIAG_LIB_PATH):
         pytest.skip("diagnostic library not built")
     blob = open(R.DIAG_LIB_PATH, "rb").read()
-    assert set(re.findall(rb"extend_gf8_bs128q_kernelILi(\d+)E", blob)) > {b"18472"}  # + A-B / diagnostic modes
+    assert set(re.findall(rb"extend_gf8_bs128q_kernelILi(\d+)E", blob)) > {b"18472"}  # round-2 schedule, A-B
+    assert set(re.findall(rb"extend_gf8_bs128s_kernelILi(\d+)E", blob)) > {b"0"}  # + diagnostic modes
     dl = R.diag_library()
     for s in R.DIAG_SIGNATURES:
         assert hasattr(dl, s), s

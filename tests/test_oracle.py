@@ -144,3 +144,12 @@ def test_simd_restatement_matches_scalar(k, S):
     """The AVX2 build (cpu_baseline) computes exactly what the scalar oracle does."""
     ods = oracle.splitmix64_bytes(k * k * S, seed=0x51D + k).reshape(k, k, S)
     assert np.array_equal(oracle.extend_square_simd(ods, nthreads=4), oracle.extend_square(ods, nthreads=4))
+
+
+@pytest.mark.skipif(not oracle.gfni_supported(), reason="host has no GFNI / AVX-512BW")
+@pytest.mark.parametrize("k,S", [(1, 64), (2, 64), (4, 512), (16, 128), (128, 512)])
+def test_gfni_restatement_matches_scalar(k, S):
+    """The cpu_baseline's AVX-512 GFNI build (fused butterflies, GF2P8AFFINEQB
+    multiplies) computes exactly the scalar oracle's extension."""
+    ods = np.random.default_rng(k * 31 + S).integers(0, 256, (k, k, S), dtype=np.uint8)
+    assert np.array_equal(oracle.extend_square_gfni(ods, nthreads=4), oracle.extend_square(ods, nthreads=4))
