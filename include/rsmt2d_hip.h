@@ -98,8 +98,8 @@ int rsm_host_free(rsm_ctx* ctx, void* p);
 /* Device-resident, in place: d_eds holds `count` consecutive [2k][2k][S] squares
  * whose top-left quadrant already holds the ODS (the EDS aliases the ODS, as in
  * ComputeExtendedDataSquare).  Enqueued on `stream` (a hipStream_t of this
- * library's HIP runtime; NULL = the context stream); asynchronous.  Batches of
- * >= 2 squares with k = 128 run both passes as ONE queue-driven launch; its
+ * library's HIP runtime; NULL = the context stream); asynchronous.  Squares with
+ * k = 128 (one or a batch) run both passes as ONE queue-driven launch; its
  * bounded waits cannot time out short of a hardware fault, and if one did, the
  * stream's next rsm_stream_check (rsm_sync for the context stream), its
  * rsm_stream_destroy or the next extension on that stream returns RSM_EDEVICE. */

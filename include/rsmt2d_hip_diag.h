@@ -23,6 +23,9 @@ int rsm_diag_set_bs_mode(int mode, int rev_col, int xcd);
 /* Kernel variant of the row pass alone (same codes; the setting above then applies
  * to every other launch). */
 int rsm_diag_set_bs_row_mode(int mode);
+/* Phase timeline of the half-split queue kernel's trace modes (51010/51012/51014):
+ * d_trace = device buffer of 256 workgroups x 256 sets x 12 words (NULL: off). */
+int rsm_diag_set_trace(void* d_trace);
 /* Both passes of `count` in-place k = 128 squares in ONE persistent launch
  * (extend_gf8_bs128q_kernel: row and Q0-column sets from one queue, Q1-column sets
  * from a ready list; `delay` squares of row sets lead the Q0-column sets).

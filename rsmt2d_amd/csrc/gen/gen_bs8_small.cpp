@@ -113,10 +113,94 @@ static void emit_xch(int G) {
            "        }\n}\n", 8 * G, 8 * G);
 }
 
+// Interleaved phases of the half-split schedule: the 64 exchange writes of half W
+// (ds_write_b32, entries as in emit_xch) spread evenly through the VALU work of the
+// OTHER half, so the LDS takes the writes while the SIMDs compute (a separate asm
+// block of 64 writes stalls the wave until the LDS has accepted them).  VALU work:
+//   kind 0: planes <-> bytes transposes of registers 8(1-W) .. 8(1-W)+7 (transpose8_dev);
+//   kind 1: large IFFT of half 1-W (bs8.hpp large_ifft_h);  kind 2: large FFT of half 1-W.
+// Operands: %0..%127 X[j][i] (8j + i), %128..%131 temporaries, %132..%137 the transpose
+// masks (SGPRs), %138 / %139 the write addresses (p < 4 / p >= 4).
+static void emit_phase(const char* name, int W, int kind) {
+    const int V = 1 - W;
+    std::vector<std::string> valu, wr;
+    for (int p = 0; p < 8; ++p)
+        for (int v = 0; v < 8; ++v) {
+            char b[96];
+            snprintf(b, sizeof b, "ds_write_b32 %%%d, %%%d offset:%d", p < 4 ? 138 : 139, 8 * (8 * W + v) + p,
+                     ((p % 4) * 8 + v) * 2048);
+            wr.push_back(b);
+        }
+    auto reg = [](int j, int i) { return 8 * j + i; };
+    if (kind == 0) {
+        // transpose8_dev, same instruction sequence (bs8.hpp)
+        struct G { int a0, b0, a1, b1, s, m, mh; };
+        const G gs[6] = {{0, 4, 1, 5, 4, 132, 133}, {2, 6, 3, 7, 4, 132, 133}, {0, 2, 1, 3, 2, 134, 135},
+                         {4, 6, 5, 7, 2, 134, 135}, {0, 1, 2, 3, 1, 136, 137}, {4, 5, 6, 7, 1, 136, 137}};
+        for (int j = 8 * V; j < 8 * V + 8; ++j)
+            for (const G& g : gs) {
+                char b[128];
+                auto shl = [&](int d, int src) {
+                    if (g.s == 1) snprintf(b, sizeof b, "v_add_u32 %%%d, %%%d, %%%d", d, reg(j, src), reg(j, src));
+                    else snprintf(b, sizeof b, "v_lshlrev_b32 %%%d, %d, %%%d", d, g.s, reg(j, src));
+                    valu.push_back(b);
+                };
+                shl(128, g.b0);
+                snprintf(b, sizeof b, "v_lshrrev_b32 %%129, %d, %%%d", g.s, reg(j, g.a0));
+                valu.push_back(b);
+                shl(130, g.b1);
+                snprintf(b, sizeof b, "v_lshrrev_b32 %%131, %d, %%%d", g.s, reg(j, g.a1));
+                valu.push_back(b);
+                snprintf(b, sizeof b, "v_bitop3_b32 %%%d, %%%d, %%128, %%%d bitop3:0xd8", reg(j, g.a0), reg(j, g.a0), g.mh);
+                valu.push_back(b);
+                snprintf(b, sizeof b, "v_bitop3_b32 %%%d, %%%d, %%129, %%%d bitop3:0xd8", reg(j, g.b0), reg(j, g.b0), g.m);
+                valu.push_back(b);
+                snprintf(b, sizeof b, "v_bitop3_b32 %%%d, %%%d, %%130, %%%d bitop3:0xd8", reg(j, g.a1), reg(j, g.a1), g.mh);
+                valu.push_back(b);
+                snprintf(b, sizeof b, "v_bitop3_b32 %%%d, %%%d, %%131, %%%d bitop3:0xd8", reg(j, g.b1), reg(j, g.b1), g.m);
+                valu.push_back(b);
+            }
+    } else {
+        const int kOffEnc = 127;
+        auto bfly = [&](int bk, unsigned L, int xs, int ys) {
+            auto map = [&](int c) { return c < 8 ? reg(xs, c) : c < 16 ? reg(ys, c - 8) : 128 + (c - 16); };
+            for (const Op& o : butterfly_ops(bk, L)) valu.push_back(op_asm(o, map));
+        };
+        for (int li = 0; li < 3; ++li) {
+            const int dh = kind == 1 ? (1 << li) : (4 >> li);
+            for (int bb = 0; bb < 8; bb += 2 * dh) {
+                const int hb = 8 * V + bb;
+                const unsigned L = kind == 1 ? kGf8.skew[kOffEnc + 8 * hb + 8 * dh] : kGf8.skew[-1 + 8 * hb + 8 * dh];
+                for (int q = 0; q < dh; ++q) bfly(kind == 1 ? 0 : 1, L, hb + q, hb + q + dh);
+            }
+        }
+    }
+    printf("RSM_BS8_DEV void %s(uint32_t (&X)[16][8], uint32_t va, uint32_t vb) {\n"
+           "    uint32_t t0, t1, t2, t3;\n    asm volatile(\n", name);
+    const size_t n = valu.size();
+    size_t w = 0;
+    for (size_t i = 0; i < n; ++i) {
+        // write w goes after VALU instruction floor((w + 1) * n / 65) (evenly spread)
+        while (w < wr.size() && (w + 1) * n / (wr.size() + 1) <= i) printf("        \"%s\\n\\t\"\n", wr[w++].c_str());
+        printf("        \"%s\\n\\t\"\n", valu[i].c_str());
+    }
+    while (w < wr.size()) printf("        \"%s\\n\\t\"\n", wr[w++].c_str());
+    printf("        \"s_nop 0\"\n        :");
+    for (int j = 0; j < 16; ++j)
+        for (int i = 0; i < 8; ++i) printf(" \"+v\"(X[%d][%d]),", j, i);
+    printf(" \"=&v\"(t0), \"=&v\"(t1), \"=&v\"(t2), \"=&v\"(t3)\n"
+           "        : \"s\"(0x0F0F0F0Fu), \"s\"(0xF0F0F0F0u), \"s\"(0x33333333u), \"s\"(0xCCCCCCCCu), "
+           "\"s\"(0x55555555u), \"s\"(0xAAAAAAAAu), \"v\"(va), \"v\"(vb) : \"memory\");\n}\n");
+}
+
 int main() {
     printf("// GENERATED by gen/gen_bs8_small.cpp -- do not edit.\n");
     emit_xch(0);
     emit_xch(1);
+    emit_phase("ph_w0_tr1", 0, 0);    // S' -> L half 0  || transposes of h1 (bytes -> planes)
+    emit_phase("ph_w1_lifft0", 1, 1); // S' -> L half 1  || large IFFT of h0
+    emit_phase("ph_w0_lfft1", 0, 2);  // L -> S' half 0  || large FFT of h1
+    emit_phase("ph_w1_tr0", 1, 0);    // L -> S' half 1  || transposes of h0 (planes -> bytes)
     emit("small_ifft_all", true);
     emit("small_fft_all", false);
     emit_half("small_ifft_h0_all", true, 0);

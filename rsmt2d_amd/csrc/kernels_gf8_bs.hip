@@ -854,15 +854,15 @@ __device__ __forceinline__ void split_dma_h1(const CodewordSet& cs, const SetAdd
         dma16<NT>(l + 1024u, a.off[1], a.rs, so);
     });
 }
-// h0 (registers 0..7) of a set into P (direct loads)
-template <bool NT>
+// half G (registers 8G..8G+7) of a set into P (direct loads)
+template <bool NT, int G = 0>
 __device__ __forceinline__ void split_direct_h0(const CodewordSet& cs, const SetAddr& a, uint32_t A,
                                                 uint32_t (&P)[8][8]) {
     const uint32_t k = cs.k, es = (uint32_t)cs.elem_stride;
     const __amdgpu_buffer_rsrc_t rs = as_rsrc(a.rs);
     bs8::sfor<8>([&](auto J) {
         constexpr int j = decltype(J)::value;
-        const uint32_t so = sym_off(e_split(A, j), k, 0, es);
+        const uint32_t so = sym_off(e_split(A, 8 * G + j), k, 0, es);
         const v4u x = __builtin_amdgcn_raw_buffer_load_b128(rs, a.off[0], so, NT ? 2 : 0);
         const v4u y = __builtin_amdgcn_raw_buffer_load_b128(rs, a.off[1], so, NT ? 2 : 0);
         P[j][0] = x.x; P[j][1] = x.y; P[j][2] = x.z; P[j][3] = x.w;
@@ -901,6 +901,16 @@ __device__ __forceinline__ void keep_half(uint32_t (&X)[16][8]) {
                      "v"(X[8 * G + v][4]), "v"(X[8 * G + v][5]), "v"(X[8 * G + v][6]), "v"(X[8 * G + v][7]));
 }
 #define RSM_LDS_SYNC asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
+// diagnostic phase timeline (TRACE): thread 0 records the 100 MHz real-time clock at
+// phase boundaries, one row of kTraceWords per (workgroup, set); vector stores only
+__device__ __forceinline__ void trace_stamp(const QueuePlan& p, uint32_t it, int w, uint32_t v) {
+#ifdef RSM_DIAG
+    if (p.trace && it < kTraceSets) {
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(p.trace, (short)0, 0x7FFFFFFF, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b32(v, r, ((blockIdx.x * kTraceSets + it) * kTraceWords + w) * 4u, 0, 0);
+    }
+#endif
+}
 
 template <int MODE>
 __device__ __forceinline__ void bs_split_wave(const QueuePlan& p, uint32_t* lds, uint32_t lds_base, uint32_t A) {
@@ -910,6 +920,22 @@ __device__ __forceinline__ void bs_split_wave(const QueuePlan& p, uint32_t* lds,
     // A/B: 65536 = h0's small FFT and stores after the next set's LDS-DMA issue (a
     // longer DMA lead, the last exchange write not overlapped)
     constexpr bool LATE0 = (MODE & 65536) != 0;
+    // 131072: the exchange writes issued as separate blocks (A/B against the
+    // production form, which interleaves them with the other half's VALU work)
+    constexpr bool IL = ARITH && XCH && !LATE0 && !(MODE & 131072);
+    // 262144: no LDS-DMA -- h1 of the next set by direct loads into Q right after this
+    // set's h0 stores (the LDS region R then holds only exchanges)
+    constexpr bool NODMA = (MODE & 262144) != 0 && !LATE0;
+    // 1048576: no LDS-DMA -- P holds h1 of the next set (loaded at the top), h0 of the
+    // next set is loaded into X[0..7] right after this set's h0 stores
+    constexpr bool XLOAD = (MODE & 1048576) != 0 && !NODMA && !LATE0;
+    // 524288: phase timeline into p.trace (diagnostic build)
+    constexpr bool TRACE = (MODE & 524288) != 0;
+    uint32_t it_no = 0;
+    auto stamp = [&](int w) {
+        if constexpr (TRACE)
+            if (threadIdx.x == 0) trace_stamp(p, it_no, w, (uint32_t)__builtin_amdgcn_s_memrealtime());
+    };
     const bool MEM = !(MODE & 4) || p.rows.S == 1;  // runtime-false in mode 4 (keeps the code alive)
     const uint32_t lane = threadIdx.x & 63u;
     const bool t0 = threadIdx.x == 0;
@@ -918,20 +944,41 @@ __device__ __forceinline__ void bs_split_wave(const QueuePlan& p, uint32_t* lds,
     uint32_t* slot = lds + kSlotW;
     uint32_t X[16][8];
     uint32_t P[8][8];
+    uint32_t Q[8][8];  // NODMA: h1 of the next set
     QClaim qc;
 
     auto addr = [&](uint32_t row, uint32_t set) { return set_addr(row ? p.rows : p.cols, set, lane); };
     auto issue_dma = [&](uint32_t row, uint32_t q1, const SetAddr& a) {
         if (!MEM) return;
+        if constexpr (NODMA) {
+            if (row) split_direct_h0<NTQ0, 1>(p.rows, a, A, Q);
+            else if (q1) split_direct_h0<NTQ1, 1>(p.cols, a, A, Q);
+            else split_direct_h0<NTQ0, 1>(p.cols, a, A, Q);
+            return;
+        }
         if (row) split_dma_h1<NTQ0>(p.rows, a, lds_base, A);
         else if (q1) split_dma_h1<NTQ1>(p.cols, a, lds_base, A);
         else split_dma_h1<NTQ0>(p.cols, a, lds_base, A);
     };
     auto issue_direct = [&](uint32_t row, uint32_t q1, const SetAddr& a) {
         if (!MEM) return;
+        if constexpr (XLOAD) {  // P = h1
+            if (row) split_direct_h0<NTQ0, 1>(p.rows, a, A, P);
+            else if (q1) split_direct_h0<NTQ1, 1>(p.cols, a, A, P);
+            else split_direct_h0<NTQ0, 1>(p.cols, a, A, P);
+            return;
+        }
         if (row) split_direct_h0<NTQ0>(p.rows, a, A, P);
         else if (q1) split_direct_h0<NTQ1>(p.cols, a, A, P);
         else split_direct_h0<NTQ0>(p.cols, a, A, P);
+    };
+    // XLOAD: h0 of a set straight into X[0..7]
+    auto issue_x0 = [&](uint32_t row, uint32_t q1, const SetAddr& a) {
+        uint32_t (&X0)[8][8] = *reinterpret_cast<uint32_t (*)[8][8]>(&X[0][0]);
+        if (!MEM) return;
+        if (row) split_direct_h0<NTQ0, 0>(p.rows, a, A, X0);
+        else if (q1) split_direct_h0<NTQ1, 0>(p.cols, a, A, X0);
+        else split_direct_h0<NTQ0, 0>(p.cols, a, A, X0);
     };
 
     // prologue: the first two items, taken synchronously; the first one loaded
@@ -957,7 +1004,8 @@ __device__ __forceinline__ void bs_split_wave(const QueuePlan& p, uint32_t* lds,
         q_item(p, cur, csq, crow, cset);
         {
             const SetAddr a = addr(crow, cset);
-            issue_dma(crow, cur & kQ1, a);
+            if constexpr (XLOAD) issue_x0(crow, cur & kQ1, a);
+            else issue_dma(crow, cur & kQ1, a);
             issue_direct(crow, cur & kQ1, a);
         }
         if (t0) {
@@ -970,10 +1018,12 @@ __device__ __forceinline__ void bs_split_wave(const QueuePlan& p, uint32_t* lds,
         // thread 0, carried across the loop (as bs_queue_wave)
         uint32_t cand = kNone, nn = kNone, nnsq = 0, nst = 0, rv = 0, sig = 0, sig_sq = kNone;
         for (;;) {
-            // ---- top: h0 from P; the next item; its h0 direct loads ----
+            stamp(0);
+            // ---- top: h0 from P (XLOAD: h1 from P, h0 already in X); the next item;
+            // its P loads ----
             bs8::sfor<8>([&](auto J) {
                 constexpr int j = decltype(J)::value;
-                bs8::sfor<8>([&](auto I) { X[j][decltype(I)::value] = P[j][decltype(I)::value]; });
+                bs8::sfor<8>([&](auto I) { X[(XLOAD ? 8 : 0) + j][decltype(I)::value] = P[j][decltype(I)::value]; });
             });
             const uint32_t nxt = __builtin_amdgcn_readfirstlane(slot[0]);
             uint32_t nsq = __builtin_amdgcn_readfirstlane(slot[1]);
@@ -993,6 +1043,13 @@ __device__ __forceinline__ void bs_split_wave(const QueuePlan& p, uint32_t* lds,
                 bs8::sfor<8>([&](auto J) { bs8::transpose8_dev(X[decltype(J)::value]); });
                 bs8::small_ifft_h0_all(X, A);
             }
+            if constexpr (XLOAD) {
+            } else if constexpr (NODMA) {
+                bs8::sfor<8>([&](auto J) {
+                    constexpr int j = decltype(J)::value;
+                    bs8::sfor<8>([&](auto I) { X[8 + j][decltype(I)::value] = Q[j][decltype(I)::value]; });
+                });
+            } else {
             // ---- h1 from the LDS-DMA landing zone (issued at the end of the last set) ----
             // ops issued after it: the previous set's h1 stores (16; LATE0: and its h0
             // stores, 16) and, if pre, this set's direct loads (16)
@@ -1017,28 +1074,46 @@ __device__ __forceinline__ void bs_split_wave(const QueuePlan& p, uint32_t* lds,
                 });
             }
             asm volatile("s_barrier" ::: "memory");  // every wave has read R
-            // ---- S' -> L, half 0 || small layers of h1 ----
-            if constexpr (XCH) bs8::xch_write_h0(X, xw, xw + 65536u);
-            if constexpr (ARITH) {
-                bs8::sfor<8>([&](auto J) { bs8::transpose8_dev(X[8 + decltype(J)::value]); });
-                bs8::small_ifft_h1_all(X, A);
             }
+            stamp(1);
+            // ---- S' -> L, half 0 || small layers of h1 ----
+            if constexpr (IL) {
+                bs8::ph_w0_tr1(X, xw, xw + 65536u);
+                bs8::small_ifft_h1_all(X, A);
+            } else {
+                if constexpr (XCH) bs8::xch_write_h0(X, xw, xw + 65536u);
+                if constexpr (ARITH) {
+                    bs8::sfor<8>([&](auto J) { bs8::transpose8_dev(X[8 + decltype(J)::value]); });
+                    bs8::small_ifft_h1_all(X, A);
+                }
+            }
+            stamp(2);
             RSM_LDS_SYNC;
+            stamp(3);
             keep_half<0>(X);
             if constexpr (XCH) bs8::xch_read_h0(X, xr, xr + 65536u);
             asm volatile("s_barrier" ::: "memory");
+            stamp(4);
             // ---- S' -> L, half 1 || large IFFT of h0 ----
-            if constexpr (XCH) bs8::xch_write_h1(X, xw, xw + 65536u);
-            if constexpr (ARITH) bs8::large_ifft_h<0>(X);
+            if constexpr (IL) {
+                bs8::ph_w1_lifft0(X, xw, xw + 65536u);
+            } else {
+                if constexpr (XCH) bs8::xch_write_h1(X, xw, xw + 65536u);
+                if constexpr (ARITH) bs8::large_ifft_h<0>(X);
+            }
             RSM_LDS_SYNC;
             keep_half<1>(X);
             if constexpr (XCH) bs8::xch_read_h1(X, xr, xr + 65536u);
             asm volatile("s_barrier" ::: "memory");
+            stamp(5);
+            if constexpr (TRACE) if (threadIdx.x == 0) trace_stamp(p, it_no, 12, (uint32_t)__builtin_amdgcn_s_memtime());
             if constexpr (ARITH) {
                 bs8::large_ifft_h<1>(X);
                 bs8::large_mid(X);
                 bs8::large_fft_h<0>(X);
             }
+            if constexpr (TRACE) if (threadIdx.x == 0) trace_stamp(p, it_no, 13, (uint32_t)__builtin_amdgcn_s_memtime());
+            stamp(6);
             // publish the row set stored at the end of the previous set: ops issued
             // since its last stores = this set's direct loads (16, if pre)
             if (pend != kNone) {
@@ -1074,9 +1149,14 @@ __device__ __forceinline__ void bs_split_wave(const QueuePlan& p, uint32_t* lds,
                 qc.rc = q_load(&p.ctr[kQReady]);
                 qc.qh = q_load(&p.ctr[kQHead1]);
             }
+            stamp(7);
             // ---- L -> S', half 0 || large FFT of h1 ----
-            if constexpr (XCH) bs8::xch_write_h0(X, xw, xw + 65536u);
-            if constexpr (ARITH) bs8::large_fft_h<1>(X);
+            if constexpr (IL) {
+                bs8::ph_w0_lfft1(X, xw, xw + 65536u);
+            } else {
+                if constexpr (XCH) bs8::xch_write_h0(X, xw, xw + 65536u);
+                if constexpr (ARITH) bs8::large_fft_h<1>(X);
+            }
             if (t0) {
                 asm volatile("" : "+v"(sig), "+v"(rv));
                 if (sig_sq != kNone) {
@@ -1111,27 +1191,54 @@ __device__ __forceinline__ void bs_split_wave(const QueuePlan& p, uint32_t* lds,
             keep_half<0>(X);
             if constexpr (XCH) bs8::xch_read_h0(X, xr, xr + 65536u);
             asm volatile("s_barrier" ::: "memory");
+            stamp(8);
             // ---- L -> S', half 1 || small FFT, bytes and stores of h0 ----
             const SetAddr a = addr(crow, cset);
             const uint32_t k = p.rows.k;
             const uint32_t oo = (uint32_t)(crow ? p.rows.out_offset : p.cols.out_offset);
             const uint32_t es = (uint32_t)(crow ? p.rows.elem_stride : p.cols.elem_stride);
-            if constexpr (XCH) bs8::xch_write_h1(X, xw, xw + 65536u);
-            if constexpr (!LATE0) {
-                if constexpr (ARITH) bs8::small_fft_h0_all(X, A);
-                split_store_h<0, ARITH, true>(X, a, A, k, oo, es, crow != 0, MEM);
+            if constexpr (IL) {
+                bs8::small_fft_h0_all(X, A);
+                bs8::ph_w1_tr0(X, xw, xw + 65536u);  // + planes -> bytes of h0
+                split_store_h<0, false, true>(X, a, A, k, oo, es, crow != 0, MEM);
+                if constexpr (XLOAD) {
+                    if (pre) {
+                        issue_x0(nrow, nxt & kQ1, an);
+                    } else {
+                        bs8::sfor<8>([&](auto J) { bs8::sfor<8>([&](auto I) { X[decltype(J)::value][decltype(I)::value] = 0u; }); });
+                    }
+                }
+            } else {
+                if constexpr (XCH) bs8::xch_write_h1(X, xw, xw + 65536u);
+                if constexpr (!LATE0) {
+                    if constexpr (ARITH) bs8::small_fft_h0_all(X, A);
+                    split_store_h<0, ARITH, true>(X, a, A, k, oo, es, crow != 0, MEM);
+                }
             }
             RSM_LDS_SYNC;
             keep_half<1>(X);
             if constexpr (XCH) bs8::xch_read_h1(X, xr, xr + 65536u);
             asm volatile("s_barrier" ::: "memory");  // R free: the next set's h1 may land
-            if (pre) issue_dma(nrow, nxt & kQ1, an);
+            if constexpr (NODMA) {
+                if (pre) {
+                    issue_dma(nrow, nxt & kQ1, an);  // into Q
+                } else {
+                    // defined on every path, so the old Q is dead after the top of the set
+                    bs8::sfor<8>([&](auto J) { bs8::sfor<8>([&](auto I) { Q[decltype(J)::value][decltype(I)::value] = 0u; }); });
+                }
+            } else if constexpr (!XLOAD) {
+                if (pre) issue_dma(nrow, nxt & kQ1, an);
+            }
             if constexpr (LATE0) {
                 if constexpr (ARITH) bs8::small_fft_h0_all(X, A);
                 split_store_h<0, ARITH, true>(X, a, A, k, oo, es, crow != 0, MEM);
             }
+            stamp(9);
             if constexpr (ARITH) bs8::small_fft_h1_all(X, A);
             split_store_h<1, ARITH, true>(X, a, A, k, oo, es, crow != 0, MEM);
+            stamp(10);
+            if constexpr (TRACE) if (threadIdx.x == 0) trace_stamp(p, it_no, 11, (crow ? 1u : 0u) | ((cur & kQ1) ? 2u : 0u) | (pre ? 0u : 4u));
+            ++it_no;
             if (crow) pend = cset / p.rn;
             if (!more) break;
             if (!pre) {
@@ -1148,7 +1255,8 @@ __device__ __forceinline__ void bs_split_wave(const QueuePlan& p, uint32_t* lds,
                 if (nsq == kNone) break;  // stuck wait: skip the set, drain
                 q_item(p, nxt, nsq, nrow, nset);
                 an = addr(nrow, nset);
-                issue_dma(nrow, nxt & kQ1, an);
+                if constexpr (XLOAD) issue_x0(nrow, nxt & kQ1, an);
+                else issue_dma(nrow, nxt & kQ1, an);
                 issue_direct(nrow, nxt & kQ1, an);
                 __builtin_amdgcn_s_waitcnt(0x0F70);
                 asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -1409,7 +1517,15 @@ bool bs128_queue_applicable(const CodewordSet& rows, const CodewordSet& cols) {
 // layers and 9.52 at the top of the set; Q0 read non-temporal +3 %, Q1 read with the
 // default policy +3 % (the Infinity-Cache re-read of Q0 needs the default policy, the
 // last read of Q1 is best non-temporal).
-hipError_t launch_extend_gf8_bs128_queue(const QueuePlan& p, hipStream_t st) {
+#ifdef RSM_DIAG
+static std::atomic<uint32_t*> g_diag_trace{nullptr};
+void set_bs128_diag_trace(uint32_t* d) { g_diag_trace.store(d); }
+#endif
+hipError_t launch_extend_gf8_bs128_queue(const QueuePlan& p0, hipStream_t st) {
+    QueuePlan p = p0;
+#ifdef RSM_DIAG
+    p.trace = g_diag_trace.load();
+#endif
     const uint32_t total = p.nmain + p.nq1;
     if (total == 0) return hipSuccess;
     const uint32_t cap = p.rows.grid ? p.rows.grid : 256u;
@@ -1428,7 +1544,16 @@ hipError_t launch_extend_gf8_bs128_queue(const QueuePlan& p, hipStream_t st) {
         case 50004: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<4>), dim3(grid), dim3(512), 0, st, p); break;
         case 50768: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<32768>), dim3(grid), dim3(512), 0, st, p); break;
         case 50772: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<32772>), dim3(grid), dim3(512), 0, st, p); break;
-        case 65536: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<65536>), dim3(grid), dim3(512), 0, st, p); break;
+        case 51000: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<65536>), dim3(grid), dim3(512), 0, st, p); break;
+        case 51001: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<131072>), dim3(grid), dim3(512), 0, st, p); break;
+        case 51002: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<262144>), dim3(grid), dim3(512), 0, st, p); break;
+        case 51010: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<524288>), dim3(grid), dim3(512), 0, st, p); break;
+        case 51020: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<1048576>), dim3(grid), dim3(512), 0, st, p); break;
+        case 51030: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<1048576 | 524288>), dim3(grid), dim3(512), 0, st, p); break;
+        case 51014: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<524292>), dim3(grid), dim3(512), 0, st, p); break;
+        case 51012: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<524290>), dim3(grid), dim3(512), 0, st, p); break;
+        case 51004: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<262148>), dim3(grid), dim3(512), 0, st, p); break;
+        case 51006: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<262146>), dim3(grid), dim3(512), 0, st, p); break;
         // round-2 schedule (bs_queue_wave) for A/B
         case 18472: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<18472>), dim3(grid), dim3(512), 0, st, p); break;
         case 2: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<18474>), dim3(grid), dim3(512), 0, st, p); break;

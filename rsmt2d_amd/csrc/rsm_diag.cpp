@@ -52,6 +52,11 @@ int rsm_diag_set_bs_mode(int mode, int rev_col, int xcd) {
     return RSM_OK;
 }
 
+int rsm_diag_set_trace(void* d_trace) {
+    set_bs128_diag_trace(static_cast<uint32_t*>(d_trace));
+    return RSM_OK;
+}
+
 int rsm_diag_set_bs_row_mode(int mode) {
     set_bs128_diag_row_mode(mode);
     return RSM_OK;

@@ -103,6 +103,7 @@ struct QueuePlan {
     uint32_t nmain;  // 2 * count * rn: row sets + Q0-column sets
     uint32_t nq1;    // count * rn: Q1-column sets
     uint32_t margin; // a Q1-column set is claimed while more than this many ready ones are unclaimed
+    uint32_t* trace; // diagnostic build only (phase timeline), else nullptr
 };
 constexpr uint32_t kQueueFixedWords = 224;
 bool bs128_queue_applicable(const CodewordSet& rows, const CodewordSet& cols);
@@ -127,6 +128,10 @@ hipError_t launch_encode_gf8_bs128_dual(const DualPlan& p, hipStream_t st);
 // A-B kernel variant of the bit-sliced encode: 40 production, 0/8/24/56 A-B
 // variants, 2 = no arithmetic, 4 = no global memory (wrong output by design)
 void set_bs128_diag_mode(int mode, int rev_col, int xcd);
+// per-set phase timeline of the half-split queue kernel (device buffer of
+// grid * kTraceSets * kTraceWords words; nullptr: off)
+constexpr uint32_t kTraceSets = 256, kTraceWords = 14;
+void set_bs128_diag_trace(uint32_t* d);
 void set_bs128_diag_row_mode(int mode);
 #endif
 

@@ -366,7 +366,7 @@ int extend_squares_queue(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, u
 int extend_squares(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, uint32_t count, hipStream_t st,
                    int phases) {
     const uint64_t W = 2ull * k;
-    if (phases == 3 && count >= 2) {
+    if (phases == 3) {  // k = 128: one queue-driven launch, a single square included
         const int rc = extend_squares_queue(ctx, d_eds, k, S, count, st);
         if (rc != RSM_EUNSUPPORTED) return rc;
     }

@@ -127,7 +127,7 @@ def test_pass_grid_caps_do_not_change_results(lib, cap):
     assert lib.rsm_ctx_set_pass_grid(ctx, 2, 0, None) == R.RSM_EINVAL
 
 
-@pytest.mark.parametrize("S,count", [(512, 2), (512, 3), (512, 17), (64, 9), (1024, 4), (512, 70)])
+@pytest.mark.parametrize("S,count", [(512, 1), (512, 2), (512, 3), (512, 17), (64, 9), (1024, 4), (512, 70), (64, 1)])
 def test_single_launch_batch_matches_two_launch(lib, S, count):
     """Batches of k = 128 squares run as ONE queue-driven launch (row sets, Q0-column
     sets, Q1-column sets from a ready list: extend_gf8_bs128q_kernel); bit-exact with
