@@ -466,15 +466,17 @@ def bench_c3(local, L, R, repeats=5, k=128, S=512):
 
 def bench_single_square(local, L, R, k=128, S=512, reps=200):
     """What a cgo ComputeExtendedDataSquare of ONE square gets (extendeddatasquare.go:
-    50-77) from device memory: rsm_extend_squares_dev with count = 1 (the single-launch
-    queue kernel over the square's 96 sets), launches back to back on one stream, so
-    each one's device time is its latency.  Oracle-checked."""
+    50-77) from device memory: rsm_extend_squares_dev with count = 1 -- the latency form
+    (encode_gf8_split_kernel: rows + Q0 columns in one launch over every CU, Q1 columns
+    in a second) -- launches back to back on one stream, so each one's device time is its
+    latency.  Oracle-checked.  Beside it the queue-driven launch for the same square and
+    a count sweep of both forms (where rsm_ctx_set_split_max's default comes from)."""
     import ctypes
     import numpy as np
     import oracle
     ctx = R.device_context(local)
     W = 2 * k
-    buf = R.DeviceBuffer(W * W * S, local)
+    buf = R.DeviceBuffer(W * W * S * 8, local)
     buf.fill_random(0x55)
     R._check(L.rsm_extend_squares_dev(ctx, buf.ptr, k, S, 1, None))
     R._check(L.rsm_sync(ctx))
@@ -484,13 +486,29 @@ def bench_single_square(local, L, R, k=128, S=512, reps=200):
     e0, e1 = ctypes.c_void_p(), ctypes.c_void_p()
     R._check(L.rsm_event_create(ctx, ctypes.byref(e0)))
     R._check(L.rsm_event_create(ctx, ctypes.byref(e1)))
-    R._check(L.rsm_event_record(ctx, e0, None))
-    for _ in range(reps):
-        R._check(L.rsm_extend_squares_dev(ctx, buf.ptr, k, S, 1, None))
-    R._check(L.rsm_event_record(ctx, e1, None))
-    ms = ctypes.c_float()
-    R._check(L.rsm_event_elapsed_ms(e0, e1, ctypes.byref(ms)))
-    t_dev = ms.value / reps / 1e3
+
+    def dev_us(count, n):
+        R._check(L.rsm_extend_squares_dev(ctx, buf.ptr, k, S, count, None))  # warm
+        R._check(L.rsm_event_record(ctx, e0, None))
+        for _ in range(n):
+            R._check(L.rsm_extend_squares_dev(ctx, buf.ptr, k, S, count, None))
+        R._check(L.rsm_event_record(ctx, e1, None))
+        ms = ctypes.c_float()
+        R._check(L.rsm_event_elapsed_ms(e0, e1, ctypes.byref(ms)))
+        return ms.value / n * 1e3
+
+    t_dev = dev_us(1, reps) / 1e6
+    prev = ctypes.c_int(0)
+    R._check(L.rsm_ctx_set_split_max(ctx, 0, ctypes.byref(prev)))
+    t_queue = dev_us(1, reps)
+    sweep = {}
+    for c in (2, 4, 8):
+        R._check(L.rsm_ctx_set_split_max(ctx, 0, None))
+        q = dev_us(c, 50)
+        R._check(L.rsm_ctx_set_split_max(ctx, 8, None))
+        sp = dev_us(c, 50)
+        sweep[str(c)] = {"split_us": round(sp, 2), "queue_us": round(q, 2)}
+    R._check(L.rsm_ctx_set_split_max(ctx, prev.value, None))
     lat = []
     for _ in range(50):  # host-observed: launch + completion of one square
         t0 = time.perf_counter()
@@ -503,8 +521,11 @@ def bench_single_square(local, L, R, k=128, S=512, reps=200):
     return {"workload": f"one k={k} S={S} square, device-resident (count = 1)",
             "single_square_us": round(t_dev * 1e6, 2), "host_observed_us_p50": round(pct(lat, 0.5) * 1e6, 1),
             "frac": round(4 * k * k * S / t_dev / 1e9 / HBM_PEAK_GBS, 4),
+            "kernel": "encode_gf8_split_kernel<4> x 2 launches (latency form)",
+            "queue_form_us": round(t_queue, 2), "count_sweep_us": sweep,
             "note": "device time per launch of back-to-back launches on one stream; host_observed = "
-                    "rsm_extend_squares_dev + rsm_sync round trip"}
+                    "rsm_extend_squares_dev + rsm_sync round trip; queue_form = the single queue-driven "
+                    "launch (rsm_ctx_set_split_max 0)"}
 
 
 def bench_c4(local, L, R, steps, B=2):

@@ -26,6 +26,9 @@ int rsm_diag_set_bs_row_mode(int mode);
 /* Phase timeline of the half-split queue kernel's trace modes (51010/51012/51014):
  * d_trace = device buffer of 256 workgroups x 256 sets x 12 words (NULL: off). */
 int rsm_diag_set_trace(void* d_trace);
+/* Phase stamps of the M = 128 split decoder: 8 words (s_memrealtime, 100 MHz) per
+ * workgroup of every following GF(2^8) decode launch; NULL = off. */
+int rsm_diag_set_dec_trace(void* d_trace);
 /* Both passes of `count` in-place k = 128 squares in ONE persistent launch
  * (extend_gf8_bs128q_kernel: row and Q0-column sets from one queue, Q1-column sets
  * from a ready list; `delay` squares of row sets lead the Q0-column sets).

@@ -116,6 +116,7 @@ SIGNATURES = {
     "rsm_ctx_destroy": (None, [_VP]),
     "rsm_ctx_device": (_I32, [_VP]),
     "rsm_ctx_set_pass_grid": (_I32, [_VP, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
+    "rsm_ctx_set_split_max": (_I32, [_VP, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     "rsm_last_error": (ctypes.c_char_p, []),
     "rsm_version": (ctypes.c_char_p, []),
     "rsm_device_count": (_I32, []),
@@ -188,6 +189,7 @@ SIGNATURES = {
 DIAG_SIGNATURES = {
     "rsm_diag_set_bs_mode": (_I32, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "rsm_diag_set_trace": (_I32, [_VP]),
+    "rsm_diag_set_dec_trace": (_I32, [_VP]),
     "rsm_diag_set_bs_row_mode": (_I32, [ctypes.c_int]),
     "rsm_diag_extend_fused": (_I32, [_VP, _VP, _U32, _U32, _U32, _U32, _VP]),
     "rsm_diag_queue_check": (_I32, [_VP, _VP]),

@@ -83,33 +83,38 @@ static void emit_half(const char* name, bool ifft, int G) {
 
 // Half-split exchange (kernels_gf8_bs.hip, bs_split_wave): half G is a transpose,
 // wave u's register 8G + v -> wave v's register 8G + u, through LDS entries
-//   (plane p, destination v, source u) at ((p * 8 + v) * 4 + u / 2) * 512 + lane * 8 + (u % 2) * 4
-// (a reader's two sources u, u + 1 share one ds_read_b64; the writers' lanes are 8 B
-// apart: a 2-way bank overlap that costs ds_write_b32 nothing).
+//   (plane pair q = p / 2, destination v, source u) at ((q * 8 + v) * 8 + u) * 512 + lane * 8 + (p % 2) * 4
+// (a reader's ds_read_b64 returns planes 2q, 2q + 1 of ONE source symbol, so the pair
+// it fills is two registers of the same symbol -- the round-2 mapping paired one plane
+// of two symbols, and the allocator paid ~100 v_mov and 12 VGPRs to re-pair them for the
+// byte stores; the writers' lanes are 8 B apart: a 2-way bank overlap that costs
+// ds_write_b32 nothing).
 // xch_write_hG: 64 ds_write_b32, no wait (the caller waits and keeps X live until then);
-//   %0..%63 = X[8G + v][p] (operand 8v + p), %64 = lds + lane*8 + (u&1)*4 + (u>>1)*512, %65 = %64 + 65536.
-// xch_read_hG: 32 ds_read_b64 then lgkmcnt(0); outputs %0..%31 = T[s/2][p] (the pair
-//   X[8G + s][p], X[8G + s + 1][p]), %32 = lds + lane*8 + u*2048, %33 = %32 + 65536.
+//   %0..%63 = X[8G + v][p] (operand 8v + p), %64 = lds + lane*8 + u*512, %65 = %64 + 65536.
+// xch_read_hG: 32 ds_read_b64 then lgkmcnt(0); outputs %0..%31 = T[u][q] (the pair
+//   X[8G + u][2q], X[8G + u][2q + 1]), %32 = lds + lane*8 + v*4096, %33 = %32 + 65536.
+static int wr_off(int p, int v) { return (((p / 2) % 2) * 8 + v) * 4096 + (p % 2) * 4; }
+static bool wr_hi(int p) { return p >= 4; }
 static void emit_xch(int G) {
     printf("RSM_BS8_DEV void xch_write_h%d(uint32_t (&X)[16][8], uint32_t va, uint32_t vb) {\n    asm volatile(\n", G);
     for (int p = 0; p < 8; ++p)
         for (int v = 0; v < 8; ++v)
-            printf("        \"ds_write_b32 %%%d, %%%d offset:%d\\n\\t\"\n", p < 4 ? 64 : 65, 8 * v + p, ((p % 4) * 8 + v) * 2048);
+            printf("        \"ds_write_b32 %%%d, %%%d offset:%d\\n\\t\"\n", wr_hi(p) ? 65 : 64, 8 * v + p, wr_off(p, v));
     printf("        :");
     for (int v = 0; v < 8; ++v)
         for (int p = 0; p < 8; ++p) printf(" \"+v\"(X[%d][%d])%s", 8 * G + v, p, (v == 7 && p == 7) ? "" : ",");
     printf("\n        : \"v\"(va), \"v\"(vb) : \"memory\");\n}\n");
     printf("RSM_BS8_DEV void xch_read_h%d(uint32_t (&X)[16][8], uint32_t ra, uint32_t rb) {\n"
-           "    uint64_t T[4][8];\n    asm volatile(\n", G);
-    for (int p = 0; p < 8; ++p)
-        for (int s2 = 0; s2 < 4; ++s2)
-            printf("        \"ds_read_b64 %%%d, %%%d offset:%d\\n\\t\"\n", 8 * s2 + p, p < 4 ? 32 : 33, (p % 4) * 16384 + s2 * 512);
+           "    uint64_t T[8][4];\n    asm volatile(\n", G);
+    for (int q = 0; q < 4; ++q)
+        for (int u = 0; u < 8; ++u)
+            printf("        \"ds_read_b64 %%%d, %%%d offset:%d\\n\\t\"\n", 4 * u + q, q < 2 ? 32 : 33, (q % 2) * 32768 + u * 512);
     printf("        \"s_waitcnt lgkmcnt(0)\"\n        :");
-    for (int s2 = 0; s2 < 4; ++s2)
-        for (int p = 0; p < 8; ++p) printf(" \"=&v\"(T[%d][%d])%s", s2, p, (s2 == 3 && p == 7) ? "" : ",");
+    for (int u = 0; u < 8; ++u)
+        for (int q = 0; q < 4; ++q) printf(" \"=&v\"(T[%d][%d])%s", u, q, (u == 7 && q == 3) ? "" : ",");
     printf("\n        : \"v\"(ra), \"v\"(rb) : \"memory\");\n");
-    printf("    for (int s2 = 0; s2 < 4; ++s2)\n        for (int p = 0; p < 8; ++p) {\n"
-           "            X[%d + 2 * s2][p] = (uint32_t)T[s2][p];\n            X[%d + 2 * s2 + 1][p] = (uint32_t)(T[s2][p] >> 32);\n"
+    printf("    for (int u = 0; u < 8; ++u)\n        for (int q = 0; q < 4; ++q) {\n"
+           "            X[%d + u][2 * q] = (uint32_t)T[u][q];\n            X[%d + u][2 * q + 1] = (uint32_t)(T[u][q] >> 32);\n"
            "        }\n}\n", 8 * G, 8 * G);
 }
 
@@ -127,8 +132,8 @@ static void emit_phase(const char* name, int W, int kind) {
     for (int p = 0; p < 8; ++p)
         for (int v = 0; v < 8; ++v) {
             char b[96];
-            snprintf(b, sizeof b, "ds_write_b32 %%%d, %%%d offset:%d", p < 4 ? 138 : 139, 8 * (8 * W + v) + p,
-                     ((p % 4) * 8 + v) * 2048);
+            snprintf(b, sizeof b, "ds_write_b32 %%%d, %%%d offset:%d", wr_hi(p) ? 139 : 138, 8 * (8 * W + v) + p,
+                     wr_off(p, v));
             wr.push_back(b);
         }
     auto reg = [](int j, int i) { return 8 * j + i; };
@@ -192,6 +197,7 @@ static void emit_phase(const char* name, int W, int kind) {
            "        : \"s\"(0x0F0F0F0Fu), \"s\"(0xF0F0F0F0u), \"s\"(0x33333333u), \"s\"(0xCCCCCCCCu), "
            "\"s\"(0x55555555u), \"s\"(0xAAAAAAAAu), \"v\"(va), \"v\"(vb) : \"memory\");\n}\n");
 }
+
 
 int main() {
     printf("// GENERATED by gen/gen_bs8_small.cpp -- do not edit.\n");

@@ -21,6 +21,7 @@
 // butterflies (groups are disjoint), and truncated groups are computed on
 // zero-padding (exact: see DESIGN.md "Truncation").
 #include <hip/hip_runtime.h>
+#include <atomic>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
@@ -491,10 +492,25 @@ __device__ __forceinline__ uint64_t pres_bits(const uint64_t (&pres)[4], uint32_
 // absent point, so its bytes -- whatever the buffer holds -- enter as 0), [1]
 // reveal by 255 - err[e].  Written once by wave 0; every wave reads them with
 // uniform LDS broadcasts instead of a dependent scalar table load per point.
+// diagnostic phase stamp (RSM_DIAG builds, ds.trace set): thread 0, 100 MHz clock
+__device__ __forceinline__ void dec_stamp(const DecodeSet& ds, int i) {
+#ifdef RSM_DIAG
+    if (ds.trace && threadIdx.x == 0) {
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(ds.trace, (short)0, 0x7FFFFFFF, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)__builtin_amdgcn_s_memrealtime(), r,
+                                              (blockIdx.x * kDecTraceWords + i) * 4u, 0, 0);
+    }
+#else
+    (void)ds;
+    (void)i;
+#endif
+}
+
 template <int NW, bool ZC>
 __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t task, uint32_t (&xch)[256][64],
                                                   PermTab (&ptab)[2][256]) {
     constexpr int PW = 256 / NW, HALF = NW / 2;
+    if constexpr (!ZC) dec_stamp(ds, 0);
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t chunks = ds.chunks;
@@ -549,6 +565,7 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
     }
     auto present = [&](uint32_t e) -> bool { return (pres[e >> 6] >> (e & 63u)) & 1u; };
     const uint64_t have = pres_bits(pres, w < HALF ? k + ib : ib) & valid;
+    if constexpr (!ZC) dec_stamp(ds, 1);
     if constexpr (ZC) load_points(have);
 
     // error locator (log domain), as decode_gf8_kernel: entries 4 lane .. 4 lane + 3;
@@ -585,6 +602,7 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
         });
     }
     __syncthreads();
+    if constexpr (!ZC) dec_stamp(ds, 2);
 
     // 1. S layout: scale every point by the error locator (absent -> 0)
     static_for<PW>([&](auto J) {
@@ -593,6 +611,7 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
     });
     // 2. IFFT layers 1..PW/2 (per-wave twiddles)
     split_low<NW, PW, false>(v, w);
+    if constexpr (!ZC) dec_stamp(ds, 3);
     // 3. S -> L
     static_for<PW>([&](auto J) { xch[PW * w + decltype(J)::value][lane] = v[decltype(J)::value]; });
     __syncthreads();
@@ -617,14 +636,17 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
                     v[decltype(H)::value] ^= xch[NW * decltype(H)::value + w + bit][lane];
                 });
     });
+    if constexpr (!ZC) dec_stamp(ds, 4);
     // 5. FFT layers 128..PW; L -> S
     split_high<NW, PW, true>(v);
     __syncthreads();
     static_for<PW>([&](auto H) { xch[NW * decltype(H)::value + w][lane] = v[decltype(H)::value]; });
     __syncthreads();
     static_for<PW>([&](auto J) { v[decltype(J)::value] = xch[PW * w + decltype(J)::value][lane]; });
+    if constexpr (!ZC) dec_stamp(ds, 5);
     // 6. FFT layers PW/2..1; reveal the missing points of this wave
     split_low<NW, PW, true>(v, w);
+    if constexpr (!ZC) dec_stamp(ds, 6);
     const uint64_t reveal = valid & ~have;
     const __amdgpu_buffer_rsrc_t rm = make_rsrc(mirror ? ds.mirror : ds.base);
     uint32_t sbase = pbase, sstep = pstep;
@@ -637,6 +659,7 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
         __builtin_amdgcn_raw_buffer_store_b32(x, rs, off, so, 0);
         if (mirror) __builtin_amdgcn_raw_buffer_store_b32(x, rm, off, so, 0);
     });
+    if constexpr (!ZC) dec_stamp(ds, 7);
 }
 
 constexpr int kSplitWaves = 16;
@@ -659,6 +682,119 @@ __global__ __launch_bounds__(64 * NW, NW / 2) void decode_gf8_split_zc_kernel(De
         decode_split_task<NW, true>(ds, __builtin_amdgcn_readfirstlane(task), xch, ptab);
         __syncthreads();  // LDS (xch, ptab) is reused by the next task
     }
+}
+
+
+// ---------------------------------------------------------------------------
+// Split encoder for M = 128 (65 <= k <= 128): the LATENCY form, for one or a few
+// squares (a single square has only 96 sets of the bit-sliced kernel's 2 KiB width,
+// and its row -> column dependency puts two ~16 us sets on the critical path).  One
+// NW-wave workgroup per (codeword, 256-byte chunk), the codewords of up to two
+// CodewordSets in one grid (rows of Q0 -> Q1 together with columns of Q0 -> Q2), so
+// a square's first phase fills every CU; PW = 128 / NW points per wave:
+//   S layout: wave w holds points e = PW w + j (j < PW): IFFT layers d < PW (offset
+//             m - 1 = 127) and FFT layers PW/2..1 (offset -1) with per-wave twiddles
+//             (one compile-time variant per wave, chosen by a wave-uniform branch);
+//   L layout: wave w holds e = NW h + w (h < PW): IFFT layers PW..64 and FFT layers
+//             64..PW, twiddles independent of w (2d >= NW).
+// Same butterflies as encode_gf8_kernel<128> (klauspost leopard8
+// ifftDITEncoder8 / fftDIT8), so the same parity; LDS [128 points][64 lanes] dwords.
+// ---------------------------------------------------------------------------
+template <int NW, int PW, bool FFT>
+__device__ __forceinline__ void enc_split_high(uint32_t (&v)[PW]) {
+    static_for<7>([&](auto LG) {
+        constexpr int d = FFT ? (64 >> decltype(LG)::value) : (1 << decltype(LG)::value);
+        if constexpr (d >= PW) {
+            constexpr int sd = d / NW;
+            static_for<PW>([&](auto H) {
+                constexpr int h = decltype(H)::value;
+                if constexpr (((h / sd) & 1) == 0) {
+                    constexpr int b = 2 * d * (h / (2 * sd));
+                    constexpr unsigned L = kGf8.skew[(FFT ? -1 : 127) + b + d];
+                    if constexpr (FFT) fft2<L>(v[h], v[h + sd]);
+                    else ifft2<L>(v[h], v[h + sd]);
+                }
+            });
+        }
+    });
+}
+template <int NW, int PW, bool FFT>
+__device__ __forceinline__ void enc_split_low(uint32_t (&v)[PW], uint32_t w) {
+    static_for<NW>([&](auto Wc) {
+        constexpr int W = decltype(Wc)::value;
+        if (w == (uint32_t)W) {
+            if constexpr (FFT) fft_layers<PW, PW * W - 1>(v);
+            else ifft_layers<PW, 127 + PW * W>(v);
+        }
+    });
+}
+
+struct SplitEncPlan {
+    CodewordSet cs[2];
+    uint32_t n0;  // tasks of cs[0]; the rest belong to cs[1]
+};
+
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void encode_gf8_split_kernel(SplitEncPlan p) {
+    constexpr int PW = 128 / NW;
+    static_assert(PW * NW == 128 && 2 * PW >= NW, "split encoder shape");
+    __shared__ uint32_t xch[128][64];
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t task = blockIdx.x;
+    const bool second = task >= p.n0;
+    const CodewordSet& cs = second ? p.cs[1] : p.cs[0];
+    if (second) task -= p.n0;
+    const uint32_t chunks = cs.chunks;
+    const uint32_t q = task / chunks;
+    const uint32_t chunk = task - q * chunks;
+    const uint32_t off0 = chunk * 256u + lane * 4u;
+    const uint32_t off = off0 < cs.S ? off0 : kOob;
+    const uint64_t rel = cw_rel(cs, q);
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(cs.base + rel);
+    const __amdgpu_buffer_rsrc_t ro = make_rsrc(cs.out_base + rel);
+    const uint32_t k = cs.k, es = (uint32_t)cs.elem_stride, oo = (uint32_t)cs.out_offset;
+    uint32_t v[PW];
+    static_for<PW>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        const uint32_t e = PW * w + j;
+        v[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, off, e < k ? e * es : kOob, 0);
+    });
+    enc_split_low<NW, PW, false>(v, w);
+    static_for<PW>([&](auto J) { xch[PW * w + decltype(J)::value][lane] = v[decltype(J)::value]; });
+    __syncthreads();
+    static_for<PW>([&](auto H) { v[decltype(H)::value] = xch[NW * decltype(H)::value + w][lane]; });
+    enc_split_high<NW, PW, false>(v);
+    enc_split_high<NW, PW, true>(v);
+    __syncthreads();
+    static_for<PW>([&](auto H) { xch[NW * decltype(H)::value + w][lane] = v[decltype(H)::value]; });
+    __syncthreads();
+    static_for<PW>([&](auto J) { v[decltype(J)::value] = xch[PW * w + decltype(J)::value][lane]; });
+    enc_split_low<NW, PW, true>(v, w);
+    static_for<PW>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        const uint32_t e = PW * w + j;
+        __builtin_amdgcn_raw_buffer_store_b32(v[j], ro, off, e < k ? oo + e * es : kOob, 0);
+    });
+}
+constexpr int kEncSplitWaves = 4;
+
+hipError_t launch_encode_gf8_split(const CodewordSet& a, const CodewordSet* b, hipStream_t st) {
+    if (ceil_pow2(a.k) != 128 || (b && ceil_pow2(b->k) != 128)) return hipErrorInvalidValue;
+    SplitEncPlan p{};
+    p.cs[0] = a;
+    p.cs[0].chunks = (a.S + 255) / 256;
+    p.n0 = p.cs[0].count * p.cs[0].chunks;
+    uint64_t tasks = p.n0;
+    if (b) {
+        p.cs[1] = *b;
+        p.cs[1].chunks = (b->S + 255) / 256;
+        tasks += (uint64_t)p.cs[1].count * p.cs[1].chunks;
+    }
+    if (tasks == 0) return hipSuccess;
+    hipLaunchKernelGGL(encode_gf8_split_kernel<kEncSplitWaves>, dim3((uint32_t)tasks), dim3(64 * kEncSplitWaves), 0,
+                       st, p);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
@@ -711,7 +847,20 @@ static hipError_t launch_dec(const DecodeSet& ds, hipStream_t st) {
     return hipGetLastError();
 }
 
-hipError_t launch_decode_gf8(const DecodeSet& ds, hipStream_t st) {
+#ifdef RSM_DIAG
+static std::atomic<uint32_t*> g_dec_trace{nullptr};
+void set_dec_diag_trace(uint32_t* d) { g_dec_trace.store(d); }
+#else
+void set_dec_diag_trace(uint32_t*) {}
+#endif
+
+hipError_t launch_decode_gf8(const DecodeSet& ds0, hipStream_t st) {
+    DecodeSet ds = ds0;
+#ifdef RSM_DIAG
+    ds.trace = g_dec_trace.load();
+#else
+    ds.trace = nullptr;
+#endif
     if (ceil_pow2(ds.k) == 128) {  // split form: kSplitWaves waves per (codeword, 256 B chunk)
         const uint64_t tasks = (uint64_t)ds.count * ds.chunks;
         if (tasks == 0) return hipSuccess;

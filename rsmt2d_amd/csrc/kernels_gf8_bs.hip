@@ -822,19 +822,23 @@ __device__ __forceinline__ void bs_queue_wave(const QueuePlan& p, uint32_t* lds,
 // into two halves that are independent in every layer but the merged middle pair
 // (bs8.hpp, "Half-split schedule").  Each LDS exchange moves one half while the
 // VALU works on the other, so the exchange (a quarter of the set's time when the
-// waves wait for it: profiles/r03_qab.jsonl) overlaps arithmetic:
-//   top   X[h0] <- P (direct loads of the previous set); direct loads of the NEXT
-//         set's h0 -> P; transposes + small IFFT h0; X[h1] <- R (LDS-DMA landed)
+// waves wait for it: profiles/r03_qab.jsonl) overlaps arithmetic.  Production form
+// (MODE 0, direct loads only -- "XLOAD"; the LDS-DMA form is diagnostic bit 1048576):
+//   top   X[h1] <- P (direct loads of this set's h1, issued at the previous top);
+//         direct loads of the NEXT set's h1 -> P; transposes + small IFFT h0
+//         (X[h0] was loaded right after the previous set's h0 stores)
 //   write h0 -> R            || transposes + small IFFT h1
 //   read  h0 (layout L)      ;  write h1 -> R || large IFFT h0
 //   read  h1                 ;  large IFFT h1, middle pair, large FFT h0
 //   write h0 -> R            || large FFT h1
-//   read  h0 (layout S')     ;  write h1 -> R || small FFT h0, planes -> bytes, stores h0
-//   read  h1                 ;  LDS-DMA of the NEXT set's h1 -> R || small FFT h1,
-//                               planes -> bytes, stores h1
-// LDS: R = [0, 128 KiB) (one half's exchange, or the landing zone of the next set's
-// h1); the queue slot words at 128 KiB.  Loads of symbol e of the set: h0 registers
-// j < 8 hold e = j + 8A, h1 registers e = (j - 8) + 8A + 64.
+//   read  h0 (layout S')     ;  write h1 -> R || small FFT h0, planes -> bytes, stores h0,
+//                               then direct loads of the NEXT set's h0 into X[h0]
+//   read  h1                 ;  small FFT h1, planes -> bytes, stores h1
+// LDS: R = [0, 128 KiB) (one half's exchange; in the DMA form also the landing zone
+// of the next set's h1); the queue slot words at 128 KiB.  Loads of symbol e of the
+// set: h0 registers j < 8 hold e = j + 8A, h1 registers e = (j - 8) + 8A + 64.
+// Same-box A/B (profiles/r03_qab.jsonl): direct-load form 8.47 us per square against
+// 8.67-8.72 for the LDS-DMA form.
 constexpr uint32_t kRBytes = 128u * 1024u;
 constexpr uint32_t kSlotW = kRBytes / 4;
 
@@ -926,11 +930,22 @@ __device__ __forceinline__ void bs_split_wave(const QueuePlan& p, uint32_t* lds,
     // 262144: no LDS-DMA -- h1 of the next set by direct loads into Q right after this
     // set's h0 stores (the LDS region R then holds only exchanges)
     constexpr bool NODMA = (MODE & 262144) != 0 && !LATE0;
-    // 1048576: no LDS-DMA -- P holds h1 of the next set (loaded at the top), h0 of the
-    // next set is loaded into X[0..7] right after this set's h0 stores
-    constexpr bool XLOAD = (MODE & 1048576) != 0 && !NODMA && !LATE0;
+    // production: no LDS-DMA -- P holds h1 of the next set (loaded at the top), h0 of
+    // the next set is loaded into X[0..7] right after this set's h0 stores;
+    // 1048576: the LDS-DMA form (h1 of the next set lands in R, A/B)
+    constexpr bool XLOAD = (MODE & 1048576) == 0 && !NODMA && !LATE0;
     // 524288: phase timeline into p.trace (diagnostic build)
     constexpr bool TRACE = (MODE & 524288) != 0;
+    // 4194304: an explicit agent-scope release (buffer_wbl2 sc1 + vmcnt(0)) by the
+    // signalling lane before each row set's counter add -- measures what the release
+    // would cost on top of the write-through (sc1) Q1 stores the hand-off relies on
+    constexpr bool REL = (MODE & 4194304) != 0;
+    auto release = [&]() {
+        if constexpr (REL) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    };
     uint32_t it_no = 0;
     auto stamp = [&](int w) {
         if constexpr (TRACE)
@@ -940,7 +955,9 @@ __device__ __forceinline__ void bs_split_wave(const QueuePlan& p, uint32_t* lds,
     const uint32_t lane = threadIdx.x & 63u;
     const bool t0 = threadIdx.x == 0;
     const uint32_t dread = lds_base + A * 16384u + lane * 16u;
-    const uint32_t xw = lds_base + lane * 8u + (A & 1u) * 4u + (A >> 1) * 512u, xr = lds_base + lane * 8u + A * 2048u;
+    // exchange entries (gen_bs8_small.cpp emit_xch): writer wave A at lane * 8 + A * 512,
+    // reader wave A at lane * 8 + A * 4096
+    const uint32_t xw = lds_base + lane * 8u + A * 512u, xr = lds_base + lane * 8u + A * 4096u;
     uint32_t* slot = lds + kSlotW;
     uint32_t X[16][8];
     uint32_t P[8][8];
@@ -1120,6 +1137,7 @@ __device__ __forceinline__ void bs_split_wave(const QueuePlan& p, uint32_t* lds,
                 if (pre) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
                 else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
                 if (t0) {
+                    release();
                     sig = q_add(&p.ctr[kQRows + pend]);
                     sig_sq = pend;
                 }
@@ -1246,7 +1264,10 @@ __device__ __forceinline__ void bs_split_wave(const QueuePlan& p, uint32_t* lds,
                 // own row set first, wait, then load the next set synchronously
                 asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
                 if (t0) {
-                    if (pend != kNone) q_signal(p, pend);
+                    if (pend != kNone) {
+                        release();
+                        q_signal(p, pend);
+                    }
                     slot[3] = q_wait(p, nxt);
                 }
                 pend = kNone;
@@ -1271,7 +1292,10 @@ __device__ __forceinline__ void bs_split_wave(const QueuePlan& p, uint32_t* lds,
     // (all its threads: 2 * count words)
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     if (t0) {
-        if (pend != kNone) q_signal(p, pend);
+        if (pend != kNone) {
+            release();
+            q_signal(p, pend);
+        }
         __builtin_amdgcn_s_waitcnt(0x0F70);
         slot[0] = q_add(&p.ctr[kQExit]) == gridDim.x - 1u ? 1u : 0u;
     }
@@ -1547,12 +1571,14 @@ hipError_t launch_extend_gf8_bs128_queue(const QueuePlan& p0, hipStream_t st) {
         case 51000: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<65536>), dim3(grid), dim3(512), 0, st, p); break;
         case 51001: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<131072>), dim3(grid), dim3(512), 0, st, p); break;
         case 51002: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<262144>), dim3(grid), dim3(512), 0, st, p); break;
-        case 51010: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<524288>), dim3(grid), dim3(512), 0, st, p); break;
-        case 51020: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<1048576>), dim3(grid), dim3(512), 0, st, p); break;
-        case 51030: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<1048576 | 524288>), dim3(grid), dim3(512), 0, st, p); break;
+        case 51010: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<1048576 | 524288>), dim3(grid), dim3(512), 0, st, p); break;
+        case 51020: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<0>), dim3(grid), dim3(512), 0, st, p); break;
+        case 51021: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<1048576>), dim3(grid), dim3(512), 0, st, p); break;
+        case 51030: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<524288>), dim3(grid), dim3(512), 0, st, p); break;
         case 51014: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<524292>), dim3(grid), dim3(512), 0, st, p); break;
         case 51012: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<524290>), dim3(grid), dim3(512), 0, st, p); break;
         case 51004: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<262148>), dim3(grid), dim3(512), 0, st, p); break;
+        case 52040: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<4194304>), dim3(grid), dim3(512), 0, st, p); break;
         case 51006: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<262146>), dim3(grid), dim3(512), 0, st, p); break;
         // round-2 schedule (bs_queue_wave) for A/B
         case 18472: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<18472>), dim3(grid), dim3(512), 0, st, p); break;

@@ -57,6 +57,11 @@ int rsm_diag_set_trace(void* d_trace) {
     return RSM_OK;
 }
 
+int rsm_diag_set_dec_trace(void* d_trace) {
+    set_dec_diag_trace(static_cast<uint32_t*>(d_trace));
+    return RSM_OK;
+}
+
 int rsm_diag_set_bs_row_mode(int mode) {
     set_bs128_diag_row_mode(mode);
     return RSM_OK;

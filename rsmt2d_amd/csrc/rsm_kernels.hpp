@@ -58,13 +58,23 @@ struct DecodeSet {
     // drain over PCIe while its next loads arrive, instead of every workgroup
     // loading, then computing, then storing in lockstep.
     uint32_t grid;
+    // diagnostic builds only: per-workgroup phase stamps of the M = 128 split decoder
+    // (kDecTraceWords s_memrealtime values per workgroup; nullptr = off)
+    uint32_t* trace;
 };
+constexpr int kDecTraceWords = 8;
+void set_dec_diag_trace(uint32_t* d);
 
 hipError_t launch_encode_gf8(const CodewordSet& cs, hipStream_t st);
 // bit-sliced M = 128 encode (kernels_gf8_bs.hip); launch_encode_gf8 picks it when applicable
 bool bs128_applicable(const CodewordSet& cs);
 hipError_t launch_encode_gf8_bs128(const CodewordSet& cs, hipStream_t st);
 hipError_t launch_decode_gf8(const DecodeSet& ds, hipStream_t st);
+// Latency form of the M = 128 encode (65 <= k <= 128) for one or a few squares
+// (kernels_gf8.hip encode_gf8_split_kernel): NW waves per (codeword, 256-B chunk) on
+// byte tables, every CU busy.  Launches the codewords of `a` and, if b != nullptr,
+// those of `b` in the same grid.
+hipError_t launch_encode_gf8_split(const CodewordSet& a, const CodewordSet* b, hipStream_t st);
 struct Gf16Dev;
 hipError_t launch_encode_gf16(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st);
 hipError_t launch_decode_gf16(const DecodeSet& ds, const Gf16Dev& g, hipStream_t st);

@@ -360,13 +360,37 @@ int extend_squares_queue(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, u
     return RSM_OK;
 }
 
+// Latency form for one or a few squares with 65 <= k <= 128 (what a cgo
+// ComputeExtendedDataSquare call extends): launch 1 = rows of Q0 -> Q1 together with
+// columns of Q0 -> Q2, launch 2 = columns of Q1 -> Q3, both on the split byte-table
+// encoder (NW waves per codeword chunk), so each phase spreads over every CU instead
+// of the queue kernel's 64 + 32 sets of ~16 us each.
+int extend_squares_split(uint8_t* d_eds, uint32_t k, uint32_t S, uint32_t count, hipStream_t st) {
+    if (field_bits(k) != 8 || ceil_pow2(k) != 128 || count == 0) return RSM_EUNSUPPORTED;
+    const CodewordSet rows = rows_set(d_eds, k, S, count);
+    CodewordSet c0 = cols_set(d_eds, k, S, count);  // columns 0 .. k-1 (Q0 -> Q2)
+    c0.per_square = k;
+    c0.count = k * count;
+    CodewordSet c1 = c0;  // columns k .. 2k-1 (Q1 -> Q3)
+    c1.base = c1.out_base = d_eds + (uint64_t)k * S;
+    hipError_t e;
+    if ((e = launch_encode_gf8_split(rows, &c0, st)) != hipSuccess) return hip_fail(e, "split extension (rows + Q0 columns)");
+    if ((e = launch_encode_gf8_split(c1, nullptr, st)) != hipSuccess) return hip_fail(e, "split extension (Q1 columns)");
+    return RSM_OK;
+}
+
 // Two-phase in-place extension; batches of k = 128 squares run both phases as one
 // queue-driven launch (extend_squares_queue), which re-reads Q0 and Q1 from the
-// Infinity Cache instead of HBM.
+// Infinity Cache instead of HBM; up to ctx->split_max squares take the latency form
+// (rsm_ctx_set_split_max; default 4, profiles/r03_single.jsonl).
 int extend_squares(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, uint32_t count, hipStream_t st,
                    int phases) {
     const uint64_t W = 2ull * k;
-    if (phases == 3) {  // k = 128: one queue-driven launch, a single square included
+    if (phases == 3 && count <= ctx->split_max.load(std::memory_order_relaxed)) {
+        const int rc = extend_squares_split(d_eds, k, S, count, st);
+        if (rc != RSM_EUNSUPPORTED) return rc;
+    }
+    if (phases == 3) {  // k = 128: one queue-driven launch
         const int rc = extend_squares_queue(ctx, d_eds, k, S, count, st);
         if (rc != RSM_EUNSUPPORTED) return rc;
     }
@@ -544,6 +568,13 @@ int rsm_ctx_set_pass_grid(rsm_ctx* ctx, int pass, int cus, int* previous) {
     if (!ctx || (pass != 0 && pass != 1) || cus < 0)
         return fail(RSM_EINVAL, "rsm_ctx_set_pass_grid: pass must be 0 (rows) or 1 (columns), cus >= 0");
     const uint32_t prev = ctx->pass_grid[pass].exchange((uint32_t)cus);
+    if (previous) *previous = (int)prev;
+    return RSM_OK;
+}
+
+int rsm_ctx_set_split_max(rsm_ctx* ctx, int squares, int* previous) {
+    if (!ctx || squares < 0) return fail(RSM_EINVAL, "rsm_ctx_set_split_max: squares must be >= 0");
+    const uint32_t prev = ctx->split_max.exchange((uint32_t)squares);
     if (previous) *previous = (int)prev;
     return RSM_OK;
 }

@@ -3,8 +3,9 @@
 Runs the c2 production shape (256 squares per launch, launches on 3 streams over 3
 buffers), records one launch's per-set phase boundaries (thread 0, 100 MHz clock)
 and prints the mean duration of every phase in us, per set kind.
-usage: python3 scripts/diag/trace_phases.py [mode ...]   (51010 production + trace,
-       51014 no global memory + trace, 51012 no arithmetic + trace)
+usage: python3 scripts/diag/trace_phases.py [mode ...]   (51030 production + trace,
+       51010 LDS-DMA form + trace, 51014 no global memory + trace, 51012 no arithmetic
+       + trace)
 """
 import ctypes
 import json
@@ -91,4 +92,4 @@ def main(modes):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1:] or ["51010", "51014", "51012"])
+    main(sys.argv[1:] or ["51030", "51014", "51012"])

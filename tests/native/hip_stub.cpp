@@ -150,6 +150,10 @@ hipError_t launch_decode_gf16(const DecodeSet& ds, const Gf16Dev& g, hipStream_t
 }
 bool bs128_applicable(const CodewordSet&) { return false; }
 hipError_t launch_encode_gf8_bs128(const CodewordSet& cs, hipStream_t st) { return launch_encode_gf8(cs, st); }
+hipError_t launch_encode_gf8_split(const CodewordSet& a, const CodewordSet* b, hipStream_t st) {
+    if (hipError_t e = launch_encode_gf8(a, st)) return e;
+    return b ? launch_encode_gf8(*b, st) : hipSuccess;
+}
 // the single-launch batch path never qualifies here (batches take the two-launch form)
 bool bs128_queue_applicable(const CodewordSet&, const CodewordSet&) { return false; }
 hipError_t launch_extend_gf8_bs128_queue(const QueuePlan&, hipStream_t) { return hipErrorInvalidValue; }

@@ -145,14 +145,51 @@ def test_single_launch_batch_matches_two_launch(lib, S, count):
     R._check(lib.rsm_extend_squares_phase_dev(ctx, a.ptr, k, S, count, 2, None))
     R._check(lib.rsm_sync(ctx))
     want = a.download(n)
-    for _ in range(2):
-        R._check(lib.rsm_memcpy(ctx, b.ptr, src.ptr, n, 2))
-        R._check(lib.rsm_extend_squares_dev(ctx, b.ptr, k, S, count, None))
-        R._check(lib.rsm_sync(ctx))
-        assert np.array_equal(b.download(n), want)
+    prev = ctypes.c_int(0)
+    R._check(lib.rsm_ctx_set_split_max(ctx, 0, ctypes.byref(prev)))  # the queue launch even for 1..4
+    try:
+        for _ in range(2):
+            R._check(lib.rsm_memcpy(ctx, b.ptr, src.ptr, n, 2))
+            R._check(lib.rsm_extend_squares_dev(ctx, b.ptr, k, S, count, None))
+            R._check(lib.rsm_sync(ctx))
+            assert np.array_equal(b.download(n), want)
+    finally:
+        R._check(lib.rsm_ctx_set_split_max(ctx, prev.value, None))
     sq = want.reshape(count, W, W, S)
     for i in (0, count - 1):
         assert np.array_equal(sq[i], oracle.extend_square(sq[i, :k, :k].copy(), nthreads=8))
+
+
+@pytest.mark.parametrize("k,S,count", [(128, 512, 1), (128, 512, 4), (65, 64, 2), (100, 1024, 1), (128, 64, 3),
+                                       (127, 320, 1)])
+def test_split_latency_form(lib, k, S, count):
+    """Up to rsm_ctx_set_split_max squares per call (default 4) with 65 <= k <= 128 take
+    the latency form (encode_gf8_split_kernel: rows + Q0 columns in one launch, Q1
+    columns in a second): every square bit-exact with the oracle and with the
+    queue-driven launch of the same batch."""
+    ctx = R.device_context(0)
+    W = 2 * k
+    n = W * W * S * count
+    src, a, b = (R.DeviceBuffer(n) for _ in range(3))
+    src.fill_random(1300 + k + count)
+    R._check(lib.rsm_sync(ctx))
+    prev = ctypes.c_int(0)
+    R._check(lib.rsm_ctx_set_split_max(ctx, 4, ctypes.byref(prev)))
+    try:
+        R._check(lib.rsm_memcpy(ctx, a.ptr, src.ptr, n, 2))
+        R._check(lib.rsm_extend_squares_dev(ctx, a.ptr, k, S, count, None))  # split form
+        R._check(lib.rsm_ctx_set_split_max(ctx, 0, None))
+        R._check(lib.rsm_memcpy(ctx, b.ptr, src.ptr, n, 2))
+        R._check(lib.rsm_extend_squares_dev(ctx, b.ptr, k, S, count, None))  # queue / two-launch form
+        R._check(lib.rsm_sync(ctx))
+    finally:
+        R._check(lib.rsm_ctx_set_split_max(ctx, prev.value, None))
+    got = a.download(n)
+    assert np.array_equal(got, b.download(n))
+    sq = got.reshape(count, W, W, S)
+    for i in range(count):
+        assert np.array_equal(sq[i], oracle.extend_square(sq[i, :k, :k].copy(), nthreads=8))
+    assert lib.rsm_ctx_set_split_max(ctx, -1, None) == R.RSM_EINVAL
 
 
 def test_single_launch_batches_on_three_streams(lib):
