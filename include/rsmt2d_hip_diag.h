@@ -29,6 +29,12 @@ int rsm_diag_set_trace(void* d_trace);
 /* Phase stamps of the M = 128 split decoder: 8 words (s_memrealtime, 100 MHz) per
  * workgroup of every following GF(2^8) decode launch; NULL = off. */
 int rsm_diag_set_dec_trace(void* d_trace);
+/* Waves per (codeword, 256-B chunk) of the two launches of the latency-form extension
+ * (2, 4 or 8 each; production 8 / 8). */
+int rsm_diag_set_split_waves(int first, int second);
+/* One square in the latency form: 1 = one launch with a device-side wait (A/B only:
+ * slower), 0 = two launches (production). */
+int rsm_diag_set_split_fused(int on);
 /* Both passes of `count` in-place k = 128 squares in ONE persistent launch
  * (extend_gf8_bs128q_kernel: row and Q0-column sets from one queue, Q1-column sets
  * from a ready list; `delay` squares of row sets lead the Q0-column sets).

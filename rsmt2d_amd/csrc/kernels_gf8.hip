@@ -508,7 +508,7 @@ __device__ __forceinline__ void dec_stamp(const DecodeSet& ds, int i) {
 
 template <int NW, bool ZC>
 __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t task, uint32_t (&xch)[256][64],
-                                                  PermTab (&ptab)[2][256]) {
+                                                  PermTab (&ptab)[2][256], PermTab (&stab)[256]) {
     constexpr int PW = 256 / NW, HALF = NW / 2;
     if constexpr (!ZC) dec_stamp(ds, 0);
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -548,21 +548,40 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
             v[j] = __builtin_amdgcn_raw_buffer_load_b32(ri, off, so, 0);
         });
     };
-    if constexpr (!ZC) load_points(valid);
-    // wave 0's error-locator weights, loaded with the points (off the critical path)
+    // presence bytes first: the ballots (and wave 0's error locator) wait only for them,
+    // while the points' loads -- issued right behind, an asm barrier keeps the order --
+    // are still in flight (vmcnt retires in order: presence loads queued behind the
+    // points made the locator wait for every point, 6.5 of 26 us per task,
+    // profiles/r03_trace_decode.jsonl)
+    uint32_t pv[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const uint32_t e = g * 64u + lane;
+        pv[g] = e < Wd ? ds.presence[cell0 + e * cell_step] : 0u;
+    }
+    // wave 0's error-locator weights and the 256 multiply tables (5 KiB, staged into
+    // LDS for the per-point gathers below), also ahead of the points
     uint32_t lw[4] = {0, 0, 0, 0};
+    constexpr int kTabWords = 256 * 5 / 64;
+    uint32_t sv[kTabWords];
     if (w == 0) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) lw[j] = d_gf8.logwalsh[lane * 4u + j];
+        const uint32_t* tw = reinterpret_cast<const uint32_t*>(&d_perm8.t[0]);
+#pragma unroll
+        for (int i = 0; i < kTabWords; ++i) sv[i] = tw[i * 64 + lane];
+    }
+    asm volatile("" ::: "memory");
+    if constexpr (!ZC) load_points(valid);
+    if (w == 0) {
+        uint32_t* st = reinterpret_cast<uint32_t*>(&stab[0]);
+#pragma unroll
+        for (int i = 0; i < kTabWords; ++i) st[i * 64 + lane] = sv[i];
     }
 
     uint64_t pres[4];
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-        const uint32_t e = g * 64u + lane;
-        const bool p = e < Wd && ds.presence[cell0 + e * cell_step] != 0;
-        pres[g] = __ballot(p);
-    }
+    for (int g = 0; g < 4; ++g) pres[g] = __ballot(pv[g] != 0);
     auto present = [&](uint32_t e) -> bool { return (pres[e >> 6] >> (e & 63u)) & 1u; };
     const uint64_t have = pres_bits(pres, w < HALF ? k + ib : ib) & valid;
     if constexpr (!ZC) dec_stamp(ds, 1);
@@ -590,8 +609,8 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
             const uint32_t e = lane * 4u + j;  // point e: a present, valid input?
             const uint32_t i = e < 128u ? e : e - 128u;
             const bool in = i < k && present(e < 128u ? k + e : i);
-            ptab[0][e] = in ? d_perm8.t[er[j]] : PermTab{0, 0, 0, 0, 0};
-            ptab[1][e] = d_perm8.t[255u - er[j]];
+            ptab[0][e] = in ? stab[er[j]] : PermTab{0, 0, 0, 0, 0};
+            ptab[1][e] = stab[255u - er[j]];
         }
     }
     if constexpr (ZC) {  // the present cells also land in the device square
@@ -669,7 +688,8 @@ template <int NW>
 __global__ __launch_bounds__(64 * NW, NW / 2) void decode_gf8_split_kernel(DecodeSet ds) {
     __shared__ uint32_t xch[256][64];
     __shared__ PermTab ptab[2][256];
-    decode_split_task<NW, false>(ds, blockIdx.x, xch, ptab);
+    __shared__ PermTab stab[256];
+    decode_split_task<NW, false>(ds, blockIdx.x, xch, ptab, stab);
 }
 
 // zero-copy form: a capped grid loops over the tasks
@@ -677,9 +697,10 @@ template <int NW>
 __global__ __launch_bounds__(64 * NW, NW / 2) void decode_gf8_split_zc_kernel(DecodeSet ds) {
     __shared__ uint32_t xch[256][64];
     __shared__ PermTab ptab[2][256];
+    __shared__ PermTab stab[256];
     const uint32_t tasks = ds.count * ds.chunks;
     for (uint32_t task = blockIdx.x; task < tasks; task += gridDim.x) {
-        decode_split_task<NW, true>(ds, __builtin_amdgcn_readfirstlane(task), xch, ptab);
+        decode_split_task<NW, true>(ds, __builtin_amdgcn_readfirstlane(task), xch, ptab, stab);
         __syncthreads();  // LDS (xch, ptab) is reused by the next task
     }
 }
@@ -696,14 +717,18 @@ __global__ __launch_bounds__(64 * NW, NW / 2) void decode_gf8_split_zc_kernel(De
 //             m - 1 = 127) and FFT layers PW/2..1 (offset -1) with per-wave twiddles
 //             (one compile-time variant per wave, chosen by a wave-uniform branch);
 //   L layout: wave w holds e = NW h + w (h < PW): IFFT layers PW..64 and FFT layers
-//             64..PW, twiddles independent of w (2d >= NW).
+//             64..PW (the top pair merged), twiddles independent of w (d >= PW >= NW).
 // Same butterflies as encode_gf8_kernel<128> (klauspost leopard8
 // ifftDITEncoder8 / fftDIT8), so the same parity; LDS [128 points][64 lanes] dwords.
 // ---------------------------------------------------------------------------
+constexpr unsigned log_of_sum8(unsigned L1, unsigned L2) {
+    const unsigned a = L1 == 255u ? 0u : kGf8.exp[L1], b = L2 == 255u ? 0u : kGf8.exp[L2];
+    return (a ^ b) == 0u ? 255u : kGf8.log[a ^ b];
+}
 template <int NW, int PW, bool FFT>
 __device__ __forceinline__ void enc_split_high(uint32_t (&v)[PW]) {
-    static_for<7>([&](auto LG) {
-        constexpr int d = FFT ? (64 >> decltype(LG)::value) : (1 << decltype(LG)::value);
+    static_for<6>([&](auto LG) {  // d = PW .. 32: the top layer d = 64 is enc_split_mid
+        constexpr int d = FFT ? (32 >> decltype(LG)::value) : (1 << decltype(LG)::value);
         if constexpr (d >= PW) {
             constexpr int sd = d / NW;
             static_for<PW>([&](auto H) {
@@ -715,6 +740,22 @@ __device__ __forceinline__ void enc_split_high(uint32_t (&v)[PW]) {
                     else ifft2<L>(v[h], v[h + sd]);
                 }
             });
+        }
+    });
+}
+// The last IFFT layer and the first FFT layer (d = 64) join the same pairs: one
+// multiply by exp(L1) + exp(L2) instead of two (bs8.hpp mid2, by linearity):
+// y ^= x; x ^= y * (exp L1 + exp L2); y ^= x.
+template <int NW, int PW>
+__device__ __forceinline__ void enc_split_mid(uint32_t (&v)[PW]) {
+    constexpr int sd = 64 / NW;
+    constexpr unsigned L = log_of_sum8(kGf8.skew[127 + 64], kGf8.skew[-1 + 64]);
+    static_for<PW>([&](auto H) {
+        constexpr int h = decltype(H)::value;
+        if constexpr (((h / sd) & 1) == 0) {
+            v[h + sd] ^= v[h];
+            if constexpr (L != 255u) gf8_muladd_ct<L>(v[h], v[h + sd]);
+            v[h + sd] ^= v[h];
         }
     });
 }
@@ -730,21 +771,49 @@ __device__ __forceinline__ void enc_split_low(uint32_t (&v)[PW], uint32_t w) {
 }
 
 struct SplitEncPlan {
-    CodewordSet cs[2];
-    uint32_t n0;  // tasks of cs[0]; the rest belong to cs[1]
+    CodewordSet cs[3];
+    uint32_t n0, n1, n2;  // tasks of cs[0], cs[1], cs[2] (in this order of block index)
+    // fused form (one square: every workgroup co-resident): cs[0] = rows of Q0 -> Q1,
+    // cs[1] = columns of Q0 -> Q2, cs[2] = columns of Q1 -> Q3, whose workgroups wait
+    // for every row task (ctr[0] == n0); ctr[32] counts finished Q1-column tasks, the
+    // last one re-zeroes both words; err: pinned host word set by a stuck wait
+    uint32_t* ctr;
+    uint32_t* err;
+    uint32_t fused;
 };
+constexpr uint32_t kSplitSpinLimit = 1u << 20;  // polls (~1 s) before a wait is declared stuck
 
 template <int NW>
 __global__ __launch_bounds__(64 * NW) void encode_gf8_split_kernel(SplitEncPlan p) {
     constexpr int PW = 128 / NW;
-    static_assert(PW * NW == 128 && 2 * PW >= NW, "split encoder shape");
+    // every layer d < PW is in S and every d >= PW must be in-register in L (d a
+    // multiple of NW): PW >= NW
+    static_assert(PW * NW == 128 && PW >= NW, "split encoder shape");
     __shared__ uint32_t xch[128][64];
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
     uint32_t task = blockIdx.x;
-    const bool second = task >= p.n0;
-    const CodewordSet& cs = second ? p.cs[1] : p.cs[0];
-    if (second) task -= p.n0;
+    const uint32_t kind = task < p.n0 ? 0u : (task < p.n0 + p.n1 ? 1u : 2u);
+    task -= kind == 0u ? 0u : (kind == 1u ? p.n0 : p.n0 + p.n1);
+    const CodewordSet& cs = p.cs[kind];
+    const bool fused = p.fused != 0u;
+    if (fused && kind == 2u) {
+        // wait for every row task's Q1 (their counter adds follow their sc1 stores and
+        // a vmcnt(0) + barrier); then ONE agent acquire before the barrier that
+        // precedes this workgroup's loads (hand-off argument)
+        if (threadIdx.x == 0) {
+            uint32_t n = 0;
+            while (__hip_atomic_load(p.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < p.n0) {
+                if (++n >= kSplitSpinLimit) {
+                    __hip_atomic_store(p.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        }
+        __syncthreads();
+    }
     const uint32_t chunks = cs.chunks;
     const uint32_t q = task / chunks;
     const uint32_t chunk = task - q * chunks;
@@ -765,36 +834,96 @@ __global__ __launch_bounds__(64 * NW) void encode_gf8_split_kernel(SplitEncPlan 
     __syncthreads();
     static_for<PW>([&](auto H) { v[decltype(H)::value] = xch[NW * decltype(H)::value + w][lane]; });
     enc_split_high<NW, PW, false>(v);
+    enc_split_mid<NW, PW>(v);
     enc_split_high<NW, PW, true>(v);
     __syncthreads();
     static_for<PW>([&](auto H) { xch[NW * decltype(H)::value + w][lane] = v[decltype(H)::value]; });
     __syncthreads();
     static_for<PW>([&](auto J) { v[decltype(J)::value] = xch[PW * w + decltype(J)::value][lane]; });
     enc_split_low<NW, PW, true>(v, w);
+    const bool handoff = fused && kind == 0u;  // Q1 of the fused form: write-through (sc1)
     static_for<PW>([&](auto J) {
         constexpr int j = decltype(J)::value;
         const uint32_t e = PW * w + j;
-        __builtin_amdgcn_raw_buffer_store_b32(v[j], ro, off, e < k ? oo + e * es : kOob, 0);
+        const uint32_t so = e < k ? oo + e * es : kOob;
+        if (handoff) __builtin_amdgcn_raw_buffer_store_b32(v[j], ro, off, so, 16);
+        else __builtin_amdgcn_raw_buffer_store_b32(v[j], ro, off, so, 0);
     });
+    if (handoff) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_fetch_add(p.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (fused && kind == 2u && threadIdx.x == 0) {
+        if (__hip_atomic_fetch_add(p.ctr + 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == p.n2 - 1u) {
+            __hip_atomic_store(p.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // every waiter is past its wait
+            __hip_atomic_store(p.ctr + 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 }
-constexpr int kEncSplitWaves = 4;
+// waves per (codeword, chunk): production 8 for both launches (single square 21.1 us
+// against 25.3 at 4 / 4, profiles/r03_single.jsonl); diagnostic builds take
+// rsm_diag_set_split_waves (A/B of 2 / 4 / 8 per launch)
+#ifdef RSM_DIAG
+static std::atomic<int> g_split_nw[2] = {8, 8};
+static std::atomic<bool> g_split_fused{false};
+void set_split_diag_waves(int first, int second) {
+    g_split_nw[0].store(first);
+    g_split_nw[1].store(second);
+}
+void set_split_diag_fused(bool on) { g_split_fused.store(on); }
+bool split_fused_enabled() { return g_split_fused.load(); }
+#else
+// the one-launch form with its device-side wait measured SLOWER than two launches
+// (30.1 vs 22.2 us: the write-through Q1 stores leave L2 and the Q1-column workgroups
+// read them back from the Infinity Cache; profiles/r03_single.jsonl) -- diagnostic only
+bool split_fused_enabled() { return false; }
+#endif
+
+static hipError_t launch_split(const SplitEncPlan& p, uint32_t tasks, int nw, hipStream_t st) {
+    switch (nw) {
+        case 2: hipLaunchKernelGGL(encode_gf8_split_kernel<2>, dim3(tasks), dim3(128), 0, st, p); break;
+        case 8: hipLaunchKernelGGL(encode_gf8_split_kernel<8>, dim3(tasks), dim3(512), 0, st, p); break;
+        default: hipLaunchKernelGGL(encode_gf8_split_kernel<4>, dim3(tasks), dim3(256), 0, st, p); break;
+    }
+    return hipGetLastError();
+}
+static int split_waves(int launch) {
+#ifdef RSM_DIAG
+    return g_split_nw[launch].load();
+#else
+    (void)launch;
+    return 8;
+#endif
+}
+static void split_set(SplitEncPlan& p, int i, const CodewordSet& c, uint32_t& n) {
+    p.cs[i] = c;
+    p.cs[i].chunks = (c.S + 255) / 256;
+    n = p.cs[i].count * p.cs[i].chunks;
+}
 
 hipError_t launch_encode_gf8_split(const CodewordSet& a, const CodewordSet* b, hipStream_t st) {
     if (ceil_pow2(a.k) != 128 || (b && ceil_pow2(b->k) != 128)) return hipErrorInvalidValue;
     SplitEncPlan p{};
-    p.cs[0] = a;
-    p.cs[0].chunks = (a.S + 255) / 256;
-    p.n0 = p.cs[0].count * p.cs[0].chunks;
-    uint64_t tasks = p.n0;
-    if (b) {
-        p.cs[1] = *b;
-        p.cs[1].chunks = (b->S + 255) / 256;
-        tasks += (uint64_t)p.cs[1].count * p.cs[1].chunks;
-    }
+    split_set(p, 0, a, p.n0);
+    if (b) split_set(p, 1, *b, p.n1);
+    const uint64_t tasks = (uint64_t)p.n0 + p.n1;
     if (tasks == 0) return hipSuccess;
-    hipLaunchKernelGGL(encode_gf8_split_kernel<kEncSplitWaves>, dim3((uint32_t)tasks), dim3(64 * kEncSplitWaves), 0,
-                       st, p);
-    return hipGetLastError();
+    return launch_split(p, (uint32_t)tasks, split_waves(b ? 0 : 1), st);
+}
+
+hipError_t launch_extend_gf8_split_fused(const CodewordSet& rows, const CodewordSet& c0, const CodewordSet& c1,
+                                         uint32_t* ctr, uint32_t* err, hipStream_t st) {
+    if (ceil_pow2(rows.k) != 128) return hipErrorInvalidValue;
+    SplitEncPlan p{};
+    split_set(p, 0, rows, p.n0);
+    split_set(p, 1, c0, p.n1);
+    split_set(p, 2, c1, p.n2);
+    p.ctr = ctr;
+    p.err = err;
+    p.fused = 1;
+    const uint64_t tasks = (uint64_t)p.n0 + p.n1 + p.n2;
+    if (tasks == 0 || p.n2 == 0) return hipErrorInvalidValue;
+    return launch_split(p, (uint32_t)tasks, split_waves(0), st);
 }
 
 // ---------------------------------------------------------------------------

@@ -57,6 +57,18 @@ int rsm_diag_set_trace(void* d_trace) {
     return RSM_OK;
 }
 
+int rsm_diag_set_split_waves(int first, int second) {
+    auto ok = [](int n) { return n == 2 || n == 4 || n == 8; };
+    if (!ok(first) || !ok(second)) return RSM_EINVAL;
+    set_split_diag_waves(first, second);
+    return RSM_OK;
+}
+
+int rsm_diag_set_split_fused(int on) {
+    set_split_diag_fused(on != 0);
+    return RSM_OK;
+}
+
 int rsm_diag_set_dec_trace(void* d_trace) {
     set_dec_diag_trace(static_cast<uint32_t*>(d_trace));
     return RSM_OK;

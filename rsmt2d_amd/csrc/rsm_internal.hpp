@@ -87,7 +87,7 @@ struct rsm_ctx {
     uint32_t cus = 256;          // compute units of `device` (persistent-grid size)
     hipStream_t stream = nullptr;
     std::atomic<uint32_t> pass_grid[2] = {0, 0};  // rsm_ctx_set_pass_grid (0 = all CUs)
-    std::atomic<uint32_t> split_max{4};            // rsm_ctx_set_split_max
+    std::atomic<uint32_t> split_max{12};           // rsm_ctx_set_split_max
 
     // lane pool (Codec calls, host-memory extension)
     static constexpr size_t kMaxLanes = 32;

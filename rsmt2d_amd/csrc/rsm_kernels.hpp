@@ -75,6 +75,15 @@ hipError_t launch_decode_gf8(const DecodeSet& ds, hipStream_t st);
 // byte tables, every CU busy.  Launches the codewords of `a` and, if b != nullptr,
 // those of `b` in the same grid.
 hipError_t launch_encode_gf8_split(const CodewordSet& a, const CodewordSet* b, hipStream_t st);
+void set_split_diag_waves(int first, int second);  // diagnostic builds only
+void set_split_diag_fused(bool on);                  // diagnostic builds only
+bool split_fused_enabled();                          // product: always
+// One square in ONE launch of the split encoder (rows -> Q1, Q0 columns -> Q2, then
+// Q1 columns -> Q3 behind a device-side wait on the row tasks); ctr: >= 33 zeroed
+// words it leaves zeroed, err: pinned host word set by a stuck wait.  Every workgroup
+// must be able to be resident at once (the caller checks the grid).
+hipError_t launch_extend_gf8_split_fused(const CodewordSet& rows, const CodewordSet& c0, const CodewordSet& c1,
+                                         uint32_t* ctr, uint32_t* err, hipStream_t st);
 struct Gf16Dev;
 hipError_t launch_encode_gf16(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st);
 hipError_t launch_decode_gf16(const DecodeSet& ds, const Gf16Dev& g, hipStream_t st);

@@ -324,6 +324,23 @@ int check_queue_reports(rsm_ctx* ctx, hipStream_t st) {
                  : RSM_OK;
 }
 
+// The stream's device-side hand-off words (zeroed once: every launch that uses them
+// leaves them zeroed) and its pinned stuck-wait report word; caller holds ss.mu.
+static int queue_words(StreamScratch& ss, uint32_t count, hipStream_t st) {
+    const size_t bytes = (kQueueFixedWords + 2 * (size_t)count) * 4;
+    hipError_t e;
+    if (bytes > ss.queue.cap) {
+        if ((e = hipStreamSynchronize(st)) != hipSuccess || (e = ss.queue.ensure(bytes)) != hipSuccess ||
+            (e = hipMemsetAsync(ss.queue.ptr, 0, ss.queue.cap, st)) != hipSuccess)
+            return hip_fail(e, "single-launch extension: queue words");
+    }
+    if (!ss.qerr.ptr) {
+        if ((e = ss.qerr.ensure(64)) != hipSuccess) return hip_fail(e, "single-launch extension: report word");
+        *static_cast<volatile uint32_t*>(ss.qerr.ptr) = 0;
+    }
+    return RSM_OK;
+}
+
 int extend_squares_queue(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, uint32_t count, hipStream_t st,
                          uint32_t delay, uint32_t margin) {
     if (field_bits(k) != 8 || count == 0) return RSM_EUNSUPPORTED;
@@ -343,20 +360,10 @@ int extend_squares_queue(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, u
     p.margin = margin == ~0u ? p.rn / 2 : margin;
     StreamScratch& ss = stream_scratch(ctx, st);
     std::lock_guard<std::mutex> lk(ss.mu);
-    const size_t bytes = (kQueueFixedWords + 2 * (size_t)count) * 4;
-    hipError_t e;
-    if (bytes > ss.queue.cap) {  // zeroed once: every launch leaves its words zeroed
-        if ((e = hipStreamSynchronize(st)) != hipSuccess || (e = ss.queue.ensure(bytes)) != hipSuccess ||
-            (e = hipMemsetAsync(ss.queue.ptr, 0, ss.queue.cap, st)) != hipSuccess)
-            return hip_fail(e, "single-launch extension: queue words");
-    }
-    if (!ss.qerr.ptr) {
-        if ((e = ss.qerr.ensure(64)) != hipSuccess) return hip_fail(e, "single-launch extension: report word");
-        *static_cast<volatile uint32_t*>(ss.qerr.ptr) = 0;
-    }
+    if (int rc = queue_words(ss, count, st)) return rc;
     p.ctr = static_cast<uint32_t*>(ss.queue.ptr);
     p.err = static_cast<uint32_t*>(ss.qerr.ptr);
-    if ((e = launch_extend_gf8_bs128_queue(p, st)) != hipSuccess) return hip_fail(e, "single-launch extension");
+    if (hipError_t e = launch_extend_gf8_bs128_queue(p, st)) return hip_fail(e, "single-launch extension");
     return RSM_OK;
 }
 
@@ -365,7 +372,7 @@ int extend_squares_queue(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, u
 // columns of Q0 -> Q2, launch 2 = columns of Q1 -> Q3, both on the split byte-table
 // encoder (NW waves per codeword chunk), so each phase spreads over every CU instead
 // of the queue kernel's 64 + 32 sets of ~16 us each.
-int extend_squares_split(uint8_t* d_eds, uint32_t k, uint32_t S, uint32_t count, hipStream_t st) {
+int extend_squares_split(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, uint32_t count, hipStream_t st) {
     if (field_bits(k) != 8 || ceil_pow2(k) != 128 || count == 0) return RSM_EUNSUPPORTED;
     const CodewordSet rows = rows_set(d_eds, k, S, count);
     CodewordSet c0 = cols_set(d_eds, k, S, count);  // columns 0 .. k-1 (Q0 -> Q2)
@@ -374,20 +381,36 @@ int extend_squares_split(uint8_t* d_eds, uint32_t k, uint32_t S, uint32_t count,
     CodewordSet c1 = c0;  // columns k .. 2k-1 (Q1 -> Q3)
     c1.base = c1.out_base = d_eds + (uint64_t)k * S;
     hipError_t e;
-    if ((e = launch_encode_gf8_split(rows, &c0, st)) != hipSuccess) return hip_fail(e, "split extension (rows + Q0 columns)");
-    if ((e = launch_encode_gf8_split(c1, nullptr, st)) != hipSuccess) return hip_fail(e, "split extension (Q1 columns)");
+    // one square: ONE launch whose Q1-column workgroups wait on the device for the row
+    // tasks -- 3 k ceil(S / 256) workgroups of 8 waves, resident at once when they fit
+    // 4 per CU (otherwise the two launches below)
+    const uint64_t wgs = 3ull * k * ((S + 255) / 256);
+    if (count == 1 && wgs <= 4ull * ctx->cus && split_fused_enabled()) {
+        if (int rc = check_queue_reports(ctx, st)) return rc;
+        StreamScratch& ss = stream_scratch(ctx, st);
+        std::lock_guard<std::mutex> lk(ss.mu);
+        if (int rc = queue_words(ss, count, st)) return rc;
+        if ((e = launch_extend_gf8_split_fused(rows, c0, c1, static_cast<uint32_t*>(ss.queue.ptr),
+                                               static_cast<uint32_t*>(ss.qerr.ptr), st)) != hipSuccess)
+            return hip_fail(e, "split extension (one launch)");
+        return RSM_OK;
+    }
+    // launch 1 = rows + Q0 columns, launch 2 = Q1 columns (moving half of the Q0
+    // columns into launch 2 measured 25.9 against 21.9 us per square, r03m)
+    if ((e = launch_encode_gf8_split(rows, &c0, st)) != hipSuccess) return hip_fail(e, "split extension (launch 1)");
+    if ((e = launch_encode_gf8_split(c1, nullptr, st)) != hipSuccess) return hip_fail(e, "split extension (launch 2)");
     return RSM_OK;
 }
 
 // Two-phase in-place extension; batches of k = 128 squares run both phases as one
 // queue-driven launch (extend_squares_queue), which re-reads Q0 and Q1 from the
 // Infinity Cache instead of HBM; up to ctx->split_max squares take the latency form
-// (rsm_ctx_set_split_max; default 4, profiles/r03_single.jsonl).
+// (rsm_ctx_set_split_max; default 12: the crossover, profiles/r03_single.jsonl).
 int extend_squares(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, uint32_t count, hipStream_t st,
                    int phases) {
     const uint64_t W = 2ull * k;
     if (phases == 3 && count <= ctx->split_max.load(std::memory_order_relaxed)) {
-        const int rc = extend_squares_split(d_eds, k, S, count, st);
+        const int rc = extend_squares_split(ctx, d_eds, k, S, count, st);
         if (rc != RSM_EUNSUPPORTED) return rc;
     }
     if (phases == 3) {  // k = 128: one queue-driven launch

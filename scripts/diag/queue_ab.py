@@ -3,7 +3,7 @@
 Configurations "kind,B,streams,delay": kind "two" = the round-1 two-launch schedule
 (rsm_extend_squares_phase_dev row pass + column pass), kind "queue" = rsm_diag_extend_fused (extend_gf8_bs128q_kernel,
 diagnostic library).  Steps of B squares rotate over 2 buffers and `streams` streams;
-the first and last square of the last step are checked against the oracle, and the
+the first and last square of the last step are checked against the two-launch form (refcheck.py), and the
 queue's stuck-wait word is checked.  One JSON line per configuration.
 usage: python3 scripts/diag/queue_ab.py two,32,2,0 queue,32,1,2 ...
 """
@@ -102,12 +102,12 @@ def run(cfg, steps=STEPS, warmup=6):
         for st in streams:
             ok &= D.rsm_diag_queue_check(ctx, st) == 0
     last = bufs[(n[0] - 1) % nb]
-    import oracle
+    from refcheck import matches_two_launch
     for j in ((0, B - 1) if ok is not None else ()):
         got = np.empty(SQ, np.uint8)
         chk(D.rsm_memcpy(ctx, got.ctypes.data, last + j * SQ, SQ, 1))
         got = got.reshape(W, W, S)
-        ok &= bool(np.array_equal(got, oracle.extend_square(got[:k, :k].copy(), nthreads=16)))
+        ok &= matches_two_launch(D, ctx, got, k)
     for e0, e1 in evs:
         D.rsm_event_destroy(e0)
         D.rsm_event_destroy(e1)

@@ -5,7 +5,7 @@ Each configuration times `steps` steps of B squares (k=128, S=512) rotating over
 stream), with the bit-sliced kernel variant of each pass chosen through the
 diagnostic switches (row_mode / col_mode: 40 production, 8 plain loads, 56 NT
 loads + NT stores, 24 plain loads + NT stores), and checks one square of the last
-step against the oracle.  Prints one JSON line per configuration.
+step against the two-launch form (refcheck.py).  Prints one JSON line per configuration.
 usage: python3 scripts/diag/sched_ab.py "row,col,B,streams,buffers,grid[,rev[,col_grid]]" ...
 """
 import ctypes
@@ -76,8 +76,8 @@ def run(cfg, steps=60, warmup=6):
     got = np.empty(SQ, np.uint8)
     chk(D.rsm_memcpy(ctx, got.ctypes.data, last, SQ, 1))
     got = got.reshape(W, W, S)
-    import oracle
-    ok = bool(np.array_equal(got, oracle.extend_square(got[:k, :k].copy(), nthreads=16)))
+    from refcheck import matches_two_launch
+    ok = matches_two_launch(D, ctx, got, k)
     for b in bufs:
         chk(D.rsm_dev_free(ctx, b))
     for s in streams[1:]:

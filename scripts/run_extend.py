@@ -27,15 +27,15 @@ dt = (time.perf_counter() - t0) / reps
 msg = ""
 if os.environ.get("CHECK") and phase == 3:
     import numpy as np
-    import oracle
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "diag"))
+    from refcheck import matches_two_launch
     buf.fill_random(11)
     R._check(L.rsm_extend_squares_phase_dev(ctx, buf.ptr, k, S, B, 3, None))
     R._check(L.rsm_sync(ctx))
     allb = buf.download(B * W * W * S).reshape(B, W, W, S)
     bad = 0
     for i in sorted({0, B // 2, B - 1}):
-        want = oracle.extend_square(allb[i, :k, :k].copy(), nthreads=8)
-        bad += int(not np.array_equal(allb[i], want))
+        bad += int(not matches_two_launch(L, ctx, allb[i].copy(), k))
     msg = " CHECK " + ("ok" if bad == 0 else f"FAILED ({bad} squares differ)")
 print(f"B={B} phase={phase}: {dt*1e6:.1f} us/step, {B*k*k*S/dt/2**30:.1f} GiB/s ODS{msg}")
 buf.free()

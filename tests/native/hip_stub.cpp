@@ -150,6 +150,11 @@ hipError_t launch_decode_gf16(const DecodeSet& ds, const Gf16Dev& g, hipStream_t
 }
 bool bs128_applicable(const CodewordSet&) { return false; }
 hipError_t launch_encode_gf8_bs128(const CodewordSet& cs, hipStream_t st) { return launch_encode_gf8(cs, st); }
+bool split_fused_enabled() { return false; }  // the stub runs the two-launch form
+hipError_t launch_extend_gf8_split_fused(const CodewordSet&, const CodewordSet&, const CodewordSet&, uint32_t*,
+                                         uint32_t*, hipStream_t) {
+    return hipErrorInvalidValue;
+}
 hipError_t launch_encode_gf8_split(const CodewordSet& a, const CodewordSet* b, hipStream_t st) {
     if (hipError_t e = launch_encode_gf8(a, st)) return e;
     return b ? launch_encode_gf8(*b, st) : hipSuccess;
