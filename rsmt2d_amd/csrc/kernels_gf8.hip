@@ -255,6 +255,25 @@ __device__ __forceinline__ uint32_t submod8(uint32_t a, uint32_t b) {
     return (d + (d >> 8)) & 255u;
 }
 
+// x of lane (lane ^ 2^LD), all 64 lanes active.  Lane-crossing without LDS round
+// trips where the hardware has a direct form (ds_bpermute, the previous form, put
+// 24 dependent LDS round trips on the decoder's error-locator path):
+//   ^1, ^2: DPP quad_perm;  ^4: row_half_mirror (^7) then quad_perm [3,2,1,0] (^3);
+//   ^8: DPP row_ror:8;  ^16: ds_swizzle SWAP 16;  ^32: v_permlane32_swap (gfx950).
+template <int LD>
+__device__ __forceinline__ uint32_t lane_xor(uint32_t x, uint32_t lane) {
+    if constexpr (LD == 0) return __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, true);
+    else if constexpr (LD == 1) return __builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, true);
+    else if constexpr (LD == 2)
+        return __builtin_amdgcn_mov_dpp(__builtin_amdgcn_mov_dpp(x, 0x141, 0xF, 0xF, true), 0x1B, 0xF, 0xF, true);
+    else if constexpr (LD == 3) return __builtin_amdgcn_mov_dpp(x, 0x128, 0xF, 0xF, true);
+    else if constexpr (LD == 4) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x401F);
+    else {
+        const auto s = __builtin_amdgcn_permlane32_swap(x, x, false, false);  // [x_lo, x_lo], [x_hi, x_hi]
+        return lane < 32u ? s[1] : s[0];
+    }
+}
+
 // FWHT over 256 log-domain entries held 4 per lane (entry 4*lane + j in e[j]).
 __device__ __forceinline__ void fwht256(uint32_t (&e)[4], uint32_t lane) {
     // dist 1, 2 inside the lane
@@ -265,16 +284,15 @@ __device__ __forceinline__ void fwht256(uint32_t (&e)[4], uint32_t lane) {
         e[1] = addmod8(a1, a3); e[3] = submod8(a1, a3);
     }
     // dist 4..128 across lanes (partner lane = lane ^ (dist/4))
+    static_for<6>([&](auto LDc) {
+        constexpr int ld = decltype(LDc)::value;
+        const bool upper = (lane & (1u << ld)) != 0;
+        uint32_t p[4];
 #pragma unroll
-    for (int ld = 0; ld < 6; ++ld) {
-        const uint32_t mask = 1u << ld;
-        const bool upper = (lane & mask) != 0;
+        for (int j = 0; j < 4; ++j) p[j] = lane_xor<ld>(e[j], lane);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t p = __shfl_xor(e[j], (int)mask, 64);
-            e[j] = upper ? submod8(p, e[j]) : addmod8(e[j], p);
-        }
-    }
+        for (int j = 0; j < 4; ++j) e[j] = upper ? submod8(p[j], e[j]) : addmod8(e[j], p[j]);
+    });
 }
 
 // Formal derivative restricted to one half (size H) of the 2H-point decoder
@@ -508,7 +526,7 @@ __device__ __forceinline__ void dec_stamp(const DecodeSet& ds, int i) {
 
 template <int NW, bool ZC>
 __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t task, uint32_t (&xch)[256][64],
-                                                  PermTab (&ptab)[2][256], PermTab (&stab)[256]) {
+                                                  uint32_t (&erl)[2][256], PermTab (&stab)[257]) {
     constexpr int PW = 256 / NW, HALF = NW / 2;
     if constexpr (!ZC) dec_stamp(ds, 0);
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -577,6 +595,7 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
         uint32_t* st = reinterpret_cast<uint32_t*>(&stab[0]);
 #pragma unroll
         for (int i = 0; i < kTabWords; ++i) st[i * 64 + lane] = sv[i];
+        if (lane < 5u) st[256 * 5 + lane] = 0u;  // entry 256: the zero multiplier
     }
 
     uint64_t pres[4];
@@ -588,7 +607,8 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
     if constexpr (ZC) load_points(have);
 
     // error locator (log domain), as decode_gf8_kernel: entries 4 lane .. 4 lane + 3;
-    // wave 0 alone (it builds the per-point tables every wave reads)
+    // wave 0 alone: it writes each point's log multiplier (erl), and every wave then reads
+    // the staged table of its own points
     if (w == 0) {
         uint32_t er[4];
 #pragma unroll
@@ -609,8 +629,8 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
             const uint32_t e = lane * 4u + j;  // point e: a present, valid input?
             const uint32_t i = e < 128u ? e : e - 128u;
             const bool in = i < k && present(e < 128u ? k + e : i);
-            ptab[0][e] = in ? stab[er[j]] : PermTab{0, 0, 0, 0, 0};
-            ptab[1][e] = stab[255u - er[j]];
+            erl[0][e] = in ? er[j] : 256u;  // scale by exp(err), 256: absent -> 0
+            erl[1][e] = 255u - er[j];       // reveal
         }
     }
     if constexpr (ZC) {  // the present cells also land in the device square
@@ -626,7 +646,7 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
     // 1. S layout: scale every point by the error locator (absent -> 0)
     static_for<PW>([&](auto J) {
         constexpr int j = decltype(J)::value;
-        v[j] = gf8_mul_tab(v[j], ptab[0][PW * w + j]);
+        v[j] = gf8_mul_tab(v[j], stab[erl[0][PW * w + j]]);
     });
     // 2. IFFT layers 1..PW/2 (per-wave twiddles)
     split_low<NW, PW, false>(v, w);
@@ -674,7 +694,7 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
         constexpr int j = decltype(J)::value;
         const uint32_t e = PW * w + j;
         const uint32_t so = ((reveal >> j) & 1ull) ? sbase + (uint32_t)j * sstep : kOob;
-        const uint32_t x = gf8_mul_tab(v[j], ptab[1][e]);
+        const uint32_t x = gf8_mul_tab(v[j], stab[erl[1][e]]);
         __builtin_amdgcn_raw_buffer_store_b32(x, rs, off, so, 0);
         if (mirror) __builtin_amdgcn_raw_buffer_store_b32(x, rm, off, so, 0);
     });
@@ -687,21 +707,21 @@ constexpr int kSplitWaves = 16;
 template <int NW>
 __global__ __launch_bounds__(64 * NW, NW / 2) void decode_gf8_split_kernel(DecodeSet ds) {
     __shared__ uint32_t xch[256][64];
-    __shared__ PermTab ptab[2][256];
-    __shared__ PermTab stab[256];
-    decode_split_task<NW, false>(ds, blockIdx.x, xch, ptab, stab);
+    __shared__ uint32_t erl[2][256];
+    __shared__ PermTab stab[257];
+    decode_split_task<NW, false>(ds, blockIdx.x, xch, erl, stab);
 }
 
 // zero-copy form: a capped grid loops over the tasks
 template <int NW>
 __global__ __launch_bounds__(64 * NW, NW / 2) void decode_gf8_split_zc_kernel(DecodeSet ds) {
     __shared__ uint32_t xch[256][64];
-    __shared__ PermTab ptab[2][256];
-    __shared__ PermTab stab[256];
+    __shared__ uint32_t erl[2][256];
+    __shared__ PermTab stab[257];
     const uint32_t tasks = ds.count * ds.chunks;
     for (uint32_t task = blockIdx.x; task < tasks; task += gridDim.x) {
-        decode_split_task<NW, true>(ds, __builtin_amdgcn_readfirstlane(task), xch, ptab, stab);
-        __syncthreads();  // LDS (xch, ptab) is reused by the next task
+        decode_split_task<NW, true>(ds, __builtin_amdgcn_readfirstlane(task), xch, erl, stab);
+        __syncthreads();  // LDS (xch, erl, stab) is reused by the next task
     }
 }
 
