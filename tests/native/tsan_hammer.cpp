@@ -64,6 +64,16 @@ int main() {
             CHECK(rsm_dev_free(ctx, roots));
             CHECK(rsm_stream_destroy(ctx, st));
         });
+    // multi-lane host extensions (count = 3 takes 3 lanes at once) from 16 threads while
+    // the 64 Codec threads above hold lanes too: with lanes taken one at a time, 11+
+    // such callers could each hold some lanes and wait forever for the rest (ADVICE
+    // round 2); acquire_lanes takes all of a call's lanes in one step
+    for (int t = 0; t < 16; ++t)
+        th.emplace_back([ctx, t] {
+            const uint32_t k = 8, S = 64, W = 2 * k, n = 3;
+            std::vector<uint8_t> ods((size_t)n * k * k * S, (uint8_t)(t + 1)), eds((size_t)n * W * W * S);
+            for (int it = 0; it < 6; ++it) CHECK(rsm_extend_squares_host(ctx, ods.data(), k, S, n, eds.data()));
+        });
     th.emplace_back([ctx] {  // EDS layer: compute, roots, import with holes, Repair
         const uint32_t k = 4, S = 64, W = 2 * k;
         std::vector<std::vector<uint8_t>> shares(k * k, std::vector<uint8_t>(S));

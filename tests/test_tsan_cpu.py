@@ -1,6 +1,6 @@
 """CPU: ThreadSanitizer build of the product's host code (rsm_runtime.cpp, eds.cpp,
 merkle.cpp, gf16_tables.cpp) against a stubbed HIP runtime (tests/native/hip_stub.cpp),
-hammered by 69 threads on one context (tests/native/tsan_hammer.cpp): concurrent
+hammered by 85 threads on one context (tests/native/tsan_hammer.cpp): concurrent
 Encode/Decode (GF(2^8) and GF(2^16)), host-memory and device-resident extensions,
 device roots on caller streams, stream create/destroy and the EDS layer.  The
 reference runs its Codec from up to 2k goroutines under `go test -race`
