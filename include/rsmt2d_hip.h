@@ -104,11 +104,13 @@ int rsm_host_free(rsm_ctx* ctx, void* p);
 /* Device-resident, in place: d_eds holds `count` consecutive [2k][2k][S] squares
  * whose top-left quadrant already holds the ODS (the EDS aliases the ODS, as in
  * ComputeExtendedDataSquare).  Enqueued on `stream` (a hipStream_t of this
- * library's HIP runtime; NULL = the context stream); asynchronous.  Squares with
- * k = 128 (one or a batch) run both passes as ONE queue-driven launch; its
- * bounded waits cannot time out short of a hardware fault, and if one did, the
- * stream's next rsm_stream_check (rsm_sync for the context stream), its
- * rsm_stream_destroy or the next extension on that stream returns RSM_EDEVICE. */
+ * library's HIP runtime; NULL = the context stream); asynchronous.  With
+ * 65 <= k <= 128, batches of more than rsm_ctx_set_split_max squares run both passes
+ * as ONE queue-driven launch, smaller batches (a single square included) as two
+ * latency-form launches over every CU.  The queue launch's bounded waits cannot time
+ * out short of a hardware fault, and if one did, the stream's next rsm_stream_check
+ * (rsm_sync for the context stream), its rsm_stream_destroy or the next extension on
+ * that stream returns RSM_EDEVICE. */
 int rsm_extend_squares_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size, uint32_t count,
                            void* stream);
 /* One phase of the above: phase 1 = row pass (Q0 -> Q1), phase 2 = column pass

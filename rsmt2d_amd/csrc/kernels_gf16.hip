@@ -220,6 +220,11 @@ struct Enc16 {
     CodewordSet cs;
     const PermTab16* tw;  // skewperm: twiddle table by skew index (zero where skipped)
     uint32_t chunks;
+    // merged middle pair: the top IFFT layer (SKEW[m - 1 + m/2]) and the top FFT layer
+    // (SKEW[m/2 - 1]) join the same pairs, so they run as ONE multiply by the sum of
+    // the two twiddles: y ^= x; x ^= y * (t1 + t2); y ^= x (nullptr: the sum is 0 and
+    // the pair is the identity).  Table from the host (run_encode).
+    const PermTab16* mid;
 };
 
 constexpr int ilog2c(int x) { return x <= 1 ? 0 : 1 + ilog2c(x / 2); }
@@ -368,8 +373,8 @@ __device__ __forceinline__ void grp_xform_g(uint32_t (&l)[E], uint32_t (&h)[E], 
 template <int E, int R, bool FFT>
 __device__ __forceinline__ void res_xform_g(uint32_t (&l)[E], uint32_t (&h)[E], const PermTab16* tw, int off) {
     constexpr int LN = ilog2c(R);
-    sfor<LN>([&](auto LGi) {
-        constexpr int L = FFT ? LN - 1 - decltype(LGi)::value : decltype(LGi)::value;
+    sfor<LN - 1>([&](auto LGi) {  // the top layer (dj = R/2) is res_mid
+        constexpr int L = FFT ? LN - 2 - decltype(LGi)::value : decltype(LGi)::value;
         constexpr int dj = 1 << L;
         sfor<R / 2 / dj>([&](auto Bk) {
             constexpr int bl = decltype(Bk)::value * 2 * dj;
@@ -385,14 +390,31 @@ __device__ __forceinline__ void res_xform_g(uint32_t (&l)[E], uint32_t (&h)[E], 
         });
     });
 }
+// The merged top pair of the residue layers (elements E R / 2 = m / 2 apart), see Enc16::mid.
+template <int E, int R>
+__device__ __forceinline__ void res_mid(uint32_t (&l)[E], uint32_t (&h)[E], const PermTab16* mid) {
+    constexpr int dj = R / 2;
+    if (!mid) return;  // y ^= x twice: the identity
+    const PermTab16& t = *mid;
+    sfor<E / R>([&](auto Sx) {
+        sfor<dj>([&](auto Q) {
+            constexpr int i = R * decltype(Sx)::value + decltype(Q)::value;
+            l[i + dj] ^= l[i];
+            h[i + dj] ^= h[i];
+            muladd16(l[i], h[i], l[i + dj], h[i + dj], t);
+            l[i + dj] ^= l[i];
+            h[i + dj] ^= h[i];
+        });
+    });
+}
 // Residue layout: register s*R + j holds element r_s + E j; a layer over j at
 // distance dj joins elements E dj apart (block start E bl): one table per
 // (layer, block) for every residue of every wave.
 template <int E, int R, bool FFT>
 __device__ __forceinline__ void res_xform(uint32_t (&l)[E], uint32_t (&h)[E], const uint32_t* rtab) {
     constexpr int LN = ilog2c(R);
-    sfor<LN>([&](auto LGi) {
-        constexpr int L = FFT ? LN - 1 - decltype(LGi)::value : decltype(LGi)::value;
+    sfor<LN - 1>([&](auto LGi) {  // the top layer (dj = R/2) is res_mid
+        constexpr int L = FFT ? LN - 2 - decltype(LGi)::value : decltype(LGi)::value;
         constexpr int dj = 1 << L;
         sfor<R / 2 / dj>([&](auto Bk) {
             constexpr int block = decltype(Bk)::value;
@@ -485,9 +507,11 @@ __global__ __launch_bounds__(M * 2, M == 256 ? 2 : 4) void enc16_kernel(Enc16 p)
         xch_plane<E, R, true>(h, xch, w, lane);
         if constexpr (LDS_TAB) {
             res_xform<E, R, false>(l, h, rtab);
+            res_mid<E, R>(l, h, p.mid);
             res_xform<E, R, true>(l, h, rtab);
         } else {
             res_xform_g<E, R, false>(l, h, p.tw, M - 1);
+            res_mid<E, R>(l, h, p.mid);
             res_xform_g<E, R, true>(l, h, p.tw, 0);
         }
         xch_plane<E, R, false>(l, xch, w, lane);
@@ -974,7 +998,11 @@ hipError_t run_encode(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st) {
     const uint64_t tasks = (uint64_t)cs.count * chunks;
     if (tasks == 0) return hipSuccess;
     if (tasks >= (1ull << 31)) return hipErrorInvalidValue;
-    Enc16 p{cs, g.skewperm, chunks};
+    // the merged middle pair's twiddle: exp(SKEW[m - 1 + m/2]) + exp(SKEW[m/2 - 1])
+    const Gf16Host& hst = gf16_host();
+    auto elem = [&](uint32_t L) { return L == kMod16 ? 0u : (uint32_t)hst.exp[L]; };
+    const uint32_t sum = elem(hst.skew[M - 1 + M / 2]) ^ elem(hst.skew[M / 2 - 1]);
+    Enc16 p{cs, g.skewperm, chunks, sum ? g.perm + hst.log[sum] : nullptr};
     // m = 256: persistent, one workgroup per CU (its twiddle tables stay in LDS);
     // m = 512: one workgroup per task (measured faster: the 16-wave form leaves no
     // registers for a persistent loop's state)
