@@ -54,6 +54,9 @@ def parse():
     p.add_argument("--no-gf16-repair", action="store_true", help="skip the k=256/512 Repair timings")
     p.add_argument("--no-roots", action="store_true", help="skip the extension + Merkle roots timing")
     p.add_argument("--no-extras", action="store_true", help="skip host-path and Codec-latency lines")
+    p.add_argument("--headline-only", action="store_true",
+                   help="only the headline line (no sub-lines, no CPU baseline): the command the committed "
+                        "rocprofv3 kernel-trace / PMC summaries are taken from")
     p.add_argument("--dist", action="store_true",
                    help="initialise torch.distributed even at N=1 (rehearses the sharded c5 path on one GPU)")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -69,7 +72,11 @@ def parse():
     p.add_argument("--row-grid", type=int, default=224,
                    help="GF(2^8) M=128 with >1 stream: CUs of the row-pass persistent grid (0 = all); the "
                         "remaining CUs run the other stream's column pass (profiles/r01h_grid_ab.txt)")
-    return p.parse_args()
+    a = p.parse_args()
+    a.no_single = a.headline_only
+    if a.headline_only:
+        a.no_cpu_baseline = a.no_c5 = a.no_c3 = a.no_c4 = a.no_gf16_repair = a.no_roots = a.no_extras = True
+    return a
 
 
 def cpu_info():
@@ -714,10 +721,11 @@ def main():
         for st in streams[1:]:
             R._check(L.rsm_stream_sync(st))
 
-    for _ in range(max(1, a.warmup)):
-        step()
+    # the first warmup step, then the correctness gate on its output (the oracle is the
+    # checker only), then the remaining warmup steps: the timed steps follow warm steps
+    # directly (a GPU left idle during the CPU-side gate drops its clocks)
+    step()
     sync_all()
-    # correctness gate on one square before timing (the oracle is the checker only)
     if rank == 0:
         import oracle
         for j in sorted({0, B - 1}):  # first and last square of the batch
@@ -725,6 +733,9 @@ def main():
             want = oracle.extend_square(got[:k, :k].copy(), nthreads=min(16, os.cpu_count() or 1))
             if not np.array_equal(got, want):
                 raise SystemExit("bench: GPU EDS differs from oracle -- refusing to report")
+    for _ in range(max(0, a.warmup - 1)):
+        step()
+    sync_all()
 
     def barrier():
         if dist is not None:
@@ -881,7 +892,7 @@ def main():
         b.free()
     for st in streams[1:]:
         R._check(L.rsm_stream_destroy(ctx, st))
-    if rank == 0 and world == 1 and k == 128:
+    if rank == 0 and world == 1 and k == 128 and not a.no_single:
         out["single_square"] = bench_single_square(local, L, R)
         if not a.no_c4:
             out["c4"] = bench_c4(local, L, R, a.steps)

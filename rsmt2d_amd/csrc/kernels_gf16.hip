@@ -370,11 +370,11 @@ __device__ __forceinline__ void grp_xform_g(uint32_t (&l)[E], uint32_t (&h)[E], 
         });
     });
 }
-template <int E, int R, bool FFT>
+template <int E, int R, bool FFT, bool MERGED = false>
 __device__ __forceinline__ void res_xform_g(uint32_t (&l)[E], uint32_t (&h)[E], const PermTab16* tw, int off) {
-    constexpr int LN = ilog2c(R);
-    sfor<LN - 1>([&](auto LGi) {  // the top layer (dj = R/2) is res_mid
-        constexpr int L = FFT ? LN - 2 - decltype(LGi)::value : decltype(LGi)::value;
+    constexpr int LN = ilog2c(R), NL = MERGED ? LN - 1 : LN;  // MERGED: the top layer is res_mid
+    sfor<NL>([&](auto LGi) {
+        constexpr int L = FFT ? NL - 1 - decltype(LGi)::value : decltype(LGi)::value;
         constexpr int dj = 1 << L;
         sfor<R / 2 / dj>([&](auto Bk) {
             constexpr int bl = decltype(Bk)::value * 2 * dj;
@@ -509,9 +509,8 @@ __global__ __launch_bounds__(M * 2, M == 256 ? 2 : 4) void enc16_kernel(Enc16 p)
             res_xform<E, R, false>(l, h, rtab);
             res_mid<E, R>(l, h, p.mid);
             res_xform<E, R, true>(l, h, rtab);
-        } else {
+        } else {  // m = 512: not merged (its 128-register form spills more with it: c5 0.58 -> 0.70 ms)
             res_xform_g<E, R, false>(l, h, p.tw, M - 1);
-            res_mid<E, R>(l, h, p.mid);
             res_xform_g<E, R, true>(l, h, p.tw, 0);
         }
         xch_plane<E, R, false>(l, xch, w, lane);
