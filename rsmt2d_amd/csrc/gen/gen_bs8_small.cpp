@@ -118,11 +118,85 @@ static void emit_xch(int G) {
            "        }\n}\n", 8 * G, 8 * G);
 }
 
+// Bytes <-> planes transposes of the half-split kernel (round 3q): a ROTATE-and-select
+// network instead of the shift pairs of bs8.hpp transpose8_dev.  The planes only need
+// a common bit layout g(byte) -- every butterfly is bitwise -- not the identity one,
+// so each swap of the 8x8 bit transpose moves ONE register by a rotation (v_alignbit,
+// half rate on gfx950) and takes both outputs from it with two full-rate selects:
+//   'b': r = rotl(b, s); b = M ? a : r; a = M ? r : a
+//   'a': r = rotr(a, s); a = M ? r : b; b = M ? b : r
+// (M: bit t of every byte set, s = 2^t).  The rotations leave plane p offset by a
+// per-plane constant; five fix-up rotations align the planes (the minimum over the
+// stage orders and per-pair choices: searched with a bit-label model, kTpFix below).
+// Per 8 registers: 17 half-rate + 24 full-rate instructions against 20 + 28 for the
+// shift form (16 % fewer VALU cycles).  g: byte b of register r -> bit (8b + r + 1) % 32.
+// The inverse runs the steps backwards (same count), so planes -> bytes restores the
+// exact byte order the stores need.
+static const int kTpFix[8] = {1, 0, 0, 31, 0, 31, 29, 28};     // rotl per plane after the stages
+static void tp_ops(bool inverse, const int (&w)[8], int tmp0, int tmp1, int mF0, int mCC, int mAA,
+                   std::vector<std::string>& out) {
+    static const int pairs[3][4][2] = {{{0, 1}, {2, 3}, {4, 5}, {6, 7}},
+                                       {{0, 2}, {1, 3}, {4, 6}, {5, 7}},
+                                       {{0, 4}, {1, 5}, {2, 6}, {3, 7}}};
+    const char* cfg[3] = {"baab", "bbaa", "bbbb"};  // t = 0, 1, 2
+    const int mask[3] = {mAA, mCC, mF0};
+    char b[128];
+    auto rot = [&](int d, int x, int rotr_amount) {  // d = rotr(x, amount)
+        snprintf(b, sizeof b, "v_alignbit_b32 %%%d, %%%d, %%%d, %d", d, x, x, rotr_amount & 31);
+        out.push_back(b);
+    };
+    auto sel = [&](int d, int m, int x, int y) {  // d = m ? x : y
+        snprintf(b, sizeof b, "v_bitop3_b32 %%%d, %%%d, %%%d, %%%d bitop3:0xd8", d, y, x, m);
+        out.push_back(b);
+    };
+    if (inverse)
+        for (int p = 0; p < 8; ++p)
+            if (kTpFix[p]) rot(w[p], w[p], kTpFix[p]);
+    for (int si = 0; si < 3; ++si) {
+        const int t = inverse ? si : 2 - si, s = 1 << t, M = mask[t];
+        for (int q = 0; q < 4; q += 2) {  // two swaps interleaved (independent instructions)
+            int tmp[2] = {tmp0, tmp1};
+            std::vector<std::string> st[2];
+            for (int h = 0; h < 2; ++h) {
+                const int a = w[pairs[t][q + h][0]], bb = w[pairs[t][q + h][1]], r = tmp[h];
+                const bool cb = cfg[t][q + h] == 'b';
+                std::vector<std::string> o;
+                std::swap(o, out);
+                if (!inverse) {
+                    if (cb) { rot(r, bb, 32 - s); sel(bb, M, a, r); sel(a, M, r, a); }
+                    else { rot(r, a, s); sel(a, M, r, bb); sel(bb, M, bb, r); }
+                } else {
+                    if (cb) { sel(r, M, a, bb); sel(a, M, bb, a); rot(bb, r, s); }
+                    else { sel(r, M, a, bb); sel(bb, M, bb, a); rot(a, r, 32 - s); }
+                }
+                std::swap(o, out);
+                st[h] = o;
+            }
+            for (int i = 0; i < 3; ++i) out.push_back(st[0][i]), out.push_back(st[1][i]);
+        }
+    }
+    if (!inverse)
+        for (int p = 0; p < 8; ++p)
+            if (kTpFix[p]) rot(w[p], w[p], 32 - kTpFix[p]);
+}
+// standalone tp_fwd_dev / tp_inv_dev (one symbol's 8 registers): %0..%7 w, %8 %9
+// temporaries, %10..%12 the masks 0xF0F0F0F0, 0xCCCCCCCC, 0xAAAAAAAA (SGPRs)
+static void emit_tp(const char* name, bool inverse) {
+    std::vector<std::string> ops;
+    const int w[8] = {0, 1, 2, 3, 4, 5, 6, 7};
+    tp_ops(inverse, w, 8, 9, 10, 11, 12, ops);
+    printf("RSM_BS8_DEV void %s(uint32_t (&w)[8]) {\n    uint32_t t0, t1;\n    asm volatile(\n", name);
+    for (size_t i = 0; i < ops.size(); ++i) printf("        \"%s%s\"\n", ops[i].c_str(), i + 1 < ops.size() ? "\\n\\t" : "");
+    printf("        : \"+v\"(w[0]), \"+v\"(w[1]), \"+v\"(w[2]), \"+v\"(w[3]), \"+v\"(w[4]), \"+v\"(w[5]), \"+v\"(w[6]), "
+           "\"+v\"(w[7]),\n          \"=&v\"(t0), \"=&v\"(t1)\n"
+           "        : \"s\"(0xF0F0F0F0u), \"s\"(0xCCCCCCCCu), \"s\"(0xAAAAAAAAu));\n}\n");
+}
+
 // Interleaved phases of the half-split schedule: the 64 exchange writes of half W
 // (ds_write_b32, entries as in emit_xch) spread evenly through the VALU work of the
 // OTHER half, so the LDS takes the writes while the SIMDs compute (a separate asm
 // block of 64 writes stalls the wave until the LDS has accepted them).  VALU work:
-//   kind 0: planes <-> bytes transposes of registers 8(1-W) .. 8(1-W)+7 (transpose8_dev);
+//   kind 0 / 3: bytes -> planes / planes -> bytes of registers 8(1-W) .. 8(1-W)+7 (tp_ops);
 //   kind 1: large IFFT of half 1-W (bs8.hpp large_ifft_h);  kind 2: large FFT of half 1-W.
 // Operands: %0..%127 X[j][i] (8j + i), %128..%131 temporaries, %132..%137 the transpose
 // masks (SGPRs), %138 / %139 the write addresses (p < 4 / p >= 4).
@@ -137,8 +211,16 @@ static void emit_phase(const char* name, int W, int kind) {
             wr.push_back(b);
         }
     auto reg = [](int j, int i) { return 8 * j + i; };
-    if (kind == 0) {
-        // transpose8_dev, same instruction sequence (bs8.hpp)
+    if (kind == 0 || kind == 3) {
+        // bytes -> planes (kind 0) / planes -> bytes (kind 3): the rotate-and-select
+        // network of tp_ops, one symbol after the other
+        for (int j = 8 * V; j < 8 * V + 8; ++j) {
+            const int w[8] = {reg(j, 0), reg(j, 1), reg(j, 2), reg(j, 3), reg(j, 4), reg(j, 5), reg(j, 6), reg(j, 7)};
+            tp_ops(kind == 3, w, 128, 129, 133, 135, 137, valu);
+        }
+    } else if (kind == 4) {
+        // transpose8_dev, same instruction sequence (bs8.hpp): the round-3 shift form, an
+        // involution, kept for the diagnostic A/B (bs_split_wave bit 8388608)
         struct G { int a0, b0, a1, b1, s, m, mh; };
         const G gs[6] = {{0, 4, 1, 5, 4, 132, 133}, {2, 6, 3, 7, 4, 132, 133}, {0, 2, 1, 3, 2, 134, 135},
                          {4, 6, 5, 7, 2, 134, 135}, {0, 1, 2, 3, 1, 136, 137}, {4, 5, 6, 7, 1, 136, 137}};
@@ -206,7 +288,13 @@ int main() {
     emit_phase("ph_w0_tr1", 0, 0);    // S' -> L half 0  || transposes of h1 (bytes -> planes)
     emit_phase("ph_w1_lifft0", 1, 1); // S' -> L half 1  || large IFFT of h0
     emit_phase("ph_w0_lfft1", 0, 2);  // L -> S' half 0  || large FFT of h1
-    emit_phase("ph_w1_tr0", 1, 0);    // L -> S' half 1  || transposes of h0 (planes -> bytes)
+    emit_phase("ph_w1_tr0", 1, 3);    // L -> S' half 1  || transposes of h0 (planes -> bytes)
+    printf("#ifdef RSM_DIAG\n");
+    emit_phase("ph_w0_tr1_old", 0, 4);
+    emit_phase("ph_w1_tr0_old", 1, 4);
+    printf("#endif\n");
+    emit_tp("tp_fwd_dev", false);
+    emit_tp("tp_inv_dev", true);
     emit("small_ifft_all", true);
     emit("small_fft_all", false);
     emit_half("small_ifft_h0_all", true, 0);

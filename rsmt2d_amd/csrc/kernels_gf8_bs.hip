@@ -874,13 +874,14 @@ __device__ __forceinline__ void split_direct_h0(const CodewordSet& cs, const Set
     });
 }
 // planes -> bytes and the 16 stores of half G (Q1 write-through, Q2/Q3 non-temporal)
-template <int G, bool TRP, bool MEM_ON>
+template <int G, bool TRP, bool MEM_ON, bool OLDTP = false>
 __device__ __forceinline__ void split_store_h(uint32_t (&X)[16][8], const SetAddr& a, uint32_t A, uint32_t k,
                                               uint32_t oo, uint32_t es, bool row, bool mem) {
     const __amdgpu_buffer_rsrc_t ro = as_rsrc(a.ro);
     bs8::sfor<8>([&](auto J) {
         constexpr int j = 8 * G + decltype(J)::value;
-        if constexpr (TRP) bs8::transpose8_dev(X[j]);
+        if constexpr (TRP && OLDTP) bs8::transpose8_dev(X[j]);
+        else if constexpr (TRP) bs8::tp_inv_dev(X[j]);  // planes (layout of gen_bs8_small tp_ops) -> bytes
         const uint32_t so = sym_off(e_split(A, j), k, oo, es);
         v4u x, y;
         x.x = X[j][0]; x.y = X[j][1]; x.z = X[j][2]; x.w = X[j][3];
@@ -940,6 +941,13 @@ __device__ __forceinline__ void bs_split_wave(const QueuePlan& p, uint32_t* lds,
     // signalling lane before each row set's counter add -- measures what the release
     // would cost on top of the write-through (sc1) Q1 stores the hand-off relies on
     constexpr bool REL = (MODE & 4194304) != 0;
+    // 8388608: the round-3 shift-pair transposes (bs8.hpp transpose8_dev) instead of the
+    // rotate-and-select network (gen_bs8_small.cpp tp_ops) -- A/B
+    constexpr bool OLDTP = (MODE & 8388608) != 0;
+    auto tp_fwd = [](uint32_t (&w)[8]) {
+        if constexpr (OLDTP) bs8::transpose8_dev(w);
+        else bs8::tp_fwd_dev(w);
+    };
     auto release = [&]() {
         if constexpr (REL) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -1057,7 +1065,7 @@ __device__ __forceinline__ void bs_split_wave(const QueuePlan& p, uint32_t* lds,
             // no claim in a workgroup's last set (nothing would take the item)
             if (t0) cand = more ? q_claim(p, qc) : kNone;
             if constexpr (ARITH) {
-                bs8::sfor<8>([&](auto J) { bs8::transpose8_dev(X[decltype(J)::value]); });
+                bs8::sfor<8>([&](auto J) { tp_fwd(X[decltype(J)::value]); });
                 bs8::small_ifft_h0_all(X, A);
             }
             if constexpr (XLOAD) {
@@ -1095,12 +1103,16 @@ __device__ __forceinline__ void bs_split_wave(const QueuePlan& p, uint32_t* lds,
             stamp(1);
             // ---- S' -> L, half 0 || small layers of h1 ----
             if constexpr (IL) {
+#ifdef RSM_DIAG
+                if constexpr (OLDTP) bs8::ph_w0_tr1_old(X, xw, xw + 65536u);
+                else
+#endif
                 bs8::ph_w0_tr1(X, xw, xw + 65536u);
                 bs8::small_ifft_h1_all(X, A);
             } else {
                 if constexpr (XCH) bs8::xch_write_h0(X, xw, xw + 65536u);
                 if constexpr (ARITH) {
-                    bs8::sfor<8>([&](auto J) { bs8::transpose8_dev(X[8 + decltype(J)::value]); });
+                    bs8::sfor<8>([&](auto J) { tp_fwd(X[8 + decltype(J)::value]); });
                     bs8::small_ifft_h1_all(X, A);
                 }
             }
@@ -1217,6 +1229,10 @@ __device__ __forceinline__ void bs_split_wave(const QueuePlan& p, uint32_t* lds,
             const uint32_t es = (uint32_t)(crow ? p.rows.elem_stride : p.cols.elem_stride);
             if constexpr (IL) {
                 bs8::small_fft_h0_all(X, A);
+#ifdef RSM_DIAG
+                if constexpr (OLDTP) bs8::ph_w1_tr0_old(X, xw, xw + 65536u);
+                else
+#endif
                 bs8::ph_w1_tr0(X, xw, xw + 65536u);  // + planes -> bytes of h0
                 split_store_h<0, false, true>(X, a, A, k, oo, es, crow != 0, MEM);
                 if constexpr (XLOAD) {
@@ -1230,7 +1246,7 @@ __device__ __forceinline__ void bs_split_wave(const QueuePlan& p, uint32_t* lds,
                 if constexpr (XCH) bs8::xch_write_h1(X, xw, xw + 65536u);
                 if constexpr (!LATE0) {
                     if constexpr (ARITH) bs8::small_fft_h0_all(X, A);
-                    split_store_h<0, ARITH, true>(X, a, A, k, oo, es, crow != 0, MEM);
+                    split_store_h<0, ARITH, true, OLDTP>(X, a, A, k, oo, es, crow != 0, MEM);
                 }
             }
             RSM_LDS_SYNC;
@@ -1249,11 +1265,11 @@ __device__ __forceinline__ void bs_split_wave(const QueuePlan& p, uint32_t* lds,
             }
             if constexpr (LATE0) {
                 if constexpr (ARITH) bs8::small_fft_h0_all(X, A);
-                split_store_h<0, ARITH, true>(X, a, A, k, oo, es, crow != 0, MEM);
+                split_store_h<0, ARITH, true, OLDTP>(X, a, A, k, oo, es, crow != 0, MEM);
             }
             stamp(9);
             if constexpr (ARITH) bs8::small_fft_h1_all(X, A);
-            split_store_h<1, ARITH, true>(X, a, A, k, oo, es, crow != 0, MEM);
+            split_store_h<1, ARITH, true, OLDTP>(X, a, A, k, oo, es, crow != 0, MEM);
             stamp(10);
             if constexpr (TRACE) if (threadIdx.x == 0) trace_stamp(p, it_no, 11, (crow ? 1u : 0u) | ((cur & kQ1) ? 2u : 0u) | (pre ? 0u : 4u));
             ++it_no;
@@ -1579,6 +1595,7 @@ hipError_t launch_extend_gf8_bs128_queue(const QueuePlan& p0, hipStream_t st) {
         case 51012: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<524290>), dim3(grid), dim3(512), 0, st, p); break;
         case 51004: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<262148>), dim3(grid), dim3(512), 0, st, p); break;
         case 52040: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<4194304>), dim3(grid), dim3(512), 0, st, p); break;
+        case 53000: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<8388608>), dim3(grid), dim3(512), 0, st, p); break;
         case 51006: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<262146>), dim3(grid), dim3(512), 0, st, p); break;
         // round-2 schedule (bs_queue_wave) for A/B
         case 18472: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<18472>), dim3(grid), dim3(512), 0, st, p); break;

@@ -140,3 +140,107 @@ def test_half_split_small_layer_blocks(gf, name, inverse, G):
                                                            ref[b + q], ref[b + q + d], mul)
         for j in range(8):
             assert unplanes(regs[8 * j:8 * j + 8]).tobytes() == ref[j].tobytes(), (name, A, j)
+
+
+# --- bytes <-> planes transposes of the half-split kernel (gen_bs8_small.cpp tp_ops) ---
+GEN = re.compile(r'"(v_alignbit_b32|v_bitop3_b32|v_xor_b32) %(\d+), %(\d+), %(\d+)(?:, (?:%(\d+)|(\d+)))?'
+                 r'(?: bitop3:(0x[0-9a-f]+))?')
+M32 = 0xFFFFFFFF
+
+
+def run_valu(text, regs):
+    """Execute the VALU text of a generated block (v_alignbit_b32, v_bitop3_b32 XOR3 /
+    select, v_xor_b32) on a register dict; LDS instructions are skipped."""
+    n = 0
+    for m in GEN.finditer(text):
+        op, d, a, b = m.group(1), int(m.group(2)), int(m.group(3)), int(m.group(4))
+        if op == "v_alignbit_b32":
+            regs[d] = (((regs[a] << 32) | regs[b]) >> int(m.group(6))) & M32
+        elif op == "v_xor_b32":
+            regs[d] = regs[a] ^ regs[b]
+        else:
+            c = regs[int(m.group(5))]
+            if m.group(7) == "0x96":
+                regs[d] = regs[a] ^ regs[b] ^ c
+            else:
+                assert m.group(7) == "0xd8", m.group(0)
+                regs[d] = (regs[b] & c) | (regs[a] & ~c & M32)  # S2 ? S1 : S0
+        n += 1
+    return n
+
+
+def layout_of(fwd_words):
+    """Bit position of byte (r, b) in the planes, from single-byte probes; None if the
+    planes do not share one layout."""
+    pos = {}
+    for r in range(8):
+        for b in range(4):
+            w = [0] * 8
+            w[r] = 0xFF << (8 * b)
+            out = fwd_words(w)
+            bits = {o.bit_length() - 1 for o in out}
+            if any(bin(o).count("1") != 1 for o in out) or len(bits) != 1:
+                return None
+            pos[(r, b)] = bits.pop()
+    return pos
+
+
+@pytest.fixture(scope="module")
+def small_text():
+    return open(os.path.join(CSRC, "bs8_small.inc")).read()
+
+
+def block(text, name):
+    return re.search(r"void %s\(.*?\{(.*?)\n\}" % name, text, re.S).group(1)
+
+
+def tp_fn(text, name):
+    body = block(text, name)
+    masks = {10: 0xF0F0F0F0, 11: 0xCCCCCCCC, 12: 0xAAAAAAAA}
+
+    def f(w):
+        regs = dict(enumerate(w))
+        regs.update({8: 0xDEADBEEF, 9: 0x12345678})
+        regs.update(masks)
+        run_valu(body, regs)
+        return [regs[i] for i in range(8)]
+    return f, body
+
+
+def test_transposes_share_one_layout_and_invert(small_text):
+    fwd, fb = tp_fn(small_text, "tp_fwd_dev")
+    inv, ib = tp_fn(small_text, "tp_inv_dev")
+    # 12 rotations + 5 fix-ups + 24 selects each way
+    assert fb.count("v_alignbit_b32") == 17 and fb.count("bitop3:0xd8") == 24
+    assert ib.count("v_alignbit_b32") == 17 and ib.count("bitop3:0xd8") == 24
+    pos = layout_of(fwd)
+    assert pos is not None and sorted(pos.values()) == list(range(32))
+    rng = np.random.default_rng(11)
+    for _ in range(64):
+        w = [int(x) for x in rng.integers(0, 2**32, 8, dtype=np.uint64)]
+        planes_ = fwd(w)
+        for (r, b), x in pos.items():
+            byte = (w[r] >> (8 * b)) & 0xFF
+            for p in range(8):
+                assert (planes_[p] >> x) & 1 == (byte >> p) & 1
+        assert inv(planes_) == w
+
+
+@pytest.mark.parametrize("name,V,inverse", [("ph_w0_tr1", 1, False), ("ph_w1_tr0", 0, True)])
+def test_phase_transposes(small_text, name, V, inverse):
+    """The transposes interleaved with the exchange writes of the other half."""
+    body = block(small_text, name)
+    fwd, _ = tp_fn(small_text, "tp_fwd_dev")
+    inv, _ = tp_fn(small_text, "tp_inv_dev")
+    rng = np.random.default_rng(12)
+    X = [int(x) for x in rng.integers(0, 2**32, 128, dtype=np.uint64)]
+    regs = dict(enumerate(X))
+    regs.update({128: 1, 129: 2, 130: 3, 131: 4, 132: 0x0F0F0F0F, 133: 0xF0F0F0F0, 134: 0x33333333,
+                 135: 0xCCCCCCCC, 136: 0x55555555, 137: 0xAAAAAAAA})
+    assert run_valu(body, regs) == 8 * 41
+    for j in range(16):
+        got = [regs[8 * j + i] for i in range(8)]
+        want = X[8 * j:8 * j + 8]
+        if j // 8 == V:
+            want = (inv if inverse else fwd)(want)
+        assert got == want, (name, j)
