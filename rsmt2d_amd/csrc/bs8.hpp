@@ -61,7 +61,7 @@ RSM_BS8_DEV void mid2_asm(uint32_t (&x)[8], uint32_t (&y)[8]);
 #include "bs8_net.inc"
 template <unsigned L>
 inline void muladd_host(uint32_t (&x)[8], const uint32_t (&y)[8]) {
-    uint32_t r[19] = {};
+    uint32_t r[24] = {};  // x, y, up to 8 temporaries
     for (int i = 0; i < 8; ++i) r[i] = x[i], r[8 + i] = y[i];
     for (int n = 0; n < kNetLen[L]; ++n) {
         const NetOp& o = kNet[L][n];

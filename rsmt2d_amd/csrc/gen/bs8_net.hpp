@@ -13,12 +13,14 @@
 #include <cstdint>
 #include <cstdio>
 #include <string>
+#include <algorithm>
+#include <set>
 #include <vector>
 #include "../gf_tables.hpp"
 
 namespace rsm::gen {
 
-// register codes: 0..7 x planes, 8..15 y planes, 16..18 temporaries
+// register codes: 0..7 x planes, 8..15 y planes, 16..21 temporaries
 enum OpKind : uint8_t { kXor2 = 0, kXor3 = 1, kSet2 = 2, kSet3 = 3 };
 struct Op {
     uint8_t kind, dst, a, b, c;
@@ -66,7 +68,7 @@ inline int direct_cost(unsigned L) {
 
 // x_i ^= (M_L y)_i as an op list: temporaries first, then step-major over the
 // output planes (consecutive instructions independent).  Memoised per L.
-inline const std::vector<Op>& mul_network(unsigned L) {
+inline const std::vector<Op>& mul_network_v1(unsigned L) {
     static std::vector<Op> memo[256];
     static bool done[256] = {};
     if (done[L]) return memo[L];
@@ -137,6 +139,143 @@ inline const std::vector<Op>& mul_network(unsigned L) {
     return ops;
 }
 
+// Round-3 search (beam over chained temporaries): a temporary is ANY mask one 2- or
+// 3-input XOR of the items already available (the y planes and earlier temporaries)
+// can make, and a row is the shortest XOR of items equal to it (cancellation allowed),
+// costing ceil(items / 2) accumulating 3-input XORs.  Beam of 24 over up to kMaxTemps
+// temporaries; the v1 network is kept where it is not beaten.
+constexpr int kMaxTemps = 6;
+struct ItemDist {
+    uint8_t d[256];
+    uint8_t prev[256], item[256];
+};
+inline void item_dist(const unsigned* items, int n, ItemDist& t) {
+    for (int m = 0; m < 256; ++m) t.d[m] = 255;
+    t.d[0] = 0;
+    uint8_t front[256], nf[256];
+    int nfr = 1, lvl = 0;
+    front[0] = 0;
+    while (nfr) {
+        ++lvl;
+        int nn = 0;
+        for (int f = 0; f < nfr; ++f)
+            for (int i = 0; i < n; ++i) {
+                const unsigned x = front[f] ^ items[i];
+                if (t.d[x] == 255) {
+                    t.d[x] = (uint8_t)lvl;
+                    t.prev[x] = front[f];
+                    t.item[x] = (uint8_t)i;
+                    nf[nn++] = (uint8_t)x;
+                }
+            }
+        for (int i = 0; i < nn; ++i) front[i] = nf[i];
+        nfr = nn;
+    }
+}
+inline int net_cost(const unsigned (&rows)[8], const std::vector<unsigned>& temps, ItemDist& t, int ne = 0) {
+    unsigned items[8 + kMaxTemps];
+    int n = 0;
+    for (int j = 0; j < 8; ++j) items[n++] = 1u << j;
+    for (unsigned m : temps) items[n++] = m;
+    item_dist(items, n, t);
+    int c = (int)temps.size();
+    for (int i = 0; i < 8; ++i) c += (t.d[rows[i]] + ne + 1) / 2;
+    return c;
+}
+inline std::vector<unsigned> beam_temps(const unsigned (&rows)[8], int* cost_out, int ne = 0) {
+    struct St {
+        int c;
+        std::vector<unsigned> t;
+    };
+    ItemDist td;
+    std::vector<St> states{{net_cost(rows, {}, td, ne), {}}};
+    St best = states[0];
+    for (int depth = 0; depth < kMaxTemps; ++depth) {
+        std::vector<St> cand;
+        std::set<std::vector<unsigned>> seen;
+        for (const St& s : states) {
+            unsigned items[8 + kMaxTemps];
+            int n = 0;
+            for (int j = 0; j < 8; ++j) items[n++] = 1u << j;
+            for (unsigned m : s.t) items[n++] = m;
+            ItemDist d;
+            item_dist(items, n, d);
+            for (unsigned m = 1; m < 256; ++m) {
+                if (d.d[m] != 2 && d.d[m] != 3) continue;
+                std::vector<unsigned> nt = s.t;
+                nt.push_back(m);
+                std::vector<unsigned> key = nt;
+                std::sort(key.begin(), key.end());
+                if (!seen.insert(key).second) continue;
+                cand.push_back(St{net_cost(rows, nt, td, ne), nt});
+            }
+        }
+        if (cand.empty()) break;
+        std::stable_sort(cand.begin(), cand.end(), [](const St& a, const St& b) { return a.c < b.c; });
+        if (cand.size() > 24) cand.resize(24);
+        states = cand;
+        if (states[0].c < best.c) best = states[0];
+    }
+    *cost_out = best.c;
+    return best.t;
+}
+// x_i ^= (M_L y)_i ^ e0_i ^ ... (ne extra symbols folded in by the block optimizer
+// below; extra symbol k, plane i has register code 24 + 8k + i).  ne = 0: the plain
+// multiply network (the v1 network where the beam does not beat it).
+inline const std::vector<Op>& mul_network_ex(unsigned L, int ne) {
+    static std::vector<Op> memo[3][256];
+    static bool done[3][256] = {};
+    if (done[ne][L]) return memo[ne][L];
+    done[ne][L] = true;
+    unsigned rows[8];
+    matrix_rows(L, rows);
+    int c2 = 0;
+    const std::vector<unsigned> temps = beam_temps(rows, &c2, ne);
+    if (ne == 0) {
+        const std::vector<Op>& v1 = mul_network_v1(L);
+        if ((int)v1.size() <= c2) return memo[ne][L] = v1;
+    }
+    std::vector<Op>& ops = memo[ne][L];
+    unsigned items[8 + kMaxTemps];
+    uint8_t code[8 + kMaxTemps];
+    int n = 0;
+    for (int j = 0; j < 8; ++j) items[n] = 1u << j, code[n++] = (uint8_t)(8 + j);
+    auto rep = [&](unsigned m, int nitems) {  // shortest item list for m over items[0..nitems)
+        ItemDist d;
+        item_dist(items, nitems, d);
+        std::vector<uint8_t> r;
+        for (unsigned x = m; x; x = d.prev[x]) r.push_back(code[d.item[x]]);
+        return r;
+    };
+    for (size_t i = 0; i < temps.size(); ++i) {
+        const std::vector<uint8_t> r = rep(temps[i], n);
+        const uint8_t dst = (uint8_t)(16 + i);
+        ops.push_back(r.size() == 2 ? Op{kSet2, dst, r[0], r[1], 0} : Op{kSet3, dst, r[0], r[1], r[2]});
+        items[n] = temps[i], code[n++] = dst;
+    }
+    std::vector<std::vector<uint8_t>> terms(8);
+    for (int i = 0; i < 8; ++i) {
+        terms[i] = rep(rows[i], n);
+        for (int k = 0; k < ne; ++k) terms[i].push_back((uint8_t)(24 + 8 * k + i));
+    }
+    for (unsigned step = 0; step < 8; ++step)
+        for (unsigned i = 0; i < 8; ++i) {
+            const auto& t = terms[i];
+            if (2 * step + 1 < t.size()) ops.push_back(Op{kXor3, (uint8_t)i, t[2 * step], t[2 * step + 1], 0});
+            else if (2 * step < t.size()) ops.push_back(Op{kXor2, (uint8_t)i, t[2 * step], 0, 0});
+        }
+    return ops;
+}
+inline const std::vector<Op>& mul_network(unsigned L) { return mul_network_ex(L, 0); }
+
+// number of temporaries an op list writes (codes 16..)
+inline int temps_used(const std::vector<Op>& ops) {
+    int n = 0;
+    for (const Op& o : ops)
+        if (o.dst >= 16 && o.dst - 15 > n) n = o.dst - 15;
+    return n;
+}
+
 // Whole butterflies (kind 0 IFFT_DIT2, 1 FFT_DIT2, 2 MID):
 //   IFFT: y ^= x; x ^= M y.      FFT: x ^= M y; y ^= x.
 //   MID : y ^= x; x ^= M y; y ^= x -- the encoder's last IFFT layer directly followed
@@ -177,6 +316,130 @@ inline std::string op_asm(const Op& o, F&& map) {
             break;
     }
     return b;
+}
+
+// ---------------------------------------------------------------------------
+// Block optimizer (round 3q): a block of butterflies (one asm statement) as a list of
+// symbol-level ops, ADD (d ^= a, 8 XORs) and MULACC (d ^= M_L a, a network), where
+// two rewrites fold an ADD into a neighbouring network's rows (an extra term per row:
+// ceil((terms + 1) / 2) instead of ceil(terms / 2) + 1 instructions):
+//   forward  MULACC(x, y) ... ADD(x, z)  ->  MULACC(x, y; +z)   (IFFT: the next layer's
+//            y ^= x on this x-output; z not written, x not read in between)
+//   backward ADD(y, x) ... MULACC(y, w)  ->  MULACC(y, w; +x)   (FFT: y ^= x deferred
+//            into the next layer's accumulate on y; x not written, y not read between)
+// and two ADDs into one register with nothing in between touching them become one
+// 3-input XOR per plane.
+struct IrOp {
+    int kind;  // 0 ADD d ^= a (+ b if b >= 0: 3-input), 1 MULACC d ^= M_L a (+ extras)
+    int d, a, b;
+    unsigned L;
+    std::vector<int> ex;
+};
+inline void ir_butterfly(std::vector<IrOp>& ir, int kind, unsigned L, int x, int y) {
+    auto add = [&] { ir.push_back(IrOp{0, y, x, -1, 0, {}}); };
+    if (kind != 1) add();
+    if (L != 255u) ir.push_back(IrOp{1, x, y, -1, L, {}});
+    if (kind != 0) add();
+}
+inline bool ir_reads(const IrOp& o, int r) {
+    if (o.a == r || o.b == r || o.d == r) return true;  // d is read too (accumulate)
+    for (int e : o.ex) if (e == r) return true;
+    return false;
+}
+inline bool ir_writes(const IrOp& o, int r) { return o.d == r; }
+inline void ir_optimize(std::vector<IrOp>& ir) {
+    bool changed = true;
+    while (changed) {
+        changed = false;
+        for (size_t i = 0; i < ir.size() && !changed; ++i) {
+            IrOp& o = ir[i];
+            if (o.kind == 1 && o.ex.size() < 2) {  // forward fold of a later ADD(d, z)
+                for (size_t j = i + 1; j < ir.size(); ++j) {
+                    const IrOp& q = ir[j];
+                    if (q.kind == 0 && q.d == o.d && q.b < 0) {
+                        bool ok = true;
+                        for (size_t m = i + 1; m < j && ok; ++m)
+                            if (ir_reads(ir[m], o.d) || ir_writes(ir[m], q.a)) ok = false;
+                        if (ok) {
+                            o.ex.push_back(q.a);
+                            ir.erase(ir.begin() + (long)j);
+                            changed = true;
+                        }
+                        break;
+                    }
+                    if (ir_reads(q, o.d)) break;
+                }
+            }
+            if (changed) break;
+            if (o.kind == 0 && o.b < 0) {  // backward: defer into a later MULACC on d
+                for (size_t j = i + 1; j < ir.size(); ++j) {
+                    IrOp& q = ir[j];
+                    if (q.kind == 1 && q.d == o.d && q.ex.size() < 2) {
+                        bool ok = true;
+                        for (size_t m = i + 1; m < j && ok; ++m)
+                            if (ir_reads(ir[m], o.d) || ir_writes(ir[m], o.a)) ok = false;
+                        if (ok && q.a != o.d) {
+                            q.ex.push_back(o.a);
+                            ir.erase(ir.begin() + (long)i);
+                            changed = true;
+                        }
+                        break;
+                    }
+                    if (ir_reads(q, o.d)) {
+                        // two ADDs into d with nothing else between: one 3-input XOR
+                        if (q.kind == 0 && q.d == o.d && q.b < 0) {
+                            bool ok = true;
+                            for (size_t m = i + 1; m < j && ok; ++m)
+                                if (ir_writes(ir[m], o.a) || ir_writes(ir[m], q.a)) ok = false;
+                            if (ok) {
+                                q.b = o.a;
+                                ir.erase(ir.begin() + (long)i);
+                                changed = true;
+                            }
+                        }
+                        break;
+                    }
+                }
+            }
+        }
+    }
+}
+// asm text of an optimized block; plane(sym, i) gives the operand of plane i of a
+// symbol, temporaries are operands tbase...
+template <typename F>
+inline void ir_emit(const std::vector<IrOp>& ir, F&& plane, int tbase, std::vector<std::string>& out) {
+    char b[128];
+    for (const IrOp& o : ir) {
+        if (o.kind == 0) {
+            for (int i = 0; i < 8; ++i) {
+                if (o.b < 0) snprintf(b, sizeof b, "v_xor_b32 %%%d, %%%d, %%%d", plane(o.d, i), plane(o.d, i), plane(o.a, i));
+                else
+                    snprintf(b, sizeof b, "v_bitop3_b32 %%%d, %%%d, %%%d, %%%d bitop3:0x96", plane(o.d, i), plane(o.d, i),
+                             plane(o.a, i), plane(o.b, i));
+                out.push_back(b);
+            }
+            continue;
+        }
+        auto map = [&](int c) {
+            return c < 8 ? plane(o.d, c) : c < 16 ? plane(o.a, c - 8) : c < 24 ? tbase + (c - 16) : plane(o.ex[(c - 24) / 8], (c - 24) % 8);
+        };
+        for (const Op& n : mul_network_ex(o.L, (int)o.ex.size())) out.push_back(op_asm(n, map));
+    }
+}
+inline int ir_temps(const std::vector<IrOp>& ir) {
+    int n = 0;
+    for (const IrOp& o : ir)
+        if (o.kind == 1) {
+            const auto& ops = mul_network_ex(o.L, (int)o.ex.size());
+            for (const Op& q : ops)
+                if (q.dst >= 16 && q.dst - 15 > n) n = q.dst - 15;
+        }
+    return n;
+}
+inline int ir_count(const std::vector<IrOp>& ir) {
+    int n = 0;
+    for (const IrOp& o : ir) n += o.kind == 0 ? 8 : (int)mul_network_ex(o.L, (int)o.ex.size()).size();
+    return n;
 }
 
 }  // namespace rsm::gen

@@ -7,6 +7,7 @@
 // overflow the instruction cache: measured 1.8x slower).  The butterflies are the
 // networks of bs8_net.hpp (the ones bs8_asm.inc and bs8_net.inc hold).
 // Operands: %0..%127 = X[j][i] (operand 8j + i), %128..%130 temporaries, %131 = A (SGPR).
+#include <algorithm>
 #include <cstdio>
 #include <string>
 #include <vector>
@@ -15,28 +16,59 @@
 using namespace rsm;
 using namespace rsm::gen;
 
-static void butterfly(int kind, unsigned L, int xs, int ys, std::vector<std::string>& out) {
-    auto map = [&](int c) { return c < 8 ? 8 * xs + c : c < 16 ? 8 * ys + (c - 8) : 128 + (c - 16); };
-    for (const Op& o : butterfly_ops(kind, L)) out.push_back(op_asm(o, map));
+// temporaries a list of butterflies needs (the most any one network uses)
+struct Bfly {
+    int kind;
+    unsigned L;
+    int xs, ys;
+};
+static int temps_of(const std::vector<Bfly>& bs) {
+    int n = 0;
+    for (const Bfly& b : bs) n = std::max(n, temps_used(butterfly_ops(b.kind, b.L)));
+    return n;
+}
+static void bfly_asm(const Bfly& b, int tbase, std::vector<std::string>& out, int regs_per_sym = 8, int sym0 = 0) {
+    auto map = [&](int c) {
+        return c < 8 ? regs_per_sym * (b.xs - sym0) + c : c < 16 ? regs_per_sym * (b.ys - sym0) + (c - 8) : tbase + (c - 16);
+    };
+    for (const Op& o : butterfly_ops(b.kind, b.L)) out.push_back(op_asm(o, map));
+}
+static void print_temps_decl(int nt) {
+    printf("    uint32_t");
+    for (int t = 0; t < nt; ++t) printf("%s t%d", t ? "," : "", t);
+    printf(";\n");
+}
+static void print_temps_ops(int nt) {  // the last operands of the output list (nt >= 1)
+    for (int t = 0; t < nt; ++t) printf(" \"=&v\"(t%d)%s", t, t + 1 < nt ? "," : "");
 }
 
-static void emit(const char* name, bool ifft) {
+static std::vector<Bfly> small_list(bool ifft, int a) {
     const int kOffEnc = 127;
-    printf("RSM_BS8_DEV void %s(uint32_t (&X)[16][8], uint32_t A) {\n    uint32_t t0, t1, t2;\n    asm volatile(\n",
-           name);
-    for (int a = 0; a < 7; ++a) printf("        \"s_cmp_eq_u32 %%131, %d\\n\\ts_cbranch_scc1 .L%s%d_%%=\\n\\t\"\n", a, name, a);
+    std::vector<Bfly> bs;
+    if (ifft) {
+        for (int d = 1; d <= 4; d <<= 1)
+            for (int b = 0; b < 16; b += 2 * d)
+                for (int q = 0; q < d; ++q) bs.push_back({0, kGf8.skew[kOffEnc + 16 * a + b + d], b + q, b + q + d});
+    } else {
+        for (int d = 4; d >= 1; d >>= 1)
+            for (int b = 0; b < 16; b += 2 * d)
+                for (int q = 0; q < d; ++q) bs.push_back({1, kGf8.skew[-1 + 16 * a + b + d], b + q, b + q + d});
+    }
+    return bs;
+}
+// operands: %0..%127 X, %128.. temporaries, then A
+static void emit(const char* name, bool ifft) {
+    int nt = 1;
+    for (int a = 0; a < 8; ++a) nt = std::max(nt, temps_of(small_list(ifft, a)));
+    const int opA = 128 + nt;
+    printf("RSM_BS8_DEV void %s(uint32_t (&X)[16][8], uint32_t A) {\n", name);
+    print_temps_decl(nt);
+    printf("    asm volatile(\n");
+    for (int a = 0; a < 7; ++a) printf("        \"s_cmp_eq_u32 %%%d, %d\\n\\ts_cbranch_scc1 .L%s%d_%%=\\n\\t\"\n", opA, a, name, a);
     printf("        \"s_branch .L%s7_%%=\\n\\t\"\n", name);
     for (int a = 0; a < 8; ++a) {
         std::vector<std::string> ins;
-        if (ifft) {
-            for (int d = 1; d <= 4; d <<= 1)
-                for (int b = 0; b < 16; b += 2 * d)
-                    for (int q = 0; q < d; ++q) butterfly(0, kGf8.skew[kOffEnc + 16 * a + b + d], b + q, b + q + d, ins);
-        } else {
-            for (int d = 4; d >= 1; d >>= 1)
-                for (int b = 0; b < 16; b += 2 * d)
-                    for (int q = 0; q < d; ++q) butterfly(1, kGf8.skew[-1 + 16 * a + b + d], b + q, b + q + d, ins);
-        }
+        for (const Bfly& b : small_list(ifft, a)) bfly_asm(b, 128, ins);
         printf("        \".L%s%d_%%=:\\n\\t\"\n", name, a);
         for (const auto& s : ins) printf("        \"%s\\n\\t\"\n", s.c_str());
         if (a < 7) printf("        \"s_branch .L%send_%%=\\n\\t\"\n", name);
@@ -44,33 +76,73 @@ static void emit(const char* name, bool ifft) {
     printf("        \".L%send_%%=:\"\n        :", name);
     for (int j = 0; j < 16; ++j)
         for (int i = 0; i < 8; ++i) printf(" \"+v\"(X[%d][%d]),", j, i);
-    printf(" \"=&v\"(t0), \"=&v\"(t1), \"=&v\"(t2)\n        : \"s\"(A) : \"scc\");\n}\n");
+    print_temps_ops(nt);
+    printf("\n        : \"s\"(A) : \"scc\");\n}\n");
 }
 
 // Half-split schedule (bs8.hpp small_ifft_h / small_fft_h): the small layers of ONE
 // half G in layout S' (register j of wave A holds e = (j & 7) + 8A + 64 (j >> 3)),
 // operands %0..%63 = X[8G + b][i] (operand 8b + i), %64..%66 temporaries, %67 = A.
-static void emit_half(const char* name, bool ifft, int G) {
+static std::vector<Bfly> half_list(bool ifft, int G, int a) {
     const int kOffEnc = 127;
-    printf("RSM_BS8_DEV void %s(uint32_t (&X)[16][8], uint32_t A) {\n    uint32_t t0, t1, t2;\n    asm volatile(\n",
-           name);
-    for (int a = 0; a < 7; ++a) printf("        \"s_cmp_eq_u32 %%67, %d\\n\\ts_cbranch_scc1 .L%s%d_%%=\\n\\t\"\n", a, name, a);
+    std::vector<Bfly> bs;
+    if (ifft) {
+        for (int d = 1; d <= 4; d <<= 1)
+            for (int b = 0; b < 8; b += 2 * d)
+                for (int q = 0; q < d; ++q) bs.push_back({0, kGf8.skew[kOffEnc + 8 * a + 64 * G + b + d], b + q, b + q + d});
+    } else {
+        for (int d = 4; d >= 1; d >>= 1)
+            for (int b = 0; b < 8; b += 2 * d)
+                for (int q = 0; q < d; ++q) bs.push_back({1, kGf8.skew[-1 + 8 * a + 64 * G + b + d], b + q, b + q + d});
+    }
+    return bs;
+}
+// A list of butterflies as the block optimizer's ops (gen/bs8_net.hpp ir_optimize):
+// IFFT layers in ascending index order (a network's next-layer y ^= x folds forward),
+// FFT layers in descending order (a y ^= x is deferred into the next layer's
+// accumulate on y before its partner is rewritten).
+static std::vector<IrOp> block_ir(const std::vector<std::vector<Bfly>>& layers) {
+    std::vector<IrOp> ir;
+    for (const auto& layer : layers) {
+        const bool fft = !layer.empty() && layer[0].kind == 1;
+        if (fft)
+            for (auto it = layer.rbegin(); it != layer.rend(); ++it) ir_butterfly(ir, it->kind, it->L, it->xs, it->ys);
+        else
+            for (const Bfly& b : layer) ir_butterfly(ir, b.kind, b.L, b.xs, b.ys);
+    }
+    ir_optimize(ir);
+    return ir;
+}
+static std::vector<std::vector<Bfly>> by_layer(const std::vector<Bfly>& bs, int per_layer) {
+    std::vector<std::vector<Bfly>> L;
+    for (size_t i = 0; i < bs.size(); i += per_layer) L.emplace_back(bs.begin() + (long)i, bs.begin() + (long)(i + per_layer));
+    return L;
+}
+static long g_plain = 0, g_opt = 0;  // VALU count of the optimized blocks vs butterfly by butterfly
+static std::vector<IrOp> opt_block(const std::vector<Bfly>& bs, int per_layer) {
+    std::vector<IrOp> ir = block_ir(by_layer(bs, per_layer));
+    for (const Bfly& b : bs) g_plain += (long)butterfly_ops(b.kind, b.L).size();
+    g_opt += ir_count(ir);
+    return ir;
+}
+
+// operands: %0..%63 = X[8G + b][i] (operand 8b + i), %64.. temporaries, then A
+static void emit_half(const char* name, bool ifft, int G) {
+    std::vector<std::vector<IrOp>> irs;
+    int nt = 1;
+    for (int a = 0; a < 8; ++a) {
+        irs.push_back(opt_block(half_list(ifft, G, a), 4));
+        nt = std::max(nt, ir_temps(irs.back()));
+    }
+    const int opA = 64 + nt;
+    printf("RSM_BS8_DEV void %s(uint32_t (&X)[16][8], uint32_t A) {\n", name);
+    print_temps_decl(nt);
+    printf("    asm volatile(\n");
+    for (int a = 0; a < 7; ++a) printf("        \"s_cmp_eq_u32 %%%d, %d\\n\\ts_cbranch_scc1 .L%s%d_%%=\\n\\t\"\n", opA, a, name, a);
     printf("        \"s_branch .L%s7_%%=\\n\\t\"\n", name);
-    auto bfly = [&](int kind, unsigned L, int xs, int ys, std::vector<std::string>& out) {
-        auto map = [&](int c) { return c < 8 ? 8 * xs + c : c < 16 ? 8 * ys + (c - 8) : 64 + (c - 16); };
-        for (const Op& o : butterfly_ops(kind, L)) out.push_back(op_asm(o, map));
-    };
     for (int a = 0; a < 8; ++a) {
         std::vector<std::string> ins;
-        if (ifft) {
-            for (int d = 1; d <= 4; d <<= 1)
-                for (int b = 0; b < 8; b += 2 * d)
-                    for (int q = 0; q < d; ++q) bfly(0, kGf8.skew[kOffEnc + 8 * a + 64 * G + b + d], b + q, b + q + d, ins);
-        } else {
-            for (int d = 4; d >= 1; d >>= 1)
-                for (int b = 0; b < 8; b += 2 * d)
-                    for (int q = 0; q < d; ++q) bfly(1, kGf8.skew[-1 + 8 * a + 64 * G + b + d], b + q, b + q + d, ins);
-        }
+        ir_emit(irs[a], [](int sym, int i) { return 8 * sym + i; }, 64, ins);
         printf("        \".L%s%d_%%=:\\n\\t\"\n", name, a);
         for (const auto& s : ins) printf("        \"%s\\n\\t\"\n", s.c_str());
         if (a < 7) printf("        \"s_branch .L%send_%%=\\n\\t\"\n", name);
@@ -78,7 +150,55 @@ static void emit_half(const char* name, bool ifft, int G) {
     printf("        \".L%send_%%=:\"\n        :", name);
     for (int j = 8 * G; j < 8 * G + 8; ++j)
         for (int i = 0; i < 8; ++i) printf(" \"+v\"(X[%d][%d]),", j, i);
-    printf(" \"=&v\"(t0), \"=&v\"(t1), \"=&v\"(t2)\n        : \"s\"(A) : \"scc\");\n}\n");
+    print_temps_ops(nt);
+    printf("\n        : \"s\"(A) : \"scc\");\n}\n");
+}
+
+// Large layers of half 1, the merged middle pair and the large layers of half 0 (the
+// work between the second exchange read and the third exchange, bs8.hpp
+// large_ifft_h<1> + large_mid + large_fft_h<0>) as ONE optimized block: %0..%127 X,
+// %128.. temporaries.
+static void emit_lmid(const char* name) {
+    const int kOffEnc = 127;
+    auto e = [](unsigned L) { return L == 255u ? 0u : (unsigned)kGf8.exp[L]; };
+    const unsigned sum = e(kGf8.skew[kOffEnc + 64]) ^ e(kGf8.skew[63]);
+    const unsigned mid = sum == 0 ? 255u : (unsigned)kGf8.log[sum];
+    std::vector<std::vector<Bfly>> layers;
+    for (int dh = 1; dh <= 4; dh <<= 1) {  // IFFT d = 8, 16, 32 on h in [8, 16)
+        std::vector<Bfly> l;
+        for (int bb = 0; bb < 8; bb += 2 * dh) {
+            const int hb = 8 + bb;
+            for (int q = 0; q < dh; ++q) l.push_back({0, kGf8.skew[kOffEnc + 8 * hb + 8 * dh], hb + q, hb + q + dh});
+        }
+        layers.push_back(l);
+    }
+    {
+        std::vector<Bfly> l;
+        for (int q = 0; q < 8; ++q) l.push_back({2, mid, q, q + 8});
+        layers.push_back(l);
+    }
+    for (int dh = 4; dh >= 1; dh >>= 1) {  // FFT d = 32, 16, 8 on h in [0, 8)
+        std::vector<Bfly> l;
+        for (int bb = 0; bb < 8; bb += 2 * dh)
+            for (int q = 0; q < dh; ++q) l.push_back({1, kGf8.skew[-1 + 8 * bb + 8 * dh], bb + q, bb + q + dh});
+        layers.push_back(l);
+    }
+    std::vector<IrOp> ir = block_ir(layers);
+    for (const auto& l : layers)
+        for (const Bfly& b : l) g_plain += (long)butterfly_ops(b.kind, b.L).size();
+    g_opt += ir_count(ir);
+    const int nt = std::max(1, ir_temps(ir));
+    std::vector<std::string> ins;
+    ir_emit(ir, [](int sym, int i) { return 8 * sym + i; }, 128, ins);
+    printf("RSM_BS8_DEV void %s(uint32_t (&X)[16][8]) {\n", name);
+    print_temps_decl(nt);
+    printf("    asm volatile(\n");
+    for (size_t i = 0; i < ins.size(); ++i) printf("        \"%s%s\"\n", ins[i].c_str(), i + 1 < ins.size() ? "\\n\\t" : "");
+    printf("        :");
+    for (int j = 0; j < 16; ++j)
+        for (int i = 0; i < 8; ++i) printf(" \"+v\"(X[%d][%d]),", j, i);
+    print_temps_ops(nt);
+    printf(");\n}\n");
 }
 
 // Half-split exchange (kernels_gf8_bs.hip, bs_split_wave): half G is a transpose,
@@ -203,27 +323,45 @@ static void emit_tp(const char* name, bool inverse) {
 static void emit_phase(const char* name, int W, int kind) {
     const int V = 1 - W;
     std::vector<std::string> valu, wr;
+    auto reg = [](int j, int i) { return 8 * j + i; };
+    // temporaries: 2 for tp_ops, 4 for the shift form, the networks' need for butterflies
+    std::vector<Bfly> bs;
+    if (kind == 1 || kind == 2) {
+        const int kOffEnc = 127;
+        for (int li = 0; li < 3; ++li) {
+            const int dh = kind == 1 ? (1 << li) : (4 >> li);
+            for (int bb = 0; bb < 8; bb += 2 * dh) {
+                const int hb = 8 * V + bb;
+                const unsigned L = kind == 1 ? kGf8.skew[kOffEnc + 8 * hb + 8 * dh] : kGf8.skew[-1 + 8 * hb + 8 * dh];
+                for (int q = 0; q < dh; ++q) bs.push_back({kind == 1 ? 0 : 1, L, hb + q, hb + q + dh});
+            }
+        }
+    }
+    std::vector<IrOp> ir;
+    if (kind == 1 || kind == 2) ir = opt_block(bs, 4);
+    const int nt = kind == 4 ? 4 : (kind == 0 || kind == 3) ? 2 : std::max(1, ir_temps(ir));
+    const int mk = 128 + nt;      // masks 0x0F.., 0xF0.., 0x33.., 0xCC.., 0x55.., 0xAA.. at mk .. mk + 5
+    const int va = mk + 6, vb = mk + 7;
     for (int p = 0; p < 8; ++p)
         for (int v = 0; v < 8; ++v) {
             char b[96];
-            snprintf(b, sizeof b, "ds_write_b32 %%%d, %%%d offset:%d", wr_hi(p) ? 139 : 138, 8 * (8 * W + v) + p,
+            snprintf(b, sizeof b, "ds_write_b32 %%%d, %%%d offset:%d", wr_hi(p) ? vb : va, 8 * (8 * W + v) + p,
                      wr_off(p, v));
             wr.push_back(b);
         }
-    auto reg = [](int j, int i) { return 8 * j + i; };
     if (kind == 0 || kind == 3) {
         // bytes -> planes (kind 0) / planes -> bytes (kind 3): the rotate-and-select
         // network of tp_ops, one symbol after the other
         for (int j = 8 * V; j < 8 * V + 8; ++j) {
             const int w[8] = {reg(j, 0), reg(j, 1), reg(j, 2), reg(j, 3), reg(j, 4), reg(j, 5), reg(j, 6), reg(j, 7)};
-            tp_ops(kind == 3, w, 128, 129, 133, 135, 137, valu);
+            tp_ops(kind == 3, w, 128, 129, mk + 1, mk + 3, mk + 5, valu);
         }
     } else if (kind == 4) {
         // transpose8_dev, same instruction sequence (bs8.hpp): the round-3 shift form, an
         // involution, kept for the diagnostic A/B (bs_split_wave bit 8388608)
         struct G { int a0, b0, a1, b1, s, m, mh; };
-        const G gs[6] = {{0, 4, 1, 5, 4, 132, 133}, {2, 6, 3, 7, 4, 132, 133}, {0, 2, 1, 3, 2, 134, 135},
-                         {4, 6, 5, 7, 2, 134, 135}, {0, 1, 2, 3, 1, 136, 137}, {4, 5, 6, 7, 1, 136, 137}};
+        const G gs[6] = {{0, 4, 1, 5, 4, mk, mk + 1}, {2, 6, 3, 7, 4, mk, mk + 1}, {0, 2, 1, 3, 2, mk + 2, mk + 3},
+                         {4, 6, 5, 7, 2, mk + 2, mk + 3}, {0, 1, 2, 3, 1, mk + 4, mk + 5}, {4, 5, 6, 7, 1, mk + 4, mk + 5}};
         for (int j = 8 * V; j < 8 * V + 8; ++j)
             for (const G& g : gs) {
                 char b[128];
@@ -248,22 +386,11 @@ static void emit_phase(const char* name, int W, int kind) {
                 valu.push_back(b);
             }
     } else {
-        const int kOffEnc = 127;
-        auto bfly = [&](int bk, unsigned L, int xs, int ys) {
-            auto map = [&](int c) { return c < 8 ? reg(xs, c) : c < 16 ? reg(ys, c - 8) : 128 + (c - 16); };
-            for (const Op& o : butterfly_ops(bk, L)) valu.push_back(op_asm(o, map));
-        };
-        for (int li = 0; li < 3; ++li) {
-            const int dh = kind == 1 ? (1 << li) : (4 >> li);
-            for (int bb = 0; bb < 8; bb += 2 * dh) {
-                const int hb = 8 * V + bb;
-                const unsigned L = kind == 1 ? kGf8.skew[kOffEnc + 8 * hb + 8 * dh] : kGf8.skew[-1 + 8 * hb + 8 * dh];
-                for (int q = 0; q < dh; ++q) bfly(kind == 1 ? 0 : 1, L, hb + q, hb + q + dh);
-            }
-        }
+        ir_emit(ir, [](int sym, int i) { return 8 * sym + i; }, 128, valu);
     }
-    printf("RSM_BS8_DEV void %s(uint32_t (&X)[16][8], uint32_t va, uint32_t vb) {\n"
-           "    uint32_t t0, t1, t2, t3;\n    asm volatile(\n", name);
+    printf("RSM_BS8_DEV void %s(uint32_t (&X)[16][8], uint32_t va, uint32_t vb) {\n", name);
+    print_temps_decl(nt);
+    printf("    asm volatile(\n");
     const size_t n = valu.size();
     size_t w = 0;
     for (size_t i = 0; i < n; ++i) {
@@ -275,8 +402,8 @@ static void emit_phase(const char* name, int W, int kind) {
     printf("        \"s_nop 0\"\n        :");
     for (int j = 0; j < 16; ++j)
         for (int i = 0; i < 8; ++i) printf(" \"+v\"(X[%d][%d]),", j, i);
-    printf(" \"=&v\"(t0), \"=&v\"(t1), \"=&v\"(t2), \"=&v\"(t3)\n"
-           "        : \"s\"(0x0F0F0F0Fu), \"s\"(0xF0F0F0F0u), \"s\"(0x33333333u), \"s\"(0xCCCCCCCCu), "
+    for (int t = 0; t < nt; ++t) printf(" \"=&v\"(t%d)%s", t, t + 1 < nt ? "," : "");
+    printf("\n        : \"s\"(0x0F0F0F0Fu), \"s\"(0xF0F0F0F0u), \"s\"(0x33333333u), \"s\"(0xCCCCCCCCu), "
            "\"s\"(0x55555555u), \"s\"(0xAAAAAAAAu), \"v\"(va), \"v\"(vb) : \"memory\");\n}\n");
 }
 
@@ -293,6 +420,7 @@ int main() {
     emit_phase("ph_w0_tr1_old", 0, 4);
     emit_phase("ph_w1_tr0_old", 1, 4);
     printf("#endif\n");
+    emit_lmid("lmid_all");
     emit_tp("tp_fwd_dev", false);
     emit_tp("tp_inv_dev", true);
     emit("small_ifft_all", true);
@@ -301,5 +429,6 @@ int main() {
     emit_half("small_ifft_h1_all", true, 1);
     emit_half("small_fft_h0_all", false, 0);
     emit_half("small_fft_h1_all", false, 1);
+    fprintf(stderr, "half-split blocks: %ld VALU butterfly by butterfly, %ld optimized\n", g_plain, g_opt);
     return 0;
 }

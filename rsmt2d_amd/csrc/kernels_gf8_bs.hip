@@ -1136,11 +1136,8 @@ __device__ __forceinline__ void bs_split_wave(const QueuePlan& p, uint32_t* lds,
             asm volatile("s_barrier" ::: "memory");
             stamp(5);
             if constexpr (TRACE) if (threadIdx.x == 0) trace_stamp(p, it_no, 12, (uint32_t)__builtin_amdgcn_s_memtime());
-            if constexpr (ARITH) {
-                bs8::large_ifft_h<1>(X);
-                bs8::large_mid(X);
-                bs8::large_fft_h<0>(X);
-            }
+            // large IFFT h1, middle pair, large FFT h0: one block (gen_bs8_small.cpp emit_lmid)
+            if constexpr (ARITH) bs8::lmid_all(X);
             if constexpr (TRACE) if (threadIdx.x == 0) trace_stamp(p, it_no, 13, (uint32_t)__builtin_amdgcn_s_memtime());
             stamp(6);
             // publish the row set stored at the end of the previous set: ops issued

@@ -81,7 +81,7 @@ def test_butterfly_blocks(gf, name):
         L = int(L)
         x = rng.integers(0, 256, 32, dtype=np.uint8)
         y = rng.integers(0, 256, 32, dtype=np.uint8)
-        regs = planes(x) + planes(y) + [int(v) for v in rng.integers(0, 2**32, 3)]  # garbage temporaries
+        regs = planes(x) + planes(y) + [int(v) for v in rng.integers(0, 2**32, 8)]  # garbage temporaries
         execute(parse(body), regs)
         wx, wy = butterfly(name, L, x, y, mul)
         assert unplanes(regs[:8]).tobytes() == wx.tobytes(), (name, L)
@@ -100,7 +100,7 @@ def test_small_layer_blocks(gf, name, inverse):
     rng = np.random.default_rng(9)
     for A, body in bodies.items():
         sym = [rng.integers(0, 256, 32, dtype=np.uint8) for _ in range(16)]
-        regs = sum((planes(s) for s in sym), []) + [int(v) for v in rng.integers(0, 2**32, 3)]
+        regs = sum((planes(s) for s in sym), []) + [int(v) for v in rng.integers(0, 2**32, 8)]
         execute(parse(body), regs)
         ref = [s.copy() for s in sym]
         for d in ((1, 2, 4) if inverse else (4, 2, 1)):
@@ -128,7 +128,7 @@ def test_half_split_small_layer_blocks(gf, name, inverse, G):
     rng = np.random.default_rng(10 + G)
     for A, body in bodies.items():
         sym = [rng.integers(0, 256, 32, dtype=np.uint8) for _ in range(8)]
-        regs = sum((planes(s) for s in sym), []) + [int(v) for v in rng.integers(0, 2**32, 3)]
+        regs = sum((planes(s) for s in sym), []) + [int(v) for v in rng.integers(0, 2**32, 8)]
         execute(parse(body), regs)
         ref = [s.copy() for s in sym]
         for d in ((1, 2, 4) if inverse else (4, 2, 1)):
@@ -226,6 +226,39 @@ def test_transposes_share_one_layout_and_invert(small_text):
         assert inv(planes_) == w
 
 
+def phase_operands(body):
+    """Temporaries (garbage) and the six SGPR masks of a generated phase block (the
+    masks follow the block's temporaries, gen_bs8_small.cpp emit_phase)."""
+    nt = len(re.findall(r'"=&v"\(t\d+\)', body))
+    regs = {128 + t: 0x9E3779B9 * (t + 1) & M32 for t in range(nt)}
+    for i, m in enumerate((0x0F0F0F0F, 0xF0F0F0F0, 0x33333333, 0xCCCCCCCC, 0x55555555, 0xAAAAAAAA)):
+        regs[128 + nt + i] = m
+    return regs
+
+
+@pytest.mark.parametrize("name,V,kind", [("ph_w1_lifft0", 0, "ifft2_asm"), ("ph_w0_lfft1", 1, "fft2_asm")])
+def test_phase_large_layers(gf, small_text, name, V, kind):
+    """The large IFFT / FFT layers of one half (layout L: register h of wave g holds
+    e = g + 8h; d = 8h-strides 1, 2, 4 within the half, bs8.hpp large_ifft_h/large_fft_h),
+    interleaved with the other half's exchange writes."""
+    mul, skew = gf
+    body = block(small_text, name)
+    rng = np.random.default_rng(13 + V)
+    sym = [rng.integers(0, 256, 32, dtype=np.uint8) for _ in range(16)]
+    regs = dict(enumerate(sum((planes(x) for x in sym), [])))
+    regs.update(phase_operands(body))
+    run_valu(body, regs)
+    ref = [x.copy() for x in sym]
+    for dh in ((1, 2, 4) if kind == "ifft2_asm" else (4, 2, 1)):
+        for bb in range(0, 8, 2 * dh):
+            hb = 8 * V + bb
+            L = skew[127 + 8 * hb + 8 * dh] if kind == "ifft2_asm" else skew[-1 + 8 * hb + 8 * dh]
+            for q in range(dh):
+                ref[hb + q], ref[hb + q + dh] = butterfly(kind, L, ref[hb + q], ref[hb + q + dh], mul)
+    for j in range(16):
+        assert unplanes([regs[8 * j + i] for i in range(8)]).tobytes() == ref[j].tobytes(), (name, j)
+
+
 @pytest.mark.parametrize("name,V,inverse", [("ph_w0_tr1", 1, False), ("ph_w1_tr0", 0, True)])
 def test_phase_transposes(small_text, name, V, inverse):
     """The transposes interleaved with the exchange writes of the other half."""
@@ -235,8 +268,7 @@ def test_phase_transposes(small_text, name, V, inverse):
     rng = np.random.default_rng(12)
     X = [int(x) for x in rng.integers(0, 2**32, 128, dtype=np.uint64)]
     regs = dict(enumerate(X))
-    regs.update({128: 1, 129: 2, 130: 3, 131: 4, 132: 0x0F0F0F0F, 133: 0xF0F0F0F0, 134: 0x33333333,
-                 135: 0xCCCCCCCC, 136: 0x55555555, 137: 0xAAAAAAAA})
+    regs.update(phase_operands(body))
     assert run_valu(body, regs) == 8 * 41
     for j in range(16):
         got = [regs[8 * j + i] for i in range(8)]
@@ -244,3 +276,35 @@ def test_phase_transposes(small_text, name, V, inverse):
         if j // 8 == V:
             want = (inv if inverse else fwd)(want)
         assert got == want, (name, j)
+
+
+def test_lmid_block(gf, small_text):
+    """Large IFFT of half 1, the merged middle pair, large FFT of half 0 (bs8.hpp
+    large_ifft_h<1> + large_mid + large_fft_h<0>) as one optimized block."""
+    mul, skew = gf
+    body = block(small_text, "lmid_all")
+    rng = np.random.default_rng(14)
+    sym = [rng.integers(0, 256, 32, dtype=np.uint8) for _ in range(16)]
+    regs = dict(enumerate(sum((planes(x) for x in sym), [])))
+    regs.update({128 + t: (0x9E3779B9 * (t + 1)) & M32 for t in range(8)})
+    run_valu(body, regs)
+    ref = [x.copy() for x in sym]
+    for dh in (1, 2, 4):
+        for bb in range(0, 8, 2 * dh):
+            hb = 8 + bb
+            for q in range(dh):
+                ref[hb + q], ref[hb + q + dh] = butterfly("ifft2_asm", skew[127 + 8 * hb + 8 * dh], ref[hb + q],
+                                                          ref[hb + q + dh], mul)
+    exp, log, _, _ = oracle.tables8()
+    e = lambda L: 0 if L == 255 else int(exp[L])
+    s = e(skew[127 + 64]) ^ e(skew[63])
+    mid = 255 if s == 0 else int(log[s])
+    for q in range(8):
+        ref[q], ref[q + 8] = butterfly("mid2_asm", mid, ref[q], ref[q + 8], mul)
+    for dh in (4, 2, 1):
+        for bb in range(0, 8, 2 * dh):
+            for q in range(dh):
+                ref[bb + q], ref[bb + q + dh] = butterfly("fft2_asm", skew[-1 + 8 * bb + 8 * dh], ref[bb + q],
+                                                          ref[bb + q + dh], mul)
+    for j in range(16):
+        assert unplanes([regs[8 * j + i] for i in range(8)]).tobytes() == ref[j].tobytes(), j
