@@ -145,6 +145,7 @@ inline const std::vector<Op>& mul_network_v1(unsigned L) {
 // costing ceil(items / 2) accumulating 3-input XORs.  Beam of 24 over up to kMaxTemps
 // temporaries; the v1 network is kept where it is not beaten.
 constexpr int kMaxTemps = 6;
+inline int g_beam = 24;  // beam width (the generators keep the default)
 struct ItemDist {
     uint8_t d[256];
     uint8_t prev[256], item[256];
@@ -212,7 +213,7 @@ inline std::vector<unsigned> beam_temps(const unsigned (&rows)[8], int* cost_out
         }
         if (cand.empty()) break;
         std::stable_sort(cand.begin(), cand.end(), [](const St& a, const St& b) { return a.c < b.c; });
-        if (cand.size() > 24) cand.resize(24);
+        if (cand.size() > (size_t)g_beam) cand.resize((size_t)g_beam);
         states = cand;
         if (states[0].c < best.c) best = states[0];
     }

@@ -1581,6 +1581,7 @@ hipError_t launch_extend_gf8_bs128_queue(const QueuePlan& p0, hipStream_t st) {
         case 50004: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<4>), dim3(grid), dim3(512), 0, st, p); break;
         case 50768: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<32768>), dim3(grid), dim3(512), 0, st, p); break;
         case 50772: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<32772>), dim3(grid), dim3(512), 0, st, p); break;
+        case 50770: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<32770>), dim3(grid), dim3(512), 0, st, p); break;
         case 51000: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<65536>), dim3(grid), dim3(512), 0, st, p); break;
         case 51001: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<131072>), dim3(grid), dim3(512), 0, st, p); break;
         case 51002: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<262144>), dim3(grid), dim3(512), 0, st, p); break;

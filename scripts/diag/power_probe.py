@@ -3,7 +3,9 @@ diagnostic mode (40 production, 50002 memory-only, 50004 compute-only) a child p
 runs scripts/diag/queue_ab.py with many steps while this process samples
 `rocm-smi --showpower --showclocks --json` (a sysfs read, no GPU work); prints the
 median power / sclk / mclk over the samples taken while the child ran.
-usage: python3 scripts/diag/power_probe.py [steps]
+usage: python3 scripts/diag/power_probe.py [steps] [mode[:steps] ...]
+(modes: 40 production, 50002 no arithmetic, 50004 no global memory, 50768 no LDS exchange,
+50772 arithmetic only, 50770 global memory only; per-mode steps so each runs ~10 s)
 """
 import json
 import os
@@ -39,14 +41,15 @@ def sample():
     return out
 
 
-def main(steps):
+def main(steps, modes=("40", "50002", "50004")):
     raw = subprocess.run(["rocm-smi", "--showpower", "--showclocks", "--json"], capture_output=True, text=True,
                          timeout=20).stdout
     print(json.dumps({"rocm_smi_raw": raw[:1500]}), flush=True)
     idle = [s for s in (sample() for _ in range(3)) if s]
     print(json.dumps({"mode": "idle", "samples": idle}), flush=True)
-    for mode in ("40", "50002", "50004"):
-        env = dict(os.environ, QAB_STEPS=str(steps))
+    for m in modes:
+        mode, _, st = m.partition(":")
+        env = dict(os.environ, QAB_STEPS=st or str(steps))
         child = subprocess.Popen([sys.executable, os.path.join(HERE, "queue_ab.py"), f"queue,256,3,2,{mode}"],
                                  env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
         time.sleep(4.0)  # context creation, buffers, warmup
@@ -67,4 +70,4 @@ def main(steps):
 
 
 if __name__ == "__main__":
-    main(int(sys.argv[1]) if len(sys.argv) > 1 else 3000)
+    main(int(sys.argv[1]) if len(sys.argv) > 1 else 3000, tuple(sys.argv[2:]) or ("40", "50002", "50004"))

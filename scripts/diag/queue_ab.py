@@ -95,7 +95,7 @@ def run(cfg, steps=STEPS, warmup=6):
     ok = True
     # diagnostic modes whose output is wrong by design (no arithmetic / memory / exchange)
     WRONG = {"2", "4", "32768", "65536", "131072", "98304", "32772", "50002", "50004", "50768", "50772",
-             "51004", "51006", "51012", "51014"}
+             "51004", "51006", "51012", "51014", "50770"}
     if mode in WRONG or (kind == "two" and mode != "40"):
         ok = None  # diagnostic mode: output wrong by design, not checked
     elif kind == "queue":
