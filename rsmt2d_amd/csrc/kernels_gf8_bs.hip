@@ -86,6 +86,46 @@ __device__ __forceinline__ SetAddr set_addr(const CodewordSet& cs, uint32_t t, u
     return a;
 }
 
+// Per-lane part of set_addr when it is the same for every set (round 3q): the share
+// size S divides the set width (2048 B), so every set starts at a codeword boundary
+// (r0 = 0) and covers G = 2048 / S whole codewords, and per_square and count are
+// multiples of G, so those G codewords lie in one square.  Lane offsets are then
+// fixed (codeword dq = v / S of the set, byte v % S, v = 1024 h + 16 lane), and a set
+// costs one wave-uniform division instead of four per-lane ones.
+struct LaneGeo {
+    uint32_t off[2];
+    uint32_t shift;  // log2(G)
+};
+__host__ __device__ inline bool lane_geo_ok(const CodewordSet& cs) {
+    const uint32_t S = cs.S;
+    if (S == 0 || kSetBytes % S != 0 || (S & (S - 1)) != 0 || cs.indices != nullptr) return false;
+    const uint32_t G = kSetBytes / S;
+    return cs.per_square % G == 0 && cs.count % G == 0;
+}
+__device__ __forceinline__ LaneGeo lane_geo(const CodewordSet& cs, uint32_t lane) {
+    LaneGeo g{};
+    const uint32_t S = cs.S, G = kSetBytes / S;
+    g.shift = 31u - (uint32_t)__builtin_clz(G);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const uint32_t v = 1024u * h + 16u * lane;
+        const uint32_t dq = v >> (31u - (uint32_t)__builtin_clz(S));
+        g.off[h] = (uint32_t)(dq * cs.cw_stride) + (v & (S - 1u));
+    }
+    return g;
+}
+__device__ __forceinline__ SetAddr set_addr_geo(const CodewordSet& cs, const LaneGeo& g, uint32_t t) {
+    SetAddr a;
+    const uint32_t q0 = t << g.shift;
+    const uint32_t sq0 = __builtin_amdgcn_readfirstlane(q0 / cs.per_square);
+    const uint64_t rel0 = (uint64_t)sq0 * cs.square_stride + (uint64_t)(q0 - sq0 * cs.per_square) * cs.cw_stride;
+    a.off[0] = g.off[0];
+    a.off[1] = g.off[1];
+    a.rs = make_srd(cs.base + rel0);
+    a.ro = make_srd(cs.out_base + rel0);
+    return a;
+}
+
 __device__ __forceinline__ uint32_t sym_off(uint32_t e, uint32_t k, uint32_t base, uint32_t es) {
     return __builtin_amdgcn_readfirstlane(e < k ? base + e * es : kOobBs);
 }
@@ -972,7 +1012,15 @@ __device__ __forceinline__ void bs_split_wave(const QueuePlan& p, uint32_t* lds,
     uint32_t Q[8][8];  // NODMA: h1 of the next set
     QClaim qc;
 
-    auto addr = [&](uint32_t row, uint32_t set) { return set_addr(row ? p.rows : p.cols, set, lane); };
+    // 16777216: fixed per-lane set offsets (the host chose it: lane_geo_ok for rows and
+    // columns -- S divides the 2 KiB set width, the production c2 shape)
+    constexpr bool GEO = (MODE & 16777216) != 0;
+    LaneGeo geo_r{}, geo_c{};
+    if constexpr (GEO) geo_r = lane_geo(p.rows, lane), geo_c = lane_geo(p.cols, lane);
+    auto addr = [&](uint32_t row, uint32_t set) {
+        if constexpr (GEO) return row ? set_addr_geo(p.rows, geo_r, set) : set_addr_geo(p.cols, geo_c, set);
+        else return set_addr(row ? p.rows : p.cols, set, lane);
+    };
     auto issue_dma = [&](uint32_t row, uint32_t q1, const SetAddr& a) {
         if (!MEM) return;
         if constexpr (NODMA) {
@@ -1567,6 +1615,7 @@ hipError_t launch_extend_gf8_bs128_queue(const QueuePlan& p0, hipStream_t st) {
     if (total == 0) return hipSuccess;
     const uint32_t cap = p.rows.grid ? p.rows.grid : 256u;
     const uint32_t grid = total < cap ? total : cap;
+    const bool geo = lane_geo_ok(p.rows) && lane_geo_ok(p.cols);
 #ifdef RSM_DIAG
     // diagnostic codes: 2 / 4 no arithmetic / no memory (wrong output by design);
     // 104 direct loads right after the first exchange, 140 after the large layers,
@@ -1576,7 +1625,11 @@ hipError_t launch_extend_gf8_bs128_queue(const QueuePlan& p0, hipStream_t st) {
     // the exchange
     switch (g_diag_mode.load()) {
         // half-split schedule (production) and its diagnostic variants
-        case 40: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<0>), dim3(grid), dim3(512), 0, st, p); break;
+        case 40:  // production (as below)
+            if (geo) hipLaunchKernelGGL((extend_gf8_bs128s_kernel<16777216>), dim3(grid), dim3(512), 0, st, p);
+            else hipLaunchKernelGGL((extend_gf8_bs128s_kernel<0>), dim3(grid), dim3(512), 0, st, p);
+            break;
+        case 54000: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<0>), dim3(grid), dim3(512), 0, st, p); break;
         case 50002: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<2>), dim3(grid), dim3(512), 0, st, p); break;
         case 50004: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<4>), dim3(grid), dim3(512), 0, st, p); break;
         case 50768: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<32768>), dim3(grid), dim3(512), 0, st, p); break;
@@ -1613,10 +1666,14 @@ hipError_t launch_extend_gf8_bs128_queue(const QueuePlan& p0, hipStream_t st) {
         case 131072: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<18472 | 131072>), dim3(grid), dim3(512), 0, st, p); break;
         case 98304: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<18472 | 98304>), dim3(grid), dim3(512), 0, st, p); break;
         case 32772: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<18476 | 32768>), dim3(grid), dim3(512), 0, st, p); break;
-        default: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<0>), dim3(grid), dim3(512), 0, st, p); break;
+        default:
+            if (geo) hipLaunchKernelGGL((extend_gf8_bs128s_kernel<16777216>), dim3(grid), dim3(512), 0, st, p);
+            else hipLaunchKernelGGL((extend_gf8_bs128s_kernel<0>), dim3(grid), dim3(512), 0, st, p);
+            break;
     }
 #else
-    hipLaunchKernelGGL((extend_gf8_bs128s_kernel<0>), dim3(grid), dim3(512), 0, st, p);
+    if (geo) hipLaunchKernelGGL((extend_gf8_bs128s_kernel<16777216>), dim3(grid), dim3(512), 0, st, p);
+    else hipLaunchKernelGGL((extend_gf8_bs128s_kernel<0>), dim3(grid), dim3(512), 0, st, p);
 #endif
     return hipGetLastError();
 }

@@ -146,13 +146,14 @@ def test_product_has_no_diagnostics(lib):
     assert not re.search(rb"RSM_[A-Z0-9_]{3,}\x00", blob), re.search(rb"RSM_[A-Z0-9_]{3,}\x00", blob)
     # kernel symbols embedded in the gfx950 code object: only the production modes
     # of the bit-sliced encode (row pass 104, column pass 184, the single-launch
-    # half-split queue extension 0: kernels_gf8_bs.hip), no diagnostic mode (bits
+    # half-split queue extension: 16777216 with fixed per-lane set offsets where S divides
+    # the set width, 0 otherwise -- kernels_gf8_bs.hip), no diagnostic mode (bits
     # 2 / 4 / 32768: no arithmetic / no memory / no exchange), no round-2 queue
     # kernel (diag A/B only), no dual (bs128p) kernel
     modes = set(re.findall(rb"encode_gf8_bs128u_kernelILi(\d+)E", blob))
     assert modes == {b"104", b"184"}, modes
     smodes = set(re.findall(rb"extend_gf8_bs128s_kernelILi(\d+)E", blob))
-    assert smodes == {b"0"}, smodes
+    assert smodes == {b"0", b"16777216"}, smodes
     assert b"extend_gf8_bs128q_kernel" not in blob
     assert not any(int(m) & (6 | 32768) for m in modes | smodes)
     assert b"encode_gf8_bs128p_kernel" not in blob
