@@ -340,8 +340,13 @@ static void emit_phase(const char* name, int W, int kind) {
     std::vector<IrOp> ir;
     if (kind == 1 || kind == 2) ir = opt_block(bs, 4);
     const int nt = kind == 4 ? 4 : (kind == 0 || kind == 3) ? 2 : std::max(1, ir_temps(ir));
-    const int mk = 128 + nt;      // masks 0x0F.., 0xF0.., 0x33.., 0xCC.., 0x55.., 0xAA.. at mk .. mk + 5
-    const int va = mk + 6, vb = mk + 7;
+    // masks: the shift form (kind 4) 0x0F.., 0xF0.., 0x33.., 0xCC.., 0x55.., 0xAA.. at mk .. mk + 5;
+    // the rotate-and-select transposes (kinds 0, 3) only 0xF0.., 0xCC.., 0xAA.. at mk .. mk + 2;
+    // the butterfly phases none (every SGPR a block holds is one the compiler must
+    // otherwise keep elsewhere -- spills to VGPR lanes, reloaded with v_readlane)
+    const int nm = kind == 4 ? 6 : (kind == 0 || kind == 3) ? 3 : 0;
+    const int mk = 128 + nt;
+    const int va = mk + nm, vb = mk + nm + 1;
     for (int p = 0; p < 8; ++p)
         for (int v = 0; v < 8; ++v) {
             char b[96];
@@ -354,7 +359,7 @@ static void emit_phase(const char* name, int W, int kind) {
         // network of tp_ops, one symbol after the other
         for (int j = 8 * V; j < 8 * V + 8; ++j) {
             const int w[8] = {reg(j, 0), reg(j, 1), reg(j, 2), reg(j, 3), reg(j, 4), reg(j, 5), reg(j, 6), reg(j, 7)};
-            tp_ops(kind == 3, w, 128, 129, mk + 1, mk + 3, mk + 5, valu);
+            tp_ops(kind == 3, w, 128, 129, mk, mk + 1, mk + 2, valu);
         }
     } else if (kind == 4) {
         // transpose8_dev, same instruction sequence (bs8.hpp): the round-3 shift form, an
@@ -403,8 +408,13 @@ static void emit_phase(const char* name, int W, int kind) {
     for (int j = 0; j < 16; ++j)
         for (int i = 0; i < 8; ++i) printf(" \"+v\"(X[%d][%d]),", j, i);
     for (int t = 0; t < nt; ++t) printf(" \"=&v\"(t%d)%s", t, t + 1 < nt ? "," : "");
-    printf("\n        : \"s\"(0x0F0F0F0Fu), \"s\"(0xF0F0F0F0u), \"s\"(0x33333333u), \"s\"(0xCCCCCCCCu), "
-           "\"s\"(0x55555555u), \"s\"(0xAAAAAAAAu), \"v\"(va), \"v\"(vb) : \"memory\");\n}\n");
+    printf("\n        : ");
+    if (nm == 6)
+        printf("\"s\"(0x0F0F0F0Fu), \"s\"(0xF0F0F0F0u), \"s\"(0x33333333u), \"s\"(0xCCCCCCCCu), "
+               "\"s\"(0x55555555u), \"s\"(0xAAAAAAAAu), ");
+    else if (nm == 3)
+        printf("\"s\"(0xF0F0F0F0u), \"s\"(0xCCCCCCCCu), \"s\"(0xAAAAAAAAu), ");
+    printf("\"v\"(va), \"v\"(vb) : \"memory\");\n}\n");
 }
 
 

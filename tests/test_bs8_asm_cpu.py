@@ -231,7 +231,8 @@ def phase_operands(body):
     masks follow the block's temporaries, gen_bs8_small.cpp emit_phase)."""
     nt = len(re.findall(r'"=&v"\(t\d+\)', body))
     regs = {128 + t: 0x9E3779B9 * (t + 1) & M32 for t in range(nt)}
-    for i, m in enumerate((0x0F0F0F0F, 0xF0F0F0F0, 0x33333333, 0xCCCCCCCC, 0x55555555, 0xAAAAAAAA)):
+    masks = [int(m, 16) for m in re.findall(r'"s"\((0x[0-9A-Fa-f]+)u\)', body)]  # in operand order
+    for i, m in enumerate(masks):
         regs[128 + nt + i] = m
     return regs
 

@@ -127,12 +127,15 @@ def test_pass_grid_caps_do_not_change_results(lib, cap):
     assert lib.rsm_ctx_set_pass_grid(ctx, 2, 0, None) == R.RSM_EINVAL
 
 
-@pytest.mark.parametrize("S,count", [(512, 1), (512, 2), (512, 3), (512, 17), (64, 9), (1024, 4), (512, 70), (64, 1)])
+@pytest.mark.parametrize("S,count", [(512, 1), (512, 2), (512, 3), (512, 17), (64, 9), (1024, 4), (512, 70), (64, 1),
+                                     (2048, 2), (192, 3), (320, 2), (4096, 1)])
 def test_single_launch_batch_matches_two_launch(lib, S, count):
     """Batches of k = 128 squares run as ONE queue-driven launch (row sets, Q0-column
-    sets, Q1-column sets from a ready list: extend_gf8_bs128q_kernel); bit-exact with
+    sets, Q1-column sets from a ready list: extend_gf8_bs128s_kernel); bit-exact with
     the two-launch form, twice on the same (self-re-zeroed) queue words, and the
-    first / last square against the oracle."""
+    first / last square against the oracle.  S dividing the 2 KiB set width takes the
+    fixed per-lane offsets (kernel variant 16777216), 192 / 320 / 4096 the general
+    per-lane division."""
     ctx = R.device_context(0)
     k = 128
     W = 2 * k
