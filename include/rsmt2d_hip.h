@@ -51,8 +51,9 @@ void rsm_ctx_destroy(rsm_ctx* ctx);
 int rsm_ctx_device(const rsm_ctx* ctx);
 /* Throughput tuning for several extensions in flight on different streams: cap the
  * persistent grid (CUs) of this context's GF(2^8) M = 128 row pass (pass 0) or
- * column pass (pass 1); 0 = all CUs (default).  *previous (may be NULL) receives
- * the old cap.  Results never depend on it. */
+ * column pass (pass 1); the single-launch queue extension (both passes) takes the
+ * pass-0 cap; 0 = all CUs (default).  *previous (may be NULL) receives the old cap.
+ * Results never depend on it. */
 int rsm_ctx_set_pass_grid(rsm_ctx* ctx, int pass, int cus, int* previous);
 /* Latency tuning: GF(2^8) extensions of up to `squares` squares per call with
  * 65 <= k <= 128 run in the latency form (two launches of the split byte-table

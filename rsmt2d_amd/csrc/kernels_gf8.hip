@@ -802,6 +802,7 @@ struct SplitEncPlan {
     uint32_t fused;
 };
 constexpr uint32_t kSplitSpinLimit = 1u << 20;  // polls (~1 s) before a wait is declared stuck
+constexpr uint32_t kSplitFlag0 = 256;  // the fused form's 64 done flags: words 256 + 16 x (1280 words in all)
 
 template <int NW>
 __global__ __launch_bounds__(64 * NW) void encode_gf8_split_kernel(SplitEncPlan p) {
@@ -817,13 +818,19 @@ __global__ __launch_bounds__(64 * NW) void encode_gf8_split_kernel(SplitEncPlan 
     task -= kind == 0u ? 0u : (kind == 1u ? p.n0 : p.n0 + p.n1);
     const CodewordSet& cs = p.cs[kind];
     const bool fused = p.fused != 0u;
+    // fused form: the rows and the Q1 columns are the critical path, the Q0 columns
+    // fill the issue slots they leave (wave priority)
+    if (fused && kind != 1u) __builtin_amdgcn_s_setprio(3);
     if (fused && kind == 2u) {
-        // wait for every row task's Q1 (their counter adds follow their sc1 stores and
-        // a vmcnt(0) + barrier); then ONE agent acquire before the barrier that
+        // wait for every row task's Q1: the row task whose counter add comes last sets
+        // 64 replicated done flags (one 64-B line each, kSplitFlag0 + 16 x), and this
+        // workgroup polls its own line -- 256 pollers on the counter word itself slowed
+        // the row tasks' memory traffic; then ONE agent acquire before the barrier that
         // precedes this workgroup's loads (hand-off argument)
         if (threadIdx.x == 0) {
             uint32_t n = 0;
-            while (__hip_atomic_load(p.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < p.n0) {
+            const uint32_t* flag = p.ctr + kSplitFlag0 + 16u * (blockIdx.x & 63u);
+            while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
                 if (++n >= kSplitSpinLimit) {
                     __hip_atomic_store(p.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     break;
@@ -872,11 +879,24 @@ __global__ __launch_bounds__(64 * NW) void encode_gf8_split_kernel(SplitEncPlan 
     if (handoff) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (threadIdx.x == 0) __hip_atomic_fetch_add(p.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else if (fused && kind == 2u && threadIdx.x == 0) {
-        if (__hip_atomic_fetch_add(p.ctr + 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == p.n2 - 1u) {
-            __hip_atomic_store(p.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // every waiter is past its wait
-            __hip_atomic_store(p.ctr + 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // the last row task (its add returns n0 - 1: every other row task's add, each
+        // behind its own write-through stores, came before) sets the 64 done flags,
+        // one lane per line, after its add has returned
+        uint32_t last = 0;
+        if (threadIdx.x == 0)
+            last = __hip_atomic_fetch_add(p.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == p.n0 - 1u;
+        if (threadIdx.x < 64u && __builtin_amdgcn_readfirstlane(last))
+            __hip_atomic_store(p.ctr + kSplitFlag0 + 16u * threadIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (fused && kind == 2u && threadIdx.x < 64u) {
+        uint32_t last = 0;
+        if (threadIdx.x == 0)
+            last = __hip_atomic_fetch_add(p.ctr + 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == p.n2 - 1u;
+        if (__builtin_amdgcn_readfirstlane(last)) {  // every waiter is past its wait: re-zero for the next launch
+            __hip_atomic_store(p.ctr + kSplitFlag0 + 16u * threadIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (threadIdx.x == 0) {
+                __hip_atomic_store(p.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(p.ctr + 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
     }
 }

@@ -347,7 +347,9 @@ int extend_squares_queue(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, u
     QueuePlan p{};
     p.rows = rows_set(d_eds, k, S, count);
     p.cols = cols_set(d_eds, k, S, count);
-    p.rows.grid = p.cols.grid = ctx->cus;
+    // persistent grid: every CU, or the row-pass cap of rsm_ctx_set_pass_grid
+    const uint32_t cap = ctx->pass_grid[0].load(std::memory_order_relaxed);
+    p.rows.grid = p.cols.grid = cap && cap < ctx->cus ? cap : ctx->cus;
     p.rows.chunks = p.cols.chunks = (S + 255) / 256;
     if (!bs128_queue_applicable(p.rows, p.cols)) return RSM_EUNSUPPORTED;
     if (int rc = check_queue_reports(ctx, st)) return rc;
@@ -389,7 +391,7 @@ int extend_squares_split(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, u
         if (int rc = check_queue_reports(ctx, st)) return rc;
         StreamScratch& ss = stream_scratch(ctx, st);
         std::lock_guard<std::mutex> lk(ss.mu);
-        if (int rc = queue_words(ss, count, st)) return rc;
+        if (int rc = queue_words(ss, 640, st)) return rc;  // >= 1280 words: counters + 64 done flags
         if ((e = launch_extend_gf8_split_fused(rows, c0, c1, static_cast<uint32_t*>(ss.queue.ptr),
                                                static_cast<uint32_t*>(ss.qerr.ptr), st)) != hipSuccess)
             return hip_fail(e, "split extension (one launch)");

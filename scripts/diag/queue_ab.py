@@ -5,7 +5,8 @@ Configurations "kind,B,streams,delay": kind "two" = the round-1 two-launch sched
 diagnostic library).  Steps of B squares rotate over 2 buffers and `streams` streams;
 the first and last square of the last step are checked against the two-launch form (refcheck.py), and the
 queue's stuck-wait word is checked.  One JSON line per configuration.
-usage: python3 scripts/diag/queue_ab.py two,32,2,0 queue,32,1,2 ...
+usage: python3 scripts/diag/queue_ab.py two,32,2,0 queue,32,1,2 queue,256,3,2,40,192 ...
+(fields: kind, squares per step, streams, delay[, mode[, grid]])
 """
 import ctypes
 import json
@@ -44,6 +45,8 @@ def run(cfg, steps=STEPS, warmup=6):
     else:
         chk(D.rsm_diag_set_bs_mode(int(mode), 1, 0))
     grid = 224 if (kind == "two" and ns > 1) else 0
+    if len(f) > 5:  # optional 6th field: persistent grid (workgroups) of the queue launch
+        grid = int(f[5])
     chk(D.rsm_ctx_set_pass_grid(ctx, 0, grid, None))
     bufs = []
     nb = max(2, ns)  # a buffer per concurrently running step
