@@ -87,3 +87,35 @@ def test_pipeline_matches_two_launch(dl):
     for p in (ref, x0, x1):
         dl.rsm_dev_free(ctx, p)
     dl.rsm_ctx_destroy(ctx)
+
+
+@pytest.mark.parametrize("k,S", [(128, 512), (100, 320)])
+def test_split_one_launch_form(dl, k, S):
+    """The latency form's one-launch variant (diagnostic: Q1-column workgroups wait on
+    64 replicated done flags, wave priorities) == the two-launch latency form and the
+    oracle, three times on the same self-re-zeroed words."""
+    n = (2 * k) ** 2 * S
+    ctx = _ctx(dl)
+    src, a, b = _buf(dl, ctx, n), _buf(dl, ctx, n), _buf(dl, ctx, n)
+    R._check_with(dl, dl.rsm_dev_fill_random(ctx, src, n, 77))
+    R._check_with(dl, dl.rsm_sync(ctx))
+    R._check_with(dl, dl.rsm_memcpy(ctx, a, src, n, 2))
+    R._check_with(dl, dl.rsm_diag_set_split_fused(0))
+    R._check_with(dl, dl.rsm_extend_squares_dev(ctx, a, k, S, 1, None))
+    R._check_with(dl, dl.rsm_sync(ctx))
+    ga = _down(dl, ctx, a, n)
+    sq = ga.reshape(2 * k, 2 * k, S)
+    assert np.array_equal(sq, oracle.extend_square(sq[:k, :k].copy(), nthreads=8))
+    try:
+        R._check_with(dl, dl.rsm_diag_set_split_fused(1))
+        for _ in range(3):
+            R._check_with(dl, dl.rsm_memcpy(ctx, b, src, n, 2))
+            R._check_with(dl, dl.rsm_extend_squares_dev(ctx, b, k, S, 1, None))
+            R._check_with(dl, dl.rsm_diag_queue_check(ctx, None))
+            R._check_with(dl, dl.rsm_sync(ctx))
+            assert np.array_equal(ga, _down(dl, ctx, b, n))
+    finally:
+        R._check_with(dl, dl.rsm_diag_set_split_fused(0))
+    for p in (src, a, b):
+        dl.rsm_dev_free(ctx, p)
+    dl.rsm_ctx_destroy(ctx)
