@@ -612,6 +612,17 @@ int64_t rsm_codec_max_chunks(void) { return (int64_t)32768 * 32768; }
 int rsm_codec_validate_chunk_size(int64_t share_size) { return validate_chunk_size(share_size); }
 int rsm_codec_field_bits(uint32_t k) { return field_bits(k); }
 
+// Device address of a lane's pinned staging: the Codec calls of GF(2^8) codewords with
+// 65 <= k <= 128 run zero-copy -- the kernel reads the shares from the pinned buffer
+// over PCIe and writes its results back there (one launch and one stream wait per
+// call, no DMA copies); nullptr where the runtime cannot map it (the copy path then).
+static void* lane_host_dev(Lane& L) {
+    void* p = nullptr;
+    if (hipHostGetDevicePointer(&p, L.host.ptr, 0) != hipSuccess) return nullptr;
+    return p;
+}
+static bool codec_zero_copy(uint32_t k) { return field_bits(k) == 8 && ceil_pow2(k) == 128; }
+
 int rsm_encode(rsm_ctx* ctx, const uint8_t* const* data, uint32_t k, uint32_t share_size,
                uint8_t* const* parity) {
     if (!ctx || !data || !parity || k == 0) return fail(RSM_EINVAL, "rsm_encode: bad arguments");
@@ -631,6 +642,24 @@ int rsm_encode(rsm_ctx* ctx, const uint8_t* const* data, uint32_t k, uint32_t sh
     if ((e = L.dev.ensure(bytes)) != hipSuccess) return hip_fail(e, "hipMalloc");
     uint8_t* h = static_cast<uint8_t*>(L.host.ptr);
     for (uint32_t i = 0; i < k; ++i) memcpy(h + i * S, data[i], S);
+    if (codec_zero_copy(k))
+        if (uint8_t* hd = static_cast<uint8_t*>(lane_host_dev(L))) {
+            // latency form (the split byte-table encoder: one 8-wave workgroup per 256-B
+            // chunk) straight on the pinned buffer
+            CodewordSet cs{};
+            cs.base = cs.out_base = hd;
+            cs.elem_stride = S;
+            cs.out_offset = (uint64_t)k * S;
+            cs.per_square = 1;
+            cs.count = 1;
+            cs.k = k;
+            cs.S = share_size;
+            cs.pass = 1;
+            if ((e = launch_encode_gf8_split(cs, nullptr, L.stream)) != hipSuccess) return hip_fail(e, "encode kernel launch");
+            if ((e = hipStreamSynchronize(L.stream)) != hipSuccess) return hip_fail(e, "encode");
+            for (uint32_t i = 0; i < k; ++i) memcpy(parity[i], h + (k + i) * S, S);
+            return RSM_OK;
+        }
     uint8_t* d = static_cast<uint8_t*>(L.dev.ptr);
     if ((e = hipMemcpyAsync(d, h, k * S, hipMemcpyHostToDevice, L.stream)) != hipSuccess)
         return hip_fail(e, "hipMemcpyAsync H2D");
@@ -680,6 +709,24 @@ int rsm_decode(rsm_ctx* ctx, uint8_t* const* shares, const uint8_t* present, uin
     }
     uint8_t* hp = h + bytes;
     for (uint32_t i = 0; i < n; ++i) hp[i] = present[i] ? 1 : 0;
+    if (codec_zero_copy(k))
+        if (uint8_t* hd = static_cast<uint8_t*>(lane_host_dev(L))) {
+            // the split decoder straight on the pinned buffer: it reads every point and
+            // the presence bytes over PCIe and writes only the missing shares back
+            DecodeSet ds{};
+            ds.base = hd;
+            ds.presence = hd + bytes;
+            ds.indices = static_cast<const uint32_t*>(ctx->zero_index.ptr);
+            ds.count = 1;
+            ds.axis = 0;
+            ds.k = k;
+            ds.S = share_size;
+            if (int rc = launch_decode(ctx, ds, L.stream)) return rc;
+            if ((e = hipStreamSynchronize(L.stream)) != hipSuccess) return hip_fail(e, "decode");
+            for (uint32_t i = 0; i < n; ++i)
+                if (!present[i]) memcpy(shares[i], h + i * S, S);
+            return RSM_OK;
+        }
     uint8_t* d = static_cast<uint8_t*>(L.dev.ptr);
     uint8_t* dpres = static_cast<uint8_t*>(L.aux.ptr);
     if ((e = hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, L.stream)) != hipSuccess)
