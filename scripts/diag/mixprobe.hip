@@ -3,7 +3,7 @@
 // row r < k of every square: read the Q0 row (k*S contiguous bytes) and write the
 // Q1 row, the Q2 row r and the Q3 row r (3 x k*S): exactly 4k^2 S per square, the
 // best any schedule of the extension can move.
-// Usage: mixprobe <squares> <wg_per_cu> <mode> [threads]
+// Usage: mixprobe <squares> <wg_per_cu> <mode> [threads] [launches]
 //   mode bits: 1 = non-temporal loads, 2 = non-temporal stores, 4 = sc1 stores,
 //              8 = read only (no stores), 16 = write only (no loads)
 // Prints one JSON line: us per square, algorithmic TB/s and fraction of 8 TB/s.
@@ -72,6 +72,7 @@ int main(int argc, char** argv) {
     const uint32_t nsq = atoi(argv[1]);
     const int wgcu = atoi(argv[2]), mode = atoi(argv[3]);
     const int thr = argc > 4 ? atoi(argv[4]) : 512;
+    const int reps = argc > 5 ? atoi(argv[5]) : 16;  // launches (the first 3 untimed)
     if (nsq == 0 || nsq > 512 || wgcu < 1 || wgcu > 8 || thr < 64 || thr > 1024 || thr % 64) {
         fprintf(stderr, "bad arguments\n");
         return 2;
@@ -100,7 +101,7 @@ int main(int argc, char** argv) {
         }
     };
     std::vector<float> ts;
-    for (int r = 0; r < 16; ++r) {
+    for (int r = 0; r < (reps > 4 ? reps : 4); ++r) {
         CK(hipEventRecord(e0, 0));
         launch(buf[r % 3]);
         CK(hipGetLastError());
