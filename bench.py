@@ -598,6 +598,73 @@ def bench_c4(local, L, R, steps, B=2):
             "kernel": "enc16_kernel<256> (row pass, column pass)"}
 
 
+def bench_nmt_roots(local, L, R, k, S, squares=32, reps=5, ns=29):
+    """The same with Celestia's tree: extension + NMT row/column roots (celestiaorg/nmt
+    v0.24.3 as rsmt2d's erasured wrappers push it: namespace 29 bytes, parity namespace
+    0xFF.. outside Q0, IgnoreMaxNamespace) of `squares` squares, all on the
+    device (rsm_extend_squares_dev for the batch + one rsm_nmt_roots_dev per square).
+    Synthetic ODS: random payload, namespaces non-decreasing along every row and column
+    (big-endian cell index), as a valid block has them; rsm_nmt_roots_squares_dev does
+    the batch in one launch pair.  The first square's roots are checked against the host
+    restatement (oracle/nmt.py) before timing."""
+    import ctypes
+    import numpy as np
+    ctx = R.device_context(local)
+    W = 2 * k
+    sq = W * W * S
+    rng = np.random.default_rng(0x4E4D54)
+    ods = rng.integers(0, 256, (k, k, S), dtype=np.uint8)
+    idx = np.arange(k * k, dtype=np.uint64).reshape(k, k)
+    for b in range(8):  # namespace = cell index, big-endian in the last 8 of its ns bytes
+        ods[:, :, ns - 1 - b] = ((idx >> np.uint64(8 * b)) & np.uint64(0xFF)).astype(np.uint8)
+    ods[:, :, : ns - 8] = 0
+    full = np.zeros((W, W, S), np.uint8)
+    full[:k, :k] = ods
+    buf = R.DeviceBuffer(squares * sq, local)
+    for i in range(squares):
+        buf.upload(full, i * sq)
+    roots = R.DeviceBuffer(squares * 2 * W * (2 * ns + 32), local)
+    status = R.DeviceBuffer(squares * 2 * W * 4, local)
+    p = R.NmtParams(ns, 1, k)
+
+    def nmt_roots():
+        R._check(L.rsm_nmt_roots_squares_dev(ctx, buf.ptr, W, S, squares, ctypes.byref(p), roots.ptr, status.ptr, None))
+
+    def run():
+        R._check(L.rsm_extend_squares_dev(ctx, buf.ptr, k, S, squares, None))
+        nmt_roots()
+
+    run()
+    R._check(L.rsm_sync(ctx))
+    got = roots.download(2 * W * (2 * ns + 32)).reshape(2 * W, 2 * ns + 32)
+    st = status.download(squares * 2 * W * 4).view(np.uint32)
+    eds = buf.download(sq).reshape(W, W, S)
+    import oracle.nmt as onmt
+    for axis, i in ((0, 0), (1, W - 1)):
+        vec = eds[i] if axis == 0 else eds[:, i]
+        want = onmt.erasured_root([bytes(c) for c in vec], i, k, ns)
+        if bytes(got[axis * W + i]) != want or st.any():
+            raise SystemExit("bench nmt roots: device root differs from the restatement")
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        run()
+    R._check(L.rsm_sync(ctx))
+    dt = (time.perf_counter() - t0) / reps
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        nmt_roots()
+    R._check(L.rsm_sync(ctx))
+    dr = (time.perf_counter() - t0) / reps
+    for b in (buf, roots, status):
+        b.free()
+    return {"workload": f"extension + NMT row/col roots (namespace {ns} B), k={k}, S={S}, {squares} squares per step",
+            "ms_per_square": round(dt / squares * 1e3, 4), "ods_GiB_s": round(squares * k * k * S / dt / 2**30, 3),
+            "roots_only_ms_per_square": round(dr / squares * 1e3, 4),
+            "note": "rsm_nmt_roots_squares_dev: one leaf launch (ns||share per cell, shared by its row and column "
+                    "tree) and one tree launch (min/max namespace nodes) for the batch; roots of square 0 checked "
+                    "against oracle/nmt.py"}
+
+
 def bench_roots(local, L, R, buf, k, S, B, steps):
     """BenchmarkExtensionWithRoots (extendeddatasquare_test.go:309-334): the 2D
     extension plus RowRoots + ColRoots (DefaultTree) of every square, all on the
@@ -888,6 +955,7 @@ def main():
         out["cpu_baseline"] = None if a.no_cpu_baseline else cpu_baseline(k, S, a.cpu_seconds)
     if rank == 0 and world == 1 and not a.no_roots:
         out["with_roots"] = bench_roots(local, L, R, buf, k, S, B, a.steps)
+        out["with_nmt_roots"] = bench_nmt_roots(local, L, R, k, S)
     for b in bufs:
         b.free()
     for st in streams[1:]:

@@ -252,6 +252,11 @@ int rsm_nmt_tree_root(void* user, int axis, uint32_t index, const uint8_t* const
  * Asynchronous on `stream`. */
 int rsm_nmt_roots_dev(rsm_ctx* ctx, const void* d_eds, uint32_t width, uint32_t share_size,
                       const rsm_nmt_params* params, void* d_roots, void* d_status, void* stream);
+/* The same for `count` consecutive device squares in one launch pair (a block's
+ * worth of squares: the trees of one square alone leave most CUs idle); d_roots and
+ * d_status hold 2*width entries per square, square after square. */
+int rsm_nmt_roots_squares_dev(rsm_ctx* ctx, const void* d_eds, uint32_t width, uint32_t share_size, uint32_t count,
+                              const rsm_nmt_params* params, void* d_roots, void* d_status, void* stream);
 
 /* ---- ExtendedDataSquare (extendeddatasquare.go, datasquare.go) ------------------ */
 /* ComputeExtendedDataSquare(data, codec, tree) (:50-77): n shares (lens[i] bytes). */

@@ -166,6 +166,7 @@ SIGNATURES = {
     "rsm_default_tree_root": (_I32, [_VP, _I32, _U32, _VP, _U32, _U32, _VP, _VP]),
     "rsm_nmt_tree_root": (_I32, [_VP, _I32, _U32, _VP, _U32, _U32, _VP, _VP]),
     "rsm_nmt_roots_dev": (_I32, [_VP, _VP, _U32, _U32, ctypes.POINTER(NmtParams), _VP, _VP, _VP]),
+    "rsm_nmt_roots_squares_dev": (_I32, [_VP, _VP, _U32, _U32, _U32, ctypes.POINTER(NmtParams), _VP, _VP, _VP]),
     "rsm_eds_compute": (_I32, [_VP, _VP, _VP, _U64, ctypes.POINTER(_VP)]),
     "rsm_eds_import": (_I32, [_VP, _VP, _VP, _U64, ctypes.POINTER(_VP)]),
     "rsm_eds_new": (_I32, [_VP, _U32, _U32, ctypes.POINTER(_VP)]),

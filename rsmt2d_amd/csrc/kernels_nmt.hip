@@ -51,10 +51,14 @@ __device__ __forceinline__ uint32_t be_word(const uint32_t* p, int i) { return _
 
 // Leaf records: leaf[cell][0..7] = namespace (big-endian words, zero padded),
 // leaf[cell][8..15] = SHA256(0x00 || ns || share).
+// Batched: blockIdx.y is the square (consecutive [W][W][S] buffers, leaf records
+// consecutive per square).
 __global__ __launch_bounds__(256) void nmt_leaf_kernel(const uint8_t* __restrict__ eds, uint32_t W, uint32_t S,
                                                        uint32_t ns, uint32_t k, uint32_t* __restrict__ leaf) {
     const uint32_t cell = blockIdx.x * 256u + threadIdx.x;
     if (cell >= W * W) return;
+    eds += (uint64_t)blockIdx.y * W * W * S;
+    leaf += (uint64_t)blockIdx.y * W * W * kLeafWords;
     const uint32_t r = cell / W, c = cell - r * W;
     const bool q0 = r < k && c < k;
     const uint32_t* dw = reinterpret_cast<const uint32_t*>(eds + (uint64_t)cell * S);
@@ -188,12 +192,16 @@ __device__ __forceinline__ void lds_store(uint32_t* p, const Node& n) {
     for (int i = 0; i < 8; ++i) p[2 * kNsWords + i] = n.d[i];
 }
 
-// One workgroup per tree (blockIdx.x < W: row tree, else column tree).  Dynamic
-// LDS: two levels of W/2 nodes (ping-pong) + 256 per-thread message buffers.
+// One workgroup per tree (blockIdx.x < W: row tree, else column tree; blockIdx.y the
+// square of a batch).  Dynamic LDS: two levels of W/2 nodes (ping-pong) + 256
+// per-thread message buffers.
 __global__ __launch_bounds__(256) void nmt_tree_kernel(const uint32_t* __restrict__ leaf, uint32_t W, uint32_t ns,
                                                        uint32_t ignore_max, uint8_t* __restrict__ roots,
                                                        uint32_t* __restrict__ status) {
     extern __shared__ uint32_t lds[];
+    leaf += (uint64_t)blockIdx.y * W * W * kLeafWords;
+    roots += (uint64_t)blockIdx.y * 2 * W * (2 * ns + 32);
+    if (status) status += (uint64_t)blockIdx.y * 2 * W;
     const uint32_t half = W / 2;
     auto lvl = [&](uint32_t which) -> uint32_t* { return lds + (size_t)which * half * kNodeWords; };
     uint8_t* mb = reinterpret_cast<uint8_t*>(lds + (size_t)2 * half * kNodeWords) + threadIdx.x * (64u * node_blocks(ns));
@@ -269,15 +277,18 @@ bool nmt_dev_supported(uint32_t W, uint32_t ns) {
     return W >= 2 && W <= kMaxWidth && ns >= 1 && ns <= kMaxNs && tree_lds_bytes(W, ns) <= kLdsCap;
 }
 
-// d_leaf: W*W*64 bytes of scratch.
+// d_leaf: squares * W*W*64 bytes of scratch; the squares are consecutive [W][W][S]
+// buffers, their 2W roots (and statuses) consecutive per square.
 hipError_t launch_nmt_roots(const uint8_t* d_eds, uint32_t W, uint32_t S, uint32_t ns, uint32_t k, uint32_t ignore_max,
-                            uint32_t* d_leaf, uint8_t* d_roots, uint32_t* d_status, hipStream_t st) {
+                            uint32_t* d_leaf, uint8_t* d_roots, uint32_t* d_status, hipStream_t st, uint32_t squares) {
+    if (squares == 0) return hipSuccess;
     const uint32_t cells = W * W;
-    hipLaunchKernelGGL(nmt_leaf_kernel, dim3((cells + 255) / 256), dim3(256), 0, st, d_eds, W, S, ns, k, d_leaf);
+    hipLaunchKernelGGL(nmt_leaf_kernel, dim3((cells + 255) / 256, squares), dim3(256), 0, st, d_eds, W, S, ns, k, d_leaf);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const size_t lds = tree_lds_bytes(W, ns);
-    hipLaunchKernelGGL(nmt_tree_kernel, dim3(2 * W), dim3(256), lds, st, d_leaf, W, ns, ignore_max, d_roots, d_status);
+    hipLaunchKernelGGL(nmt_tree_kernel, dim3(2 * W, squares), dim3(256), lds, st, d_leaf, W, ns, ignore_max, d_roots,
+                       d_status);
     return hipGetLastError();
 }
 

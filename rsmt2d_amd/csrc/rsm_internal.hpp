@@ -158,10 +158,11 @@ int device_roots(rsm_ctx* ctx, const uint8_t* d_eds, uint32_t W, uint32_t S, uin
                  uint32_t squares = 1);
 // Whether (tree_fn, user) is a tree the GPU computes for a square of width W.
 bool device_tree_for(rsm_tree_root_fn fn, void* user, uint32_t W, DevTree* out);
-// Roots of all 2W trees of a complete device square: d_roots 2W * t.root_len bytes
-// (rows, then columns); d_status 2W words, non-zero where a tree fails (NMT push
-// order; all zero for the DefaultTree).  Asynchronous on st.
+// Roots of all 2W trees of `squares` complete consecutive device squares: d_roots
+// 2W * t.root_len bytes per square (rows, then columns); d_status 2W words per square,
+// non-zero where a tree fails (NMT push order; all zero for the DefaultTree).
+// Asynchronous on st.
 int device_tree_roots(rsm_ctx* ctx, const DevTree& t, const uint8_t* d_eds, uint32_t W, uint32_t S,
-                      uint8_t* d_roots, uint32_t* d_status, hipStream_t st);
+                      uint8_t* d_roots, uint32_t* d_status, hipStream_t st, uint32_t squares = 1);
 
 }  // namespace rsm

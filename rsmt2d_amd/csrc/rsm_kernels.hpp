@@ -93,7 +93,7 @@ bool roots_dev_supported(uint32_t W);
 // d_roots 2W roots of 2*ns+32 bytes, d_status (nullable) 2W words.
 bool nmt_dev_supported(uint32_t W, uint32_t ns);
 hipError_t launch_nmt_roots(const uint8_t* d_eds, uint32_t W, uint32_t S, uint32_t ns, uint32_t k, uint32_t ignore_max,
-                            uint32_t* d_leaf, uint8_t* d_roots, uint32_t* d_status, hipStream_t st);
+                            uint32_t* d_leaf, uint8_t* d_roots, uint32_t* d_status, hipStream_t st, uint32_t squares = 1);
 hipError_t launch_roots(const uint8_t* d_eds, uint32_t W, uint32_t S, uint32_t squares, uint32_t* d_leaf,
                         uint8_t* d_roots, hipStream_t st);
 hipError_t launch_leaf_hashes(const uint8_t* d_cells, uint32_t cells, uint32_t S, uint32_t* d_leaf, hipStream_t st);

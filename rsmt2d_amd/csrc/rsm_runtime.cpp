@@ -485,23 +485,23 @@ bool device_tree_for(rsm_tree_root_fn fn, void* user, uint32_t W, DevTree* out) 
 }
 
 int device_tree_roots(rsm_ctx* ctx, const DevTree& t, const uint8_t* d_eds, uint32_t W, uint32_t S,
-                      uint8_t* d_roots, uint32_t* d_status, hipStream_t st) {
+                      uint8_t* d_roots, uint32_t* d_status, hipStream_t st, uint32_t squares) {
     hipError_t e;
     if (!t.nmt) {
-        if (d_status && (e = hipMemsetAsync(d_status, 0, (size_t)2 * W * 4, st)) != hipSuccess)
+        if (d_status && (e = hipMemsetAsync(d_status, 0, (size_t)squares * 2 * W * 4, st)) != hipSuccess)
             return hip_fail(e, "hipMemsetAsync (status)");
-        return device_roots(ctx, d_eds, W, S, d_roots, st);
+        return device_roots(ctx, d_eds, W, S, d_roots, st, squares);
     }
     if (S < t.p.namespace_size) return fail(RSM_ETREE, "data is too short to contain namespace ID");
     StreamScratch& ss = stream_scratch(ctx, st);
     std::lock_guard<std::mutex> lk(ss.mu);
-    const size_t need = (size_t)W * W * 64;
+    const size_t need = (size_t)squares * W * W * 64;
     if (need > ss.leaf.cap) {
         if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
         if ((e = ss.leaf.ensure(need)) != hipSuccess) return hip_fail(e, "hipMalloc (NMT leaves)");
     }
     if ((e = launch_nmt_roots(d_eds, W, S, t.p.namespace_size, t.p.square_size, t.p.ignore_max_namespace,
-                              static_cast<uint32_t*>(ss.leaf.ptr), d_roots, d_status, st)) != hipSuccess)
+                              static_cast<uint32_t*>(ss.leaf.ptr), d_roots, d_status, st, squares)) != hipSuccess)
         return hip_fail(e, "NMT roots kernel launch");
     return RSM_OK;
 }
@@ -929,6 +929,23 @@ int rsm_nmt_roots_dev(rsm_ctx* ctx, const void* d_eds, uint32_t width, uint32_t 
                     params->namespace_size);
     return device_tree_roots(ctx, t, static_cast<const uint8_t*>(d_eds), width, share_size,
                              static_cast<uint8_t*>(d_roots), static_cast<uint32_t*>(d_status), pick(ctx, stream));
+}
+
+int rsm_nmt_roots_squares_dev(rsm_ctx* ctx, const void* d_eds, uint32_t width, uint32_t share_size, uint32_t count,
+                              const rsm_nmt_params* params, void* d_roots, void* d_status, void* stream) {
+    if (!ctx || !d_eds || !d_roots || !params || width == 0)
+        return fail(RSM_EINVAL, "rsm_nmt_roots_squares_dev: bad arguments");
+    if (int rc = validate_chunk_size(share_size)) return rc;
+    if (count == 0) return RSM_OK;
+    if (int rc = use_device(ctx)) return rc;
+    DevTree t;
+    if (!device_tree_for(rsm_nmt_tree_root, const_cast<rsm_nmt_params*>(params), width, &t))
+        return fail(RSM_EUNSUPPORTED, "device NMT roots: width %u, namespace size %u not supported", width,
+                    params->namespace_size);
+    if ((uint64_t)count * width * width * 64 > (1ull << 34))
+        return fail(RSM_EUNSUPPORTED, "rsm_nmt_roots_squares_dev: %u squares need over 16 GiB of leaf records", count);
+    return device_tree_roots(ctx, t, static_cast<const uint8_t*>(d_eds), width, share_size,
+                             static_cast<uint8_t*>(d_roots), static_cast<uint32_t*>(d_status), pick(ctx, stream), count);
 }
 
 int rsm_roots_squares_dev(rsm_ctx* ctx, const void* d_eds, uint32_t width, uint32_t share_size, uint32_t count,

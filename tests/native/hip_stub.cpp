@@ -184,10 +184,14 @@ hipError_t launch_tree_roots(const uint32_t* d_leaf, uint32_t W, uint32_t first,
 }
 bool nmt_dev_supported(uint32_t W, uint32_t ns) { return W >= 2 && W <= 1024 && ns >= 1 && ns <= 32; }
 hipError_t launch_nmt_roots(const uint8_t* d_eds, uint32_t W, uint32_t S, uint32_t ns, uint32_t, uint32_t,
-                            uint32_t* d_leaf, uint8_t* d_roots, uint32_t* d_status, hipStream_t) {
-    for (uint64_t c = 0; c < (uint64_t)W * W; ++c) d_leaf[c * 16] = d_eds[c * S];
-    memset(d_roots, 0, (size_t)2 * W * (2 * ns + 32));
-    if (d_status) memset(d_status, 0, (size_t)2 * W * 4);
+                            uint32_t* d_leaf, uint8_t* d_roots, uint32_t* d_status, hipStream_t, uint32_t squares) {
+    for (uint32_t q = 0; q < squares; ++q) {
+        const uint8_t* e = d_eds + (uint64_t)q * W * W * S;
+        uint32_t* lf = d_leaf + (uint64_t)q * W * W * 16;
+        for (uint64_t c = 0; c < (uint64_t)W * W; ++c) lf[c * 16] = e[c * S];
+        memset(d_roots + (uint64_t)q * 2 * W * (2 * ns + 32), 0, (size_t)2 * W * (2 * ns + 32));
+        if (d_status) memset(d_status + (uint64_t)q * 2 * W, 0, (size_t)2 * W * 4);
+    }
     return hipSuccess;
 }
 hipError_t launch_fill_random(void* p, uint64_t bytes, uint64_t seed, hipStream_t) {

@@ -94,6 +94,41 @@ def test_nmt_roots_dev_vs_oracle(lib, k, ns, S):
     assert [bytes(got[(W + i) * RL:(W + i + 1) * RL]) for i in range(W)] == want_c
 
 
+@pytest.mark.parametrize("k,ns,S,count", [(4, 29, 64, 3), (16, 29, 512, 5), (8, 8, 128, 2)])
+def test_nmt_roots_squares_dev_batched(lib, k, ns, S, count):
+    """rsm_nmt_roots_squares_dev over a batch of squares (one launch pair) == the
+    oracle's roots of every square; one square with an unordered namespace reports its
+    failing trees in its own status words only."""
+    ctx = R.device_context(0)
+    W = 2 * k
+    RL = 2 * ns + 32
+    sqs = []
+    for q in range(count):
+        ods = np.frombuffer(b"".join(gen_rand_sorted_ds(k, S, ns, seed=100 + q)), np.uint8).reshape(k, k, S).copy()
+        if q == count - 1:
+            ods[0, 1, :ns], ods[0, 0, :ns] = ods[0, 0, :ns].copy(), ods[0, 1, :ns].copy()  # row 0 out of order
+        sqs.append(oracle.extend_square(ods, nthreads=8))
+    batch = np.stack(sqs)
+    d = R.DeviceBuffer(batch.nbytes)
+    roots = R.DeviceBuffer(count * 2 * W * RL)
+    status = R.DeviceBuffer(count * 2 * W * 4)
+    d.upload(batch)
+    p = R.NmtParams(ns, 1, k)
+    R._check(lib.rsm_nmt_roots_squares_dev(ctx, d.ptr, W, S, count, ctypes.byref(p), roots.ptr, status.ptr, None))
+    R._check(lib.rsm_sync(ctx))
+    got = roots.download(count * 2 * W * RL).reshape(count, 2 * W, RL)
+    st = np.frombuffer(status.download(count * 2 * W * 4).tobytes(), np.uint32).reshape(count, 2 * W)
+    for q in range(count - 1):
+        assert not st[q].any()
+        want_r, want_c = nmt.eds_roots(sqs[q], k, ns)
+        assert [bytes(got[q, i]) for i in range(W)] == want_r
+        assert [bytes(got[q, W + i]) for i in range(W)] == want_c
+    bad = st[count - 1]
+    if not np.array_equal(sqs[-1][0, 0, :ns], sqs[-1][0, 1, :ns]):
+        assert bad[0] != 0  # row 0's push order
+    assert not bad[k:W].any()  # parity rows: parity namespace everywhere past Q0
+
+
 def test_nmt_push_order_error_device_and_host():
     """Unsorted namespaces: the reference's Push fails, so RowRoots errors (device
     and host paths alike)."""
