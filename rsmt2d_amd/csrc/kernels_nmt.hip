@@ -23,12 +23,20 @@
 // Namespace sizes up to 32 bytes (Celestia: 29), widths up to 1024 (LDS permitting).
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <utility>
 
 #include "sha256_dev.hpp"
 
 namespace rsm {
 
 namespace {
+
+template <int N, typename F>
+__device__ __forceinline__ void sfor_n(F&& f) {
+    [&]<int... I>(std::integer_sequence<int, I...>) {
+        (f(std::integral_constant<int, I>{}), ...);
+    }(std::make_integer_sequence<int, N>{});
+}
 
 constexpr uint32_t kMaxNs = 32;
 constexpr uint32_t kNsWords = kMaxNs / 4;
@@ -271,6 +279,215 @@ __global__ __launch_bounds__(256) void nmt_tree_kernel(const uint32_t* __restric
     }
 }
 
+// ---------------------------------------------------------------------------
+// Wave-per-tree form for a compile-time namespace size (Celestia: 29): TPW trees per
+// wave, four waves per workgroup, each tree's levels in place in the wave's own LDS
+// (node j of a level reads 2j and 2j + 1 >= j: a level's reads precede its writes),
+// no workgroup barrier -- the DefaultTree kernel's structure (kernels_sha.hip), which
+// beat the level-by-level workgroup form 3x there.  The node message
+// 0x01 || l || r (l, r = min || max || digest) is assembled in registers from
+// compile-time byte positions (the backend forms v_perm / v_alignbit from them)
+// instead of byte stores to a per-thread LDS buffer.  Same tree, same checks, same
+// output as nmt_tree_kernel.
+template <int NS>
+struct WNode {
+    static constexpr int kW = (NS + 3) / 4;
+    uint32_t mn[kW], mx[kW], d[8];
+};
+template <int NS, int B>
+__device__ __forceinline__ uint32_t node_byte(const WNode<NS>& n) {  // byte B of min || max || digest
+    if constexpr (B < NS) return (n.mn[B >> 2] >> (24 - 8 * (B & 3))) & 0xFFu;
+    else if constexpr (B < 2 * NS) return (n.mx[(B - NS) >> 2] >> (24 - 8 * ((B - NS) & 3))) & 0xFFu;
+    else return (n.d[(B - 2 * NS) >> 2] >> (24 - 8 * ((B - 2 * NS) & 3))) & 0xFFu;
+}
+template <int NS, int I>
+__device__ __forceinline__ uint32_t msg_byte(const WNode<NS>& l, const WNode<NS>& r) {
+    constexpr int NL = 2 * NS + 32, LEN = 1 + 2 * NL, NB = (LEN + 8) / 64 + 1;
+    if constexpr (I == 0) return 0x01u;
+    else if constexpr (I <= NL) return node_byte<NS, I - 1>(l);
+    else if constexpr (I <= 2 * NL) return node_byte<NS, I - 1 - NL>(r);
+    else if constexpr (I == LEN) return 0x80u;
+    else if constexpr (I == 64 * NB - 2) return ((8u * LEN) >> 8) & 0xFFu;
+    else if constexpr (I == 64 * NB - 1) return (8u * LEN) & 0xFFu;
+    else return 0u;
+}
+template <int NS>
+__device__ __forceinline__ bool hash_node_w(const WNode<NS>& l, const WNode<NS>& r, bool ignore_max, WNode<NS>& out) {
+    constexpr int NL = 2 * NS + 32, LEN = 1 + 2 * NL, NB = (LEN + 8) / 64 + 1;
+    uint32_t h[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) h[i] = kH0[i];
+    sfor_n<NB>([&](auto Bc) {
+        constexpr int b = decltype(Bc)::value;
+        uint32_t w[16];
+        sfor_n<16>([&](auto Ic) {
+            constexpr int t = 16 * b + decltype(Ic)::value;
+            w[decltype(Ic)::value] = (msg_byte<NS, 4 * t>(l, r) << 24) | (msg_byte<NS, 4 * t + 1>(l, r) << 16) |
+                                     (msg_byte<NS, 4 * t + 2>(l, r) << 8) | msg_byte<NS, 4 * t + 3>(l, r);
+        });
+        sha_block(h, w);
+    });
+    constexpr int kW = WNode<NS>::kW;
+    bool rmin_is_max = true;
+#pragma unroll
+    for (int i = 0; i < kW; ++i) rmin_is_max &= r.mn[i] == head_mask(NS - 4 * i);
+    bool less = false, decided = false;  // r.mn < l.mx ?
+#pragma unroll
+    for (int i = 0; i < kW; ++i)
+        if (!decided && r.mn[i] != l.mx[i]) {
+            less = r.mn[i] < l.mx[i];
+            decided = true;
+        }
+#pragma unroll
+    for (int i = 0; i < kW; ++i) {
+        out.mn[i] = l.mn[i];
+        out.mx[i] = (ignore_max && rmin_is_max) ? l.mx[i] : r.mx[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) out.d[i] = h[i];
+    return !less;
+}
+template <int NS>
+__host__ __device__ constexpr uint32_t wnode_words() { return 2 * WNode<NS>::kW + 8; }
+template <int NS>
+__host__ __device__ constexpr uint32_t wtree_lds_words(uint32_t W) { return ((W + 1) / 2) * wnode_words<NS>(); }
+constexpr uint32_t kNmtTreesPerBlock = 4;  // one wave per tree group
+
+template <int NS, int TPW>
+__global__ __launch_bounds__(256) void nmt_tree_wave_kernel(const uint32_t* __restrict__ leaf, uint32_t W,
+                                                            uint32_t ignore_max, uint8_t* __restrict__ roots,
+                                                            uint32_t* __restrict__ status) {
+    constexpr int kW = WNode<NS>::kW;
+    constexpr uint32_t NW = wnode_words<NS>();
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t t0 = (blockIdx.x * kNmtTreesPerBlock + wv) * TPW, count = 2 * W;
+    if (t0 >= count) return;  // whole wave (no workgroup barrier in this kernel)
+    const uint32_t nt = count - t0 < (uint32_t)TPW ? count - t0 : (uint32_t)TPW;
+    leaf += (uint64_t)blockIdx.y * W * W * kLeafWords;
+    roots += (uint64_t)blockIdx.y * 2 * W * (2 * NS + 32);
+    if (status) status += (uint64_t)blockIdx.y * 2 * W;
+    extern __shared__ uint32_t lds_raw[];
+    uint32_t* const base = lds_raw + (size_t)wv * TPW * wtree_lds_words<NS>(W);
+    auto lvl = [&](uint32_t u) { return base + (size_t)u * wtree_lds_words<NS>(W); };
+    const bool ig = ignore_max != 0;
+    auto leaf_at = [&](uint32_t tree, uint32_t pos, WNode<NS>& n) {
+        const uint32_t axis = tree >= W ? 1u : 0u, idx = tree - axis * W;
+        const uint64_t cell = axis == 0 ? (uint64_t)idx * W + pos : (uint64_t)pos * W + idx;
+        const uint32_t* sp = leaf + cell * kLeafWords;
+#pragma unroll
+        for (int i = 0; i < kW; ++i) n.mn[i] = n.mx[i] = sp[i];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) n.d[i] = sp[kNsWords + i];
+    };
+    auto ld = [&](const uint32_t* p, WNode<NS>& n) {
+#pragma unroll
+        for (int i = 0; i < kW; ++i) n.mn[i] = p[i], n.mx[i] = p[kW + i];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) n.d[i] = p[2 * kW + i];
+    };
+    auto st = [&](uint32_t* p, const WNode<NS>& n) {
+#pragma unroll
+        for (int i = 0; i < kW; ++i) p[i] = n.mn[i], p[kW + i] = n.mx[i];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) p[2 * kW + i] = n.d[i];
+    };
+    auto ns_lt = [&](const uint32_t* a, const uint32_t* b) {  // a < b
+        bool less = false, decided = false;
+#pragma unroll
+        for (int i = 0; i < kW; ++i)
+            if (!decided && a[i] != b[i]) {
+                less = a[i] < b[i];
+                decided = true;
+            }
+        return less;
+    };
+    auto wave_sync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    uint32_t bad = 0;  // bit u: tree u of this wave failed (push order / sibling order)
+    // level 1 from the leaf records (push order checked on every consecutive pair)
+    uint32_t cnt = W, next = (W + 1) / 2;
+    for (uint32_t v = lane; v < nt * next; v += 64u) {
+        const uint32_t u = v / next, j = v - u * next;
+        WNode<NS> a, b, o;
+        leaf_at(t0 + u, 2 * j, a);
+        bool ok = true;
+        if (2 * j + 1 < cnt) {
+            leaf_at(t0 + u, 2 * j + 1, b);
+            if (ns_lt(b.mn, a.mn)) ok = false;
+            if (2 * j + 2 < cnt) {
+                WNode<NS> c;
+                leaf_at(t0 + u, 2 * j + 2, c);
+                if (ns_lt(c.mn, b.mn)) ok = false;
+            }
+            if (!hash_node_w<NS>(a, b, ig, o)) ok = false;
+        } else {
+            o = a;
+        }
+        st(lvl(u) + (size_t)j * NW, o);
+        if (!ok) bad |= 1u << u;
+    }
+    wave_sync();
+    for (cnt = next; cnt > 1; cnt = next) {
+        next = (cnt + 1) / 2;
+        for (uint32_t v = lane; v < nt * next; v += 64u) {
+            const uint32_t u = v / next, j = v - u * next;
+            WNode<NS> a, b, o;
+            ld(lvl(u) + (size_t)(2 * j) * NW, a);
+            if (2 * j + 1 < cnt) {
+                ld(lvl(u) + (size_t)(2 * j + 1) * NW, b);
+                if (!hash_node_w<NS>(a, b, ig, o)) bad |= 1u << u;
+            } else {
+                o = a;
+            }
+            wave_sync();  // every lane's reads of this level before any write (j < 2j)
+            st(lvl(u) + (size_t)j * NW, o);
+        }
+        wave_sync();
+    }
+    // OR of the lanes' failure bits per tree
+    uint32_t all = bad;
+#pragma unroll
+    for (int sft = 1; sft < 64; sft <<= 1) all |= __shfl_xor(all, sft);
+    if (lane < nt) {
+        const uint32_t tree = t0 + lane;
+        WNode<NS> rt;
+        ld(lvl(lane), rt);
+        uint8_t* o = roots + (uint64_t)tree * (2 * NS + 32);
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            o[i] = be_byte(rt.mn, i);
+            o[NS + i] = be_byte(rt.mx, i);
+        }
+#pragma unroll
+        for (int i = 0; i < 32; ++i) o[2 * NS + i] = be_byte(rt.d, i);
+        if (status) status[tree] = (all >> lane) & 1u;
+    }
+}
+
+// trees per wave: as many as keep four waves' LDS within a third of the CU
+template <int NS>
+inline uint32_t nmt_trees_per_wave(uint32_t W) {
+    for (uint32_t t = 4; t > 1; t >>= 1)
+        if ((size_t)kNmtTreesPerBlock * t * wtree_lds_words<NS>(W) * 4u <= 52u * 1024u) return t;
+    return 1;
+}
+template <int NS>
+hipError_t launch_nmt_tree_wave(const uint32_t* d_leaf, uint32_t W, uint32_t ignore_max, uint8_t* d_roots,
+                                uint32_t* d_status, uint32_t squares, hipStream_t st) {
+    const uint32_t tpw = nmt_trees_per_wave<NS>(W);
+    const uint32_t blocks = (2 * W + kNmtTreesPerBlock * tpw - 1) / (kNmtTreesPerBlock * tpw);
+    const size_t lds = (size_t)kNmtTreesPerBlock * tpw * wtree_lds_words<NS>(W) * 4u;
+    switch (tpw) {
+        case 4: hipLaunchKernelGGL((nmt_tree_wave_kernel<NS, 4>), dim3(blocks, squares), dim3(256), lds, st, d_leaf, W, ignore_max, d_roots, d_status); break;
+        case 2: hipLaunchKernelGGL((nmt_tree_wave_kernel<NS, 2>), dim3(blocks, squares), dim3(256), lds, st, d_leaf, W, ignore_max, d_roots, d_status); break;
+        default: hipLaunchKernelGGL((nmt_tree_wave_kernel<NS, 1>), dim3(blocks, squares), dim3(256), lds, st, d_leaf, W, ignore_max, d_roots, d_status); break;
+    }
+    return hipGetLastError();
+}
+
 }  // namespace
 
 bool nmt_dev_supported(uint32_t W, uint32_t ns) {
@@ -286,6 +503,9 @@ hipError_t launch_nmt_roots(const uint8_t* d_eds, uint32_t W, uint32_t S, uint32
     hipLaunchKernelGGL(nmt_leaf_kernel, dim3((cells + 255) / 256, squares), dim3(256), 0, st, d_eds, W, S, ns, k, d_leaf);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    // Celestia's namespace size: the wave-per-tree kernel (its LDS permitting)
+    if (ns == 29 && (size_t)kNmtTreesPerBlock * wtree_lds_words<29>(W) * 4u <= kLdsCap)
+        return launch_nmt_tree_wave<29>(d_leaf, W, ignore_max, d_roots, d_status, squares, st);
     const size_t lds = tree_lds_bytes(W, ns);
     hipLaunchKernelGGL(nmt_tree_kernel, dim3(2 * W, squares), dim3(256), lds, st, d_leaf, W, ns, ignore_max, d_roots,
                        d_status);
