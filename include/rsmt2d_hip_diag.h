@@ -35,6 +35,8 @@ int rsm_diag_set_split_waves(int first, int second);
 /* One square in the latency form: 1 = one launch with a device-side wait (A/B only:
  * slower), 0 = two launches (production). */
 int rsm_diag_set_split_fused(int on);
+/* GF(2^16) m = 512 encoder form: 1 = 8 waves x 64 elements (A/B), 0 = 16 x 32 (production). */
+int rsm_diag_set_enc16_e64(int on);
 /* Both passes of `count` in-place k = 128 squares in ONE persistent launch
  * (extend_gf8_bs128q_kernel: row and Q0-column sets from one queue, Q1-column sets
  * from a ready list; `delay` squares of row sets lead the Q0-column sets).

@@ -23,6 +23,7 @@
 // Every wave works on one (codeword, 512-byte chunk, group|residue) task, so all
 // lanes share each twiddle (wave-uniform SGPR table loads).
 #include <hip/hip_runtime.h>
+#include <atomic>
 #include <cstdint>
 #include <cstdlib>
 #include <utility>
@@ -465,9 +466,12 @@ __device__ __forceinline__ void xch_plane(uint32_t (&v)[E], uint32_t (*xch)[64],
 //            waves waiting (the tables of a transform exceed the scalar cache);
 //   m = 512: 16 waves (128 registers each, no room for LDS-read tables), one
 //            workgroup per task, tables by scalar loads (A/B: faster here).
-template <int M>
-__global__ __launch_bounds__(M * 2, M == 256 ? 2 : 4) void enc16_kernel(Enc16 p) {
-    constexpr int WAVES = M / 32, E = 32, R = M / E;
+// E = 64 (m = 512 only, round 3q): 8 waves of 64 elements, 256 registers each (the
+// 16-wave form is held to 128 registers and spills 44 dwords per lane); the merged
+// middle pair is affordable there.
+template <int M, int E = 32>
+__global__ __launch_bounds__(M * 64 / E, M == 256 ? 2 : (E == 32 ? 4 : 1)) void enc16_kernel(Enc16 p) {
+    constexpr int WAVES = M / E, R = M / E;
     constexpr bool LDS_TAB = M == 256;
     constexpr int GT = WAVES * (E - 1) * kTabW;
     __shared__ uint32_t xch[M][64];
@@ -509,7 +513,11 @@ __global__ __launch_bounds__(M * 2, M == 256 ? 2 : 4) void enc16_kernel(Enc16 p)
             res_xform<E, R, false>(l, h, rtab);
             res_mid<E, R>(l, h, p.mid);
             res_xform<E, R, true>(l, h, rtab);
-        } else {  // m = 512: not merged (its 128-register form spills more with it: c5 0.58 -> 0.70 ms)
+        } else if constexpr (E == 64) {  // m = 512, 256 registers: the merged middle pair
+            res_xform_g<E, R, false, true>(l, h, p.tw, M - 1);
+            res_mid<E, R>(l, h, p.mid);
+            res_xform_g<E, R, true, true>(l, h, p.tw, 0);
+        } else {  // m = 512, 16 waves: not merged (its 128-register form spills more with it: c5 0.58 -> 0.70 ms)
             res_xform_g<E, R, false>(l, h, p.tw, M - 1);
             res_xform_g<E, R, true>(l, h, p.tw, 0);
         }
@@ -991,6 +999,14 @@ __global__ __launch_bounds__(1024) void errloc16g_kernel(G16Pass p) {
 
 inline uint32_t blocks_for(uint64_t tasks) { return (uint32_t)((tasks + 3) / 4); }
 
+// m = 512 encoder form: 16 waves x 32 elements (production) or 8 x 64 (diagnostic A/B)
+#ifdef RSM_DIAG
+static std::atomic<bool> g_enc16_e64{false};
+static bool enc16_e64() { return g_enc16_e64.load(); }
+#else
+static bool enc16_e64() { return false; }
+#endif
+
 template <int M>
 hipError_t run_encode(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st) {
     const uint32_t chunks = (cs.S + 511) / 512;
@@ -1006,6 +1022,12 @@ hipError_t run_encode(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st) {
     // m = 512: one workgroup per task (measured faster: the 16-wave form leaves no
     // registers for a persistent loop's state)
     const uint32_t grid = M == 256 && tasks > g.cus ? g.cus : (uint32_t)tasks;
+    if constexpr (M == 512) {
+        if (enc16_e64()) {
+            hipLaunchKernelGGL((enc16_kernel<512, 64>), dim3(grid), dim3(512), 0, st, p);
+            return hipGetLastError();
+        }
+    }
     hipLaunchKernelGGL(enc16_kernel<M>, dim3(grid), dim3(M * 2), 0, st, p);
     return hipGetLastError();
 }
@@ -1192,6 +1214,10 @@ static hipError_t run_decode_generic(const DecodeSet& ds, const Gf16Dev& g, hipS
     return hipSuccess;
 }
 }  // namespace
+
+#ifdef RSM_DIAG
+void set_enc16_diag_e64(bool on) { g_enc16_e64.store(on); }
+#endif
 
 hipError_t launch_encode_gf16(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st) {
     switch (ceil_pow2(cs.k)) {

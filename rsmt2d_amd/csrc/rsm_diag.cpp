@@ -69,6 +69,11 @@ int rsm_diag_set_split_fused(int on) {
     return RSM_OK;
 }
 
+int rsm_diag_set_enc16_e64(int on) {
+    set_enc16_diag_e64(on != 0);
+    return RSM_OK;
+}
+
 int rsm_diag_set_dec_trace(void* d_trace) {
     set_dec_diag_trace(static_cast<uint32_t*>(d_trace));
     return RSM_OK;

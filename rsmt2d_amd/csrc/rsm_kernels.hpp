@@ -77,6 +77,7 @@ hipError_t launch_decode_gf8(const DecodeSet& ds, hipStream_t st);
 hipError_t launch_encode_gf8_split(const CodewordSet& a, const CodewordSet* b, hipStream_t st);
 void set_split_diag_waves(int first, int second);  // diagnostic builds only
 void set_split_diag_fused(bool on);                  // diagnostic builds only
+void set_enc16_diag_e64(bool on);                    // diagnostic builds only
 bool split_fused_enabled();                          // product: always
 // One square in ONE launch of the split encoder (rows -> Q1, Q0 columns -> Q2, then
 // Q1 columns -> Q3 behind a device-side wait on the row tasks); ctr: >= 33 zeroed

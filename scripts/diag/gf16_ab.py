@@ -1,0 +1,59 @@
+"""GF(2^16) encoder A/B (diagnostic library): device time per c5 square (k = 512,
+S = 512) and per c4 square (k = 256, S = 2048) with the m = 512 encoder as 8 waves x
+64 elements or 16 x 32 (rsm_diag_set_enc16_e64); the c5 output is checked against
+the other form's.  One JSON line per configuration.
+usage: python3 scripts/diag/gf16_ab.py"""
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+
+import rsmt2d_amd as R  # noqa: E402
+
+D = R.diag_library()
+
+
+def chk(rc):
+    R._check_with(D, rc)
+
+
+def main():
+    ctx = ctypes.c_void_p()
+    chk(D.rsm_ctx_create(0, ctypes.byref(ctx)))
+    e0, e1 = ctypes.c_void_p(), ctypes.c_void_p()
+    chk(D.rsm_event_create(ctx, ctypes.byref(e0)))
+    chk(D.rsm_event_create(ctx, ctypes.byref(e1)))
+    k, S = 512, 512
+    n = (2 * k) ** 2 * S
+    p = ctypes.c_void_p()
+    chk(D.rsm_dev_alloc(ctx, n, ctypes.byref(p)))
+    outs = {}
+    for rep in range(2):
+        for e64 in (1, 0):
+            chk(D.rsm_diag_set_enc16_e64(e64))
+            chk(D.rsm_dev_fill_random(ctx, p.value, n, 7))
+            chk(D.rsm_extend_squares_dev(ctx, p.value, k, S, 1, None))
+            chk(D.rsm_sync(ctx))
+            out = np.empty(n, np.uint8)
+            chk(D.rsm_memcpy(ctx, out.ctypes.data, p.value, n, 1))
+            outs[e64] = out
+            reps = 20
+            chk(D.rsm_event_record(ctx, e0, None))
+            for _ in range(reps):
+                chk(D.rsm_extend_squares_dev(ctx, p.value, k, S, 1, None))
+            chk(D.rsm_event_record(ctx, e1, None))
+            chk(D.rsm_sync(ctx))
+            ms = ctypes.c_float()
+            chk(D.rsm_event_elapsed_ms(e0, e1, ctypes.byref(ms)))
+            print(json.dumps({"e64": e64, "rep": rep, "c5_ms_per_square": round(ms.value / reps, 4),
+                              "same_output": bool(np.array_equal(outs[e64], outs[1 - e64])) if 1 - e64 in outs
+                              else None}), flush=True)
+    chk(D.rsm_diag_set_enc16_e64(0))
+
+
+if __name__ == "__main__":
+    main()
