@@ -446,8 +446,8 @@ __global__ __launch_bounds__(64) void decode_gf8_kernel(DecodeSet ds) {
 // The derivative (closed form out[e] = in[e] ^ XOR_{t: e_t = 0} in[e + 2^t], see
 // derivative_half) needs, in L, the partners across the low log2(NW) bits from
 // the other waves: all waves publish their post-IFFT points to LDS once, then each
-// adds the (original) partner values.  LDS: [256 points][64 lanes] dwords = 64 KiB,
-// so two workgroups share a CU.  Production NW = 16 (8 waves per SIMD: the
+// adds the (original) partner values.  LDS: [256 points][64 lanes] dwords = 64 KiB
+// + 15 KiB of multiply tables, so two workgroups share a CU (158 of 160 KiB).  Production NW = 16 (8 waves per SIMD: the
 // shift/and/perm/xor chains of the byte-table multiplies need the latency cover;
 // c3 sweep 42.5 / 33.7 / 32.0 us at NW = 4 / 8 / 16).
 // ---------------------------------------------------------------------------
@@ -526,7 +526,7 @@ __device__ __forceinline__ void dec_stamp(const DecodeSet& ds, int i) {
 
 template <int NW, bool ZC>
 __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t task, uint32_t (&xch)[256][64],
-                                                  uint32_t (&erl)[2][256], PermTab (&stab)[257]) {
+                                                  PermTab (&ptab)[2][256], PermTab (&stab)[257]) {
     constexpr int PW = 256 / NW, HALF = NW / 2;
     if constexpr (!ZC) dec_stamp(ds, 0);
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -607,7 +607,8 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
     if constexpr (ZC) load_points(have);
 
     // error locator (log domain), as decode_gf8_kernel: entries 4 lane .. 4 lane + 3;
-    // wave 0 alone: it writes each point's log multiplier (erl), and every wave then reads
+    // wave 0 alone: it resolves each point's multiply table (ptab: the staged table of
+    // exp(err) / exp(-err), so every wave's per-point multiply is ONE uniform LDS read)
     // the staged table of its own points
     if (w == 0) {
         uint32_t er[4];
@@ -629,8 +630,8 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
             const uint32_t e = lane * 4u + j;  // point e: a present, valid input?
             const uint32_t i = e < 128u ? e : e - 128u;
             const bool in = i < k && present(e < 128u ? k + e : i);
-            erl[0][e] = in ? er[j] : 256u;  // scale by exp(err), 256: absent -> 0
-            erl[1][e] = 255u - er[j];       // reveal
+            ptab[0][e] = stab[in ? er[j] : 256u];  // scale by exp(err), 256: absent -> 0
+            ptab[1][e] = stab[255u - er[j]];       // reveal
         }
     }
     if constexpr (ZC) {  // the present cells also land in the device square
@@ -646,7 +647,7 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
     // 1. S layout: scale every point by the error locator (absent -> 0)
     static_for<PW>([&](auto J) {
         constexpr int j = decltype(J)::value;
-        v[j] = gf8_mul_tab(v[j], stab[erl[0][PW * w + j]]);
+        v[j] = gf8_mul_tab(v[j], ptab[0][PW * w + j]);
     });
     // 2. IFFT layers 1..PW/2 (per-wave twiddles)
     split_low<NW, PW, false>(v, w);
@@ -694,7 +695,7 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
         constexpr int j = decltype(J)::value;
         const uint32_t e = PW * w + j;
         const uint32_t so = ((reveal >> j) & 1ull) ? sbase + (uint32_t)j * sstep : kOob;
-        const uint32_t x = gf8_mul_tab(v[j], stab[erl[1][e]]);
+        const uint32_t x = gf8_mul_tab(v[j], ptab[1][e]);
         __builtin_amdgcn_raw_buffer_store_b32(x, rs, off, so, 0);
         if (mirror) __builtin_amdgcn_raw_buffer_store_b32(x, rm, off, so, 0);
     });
@@ -707,21 +708,21 @@ constexpr int kSplitWaves = 16;
 template <int NW>
 __global__ __launch_bounds__(64 * NW, NW / 2) void decode_gf8_split_kernel(DecodeSet ds) {
     __shared__ uint32_t xch[256][64];
-    __shared__ uint32_t erl[2][256];
+    __shared__ PermTab ptab[2][256];
     __shared__ PermTab stab[257];
-    decode_split_task<NW, false>(ds, blockIdx.x, xch, erl, stab);
+    decode_split_task<NW, false>(ds, blockIdx.x, xch, ptab, stab);
 }
 
 // zero-copy form: a capped grid loops over the tasks
 template <int NW>
 __global__ __launch_bounds__(64 * NW, NW / 2) void decode_gf8_split_zc_kernel(DecodeSet ds) {
     __shared__ uint32_t xch[256][64];
-    __shared__ uint32_t erl[2][256];
+    __shared__ PermTab ptab[2][256];
     __shared__ PermTab stab[257];
     const uint32_t tasks = ds.count * ds.chunks;
     for (uint32_t task = blockIdx.x; task < tasks; task += gridDim.x) {
-        decode_split_task<NW, true>(ds, __builtin_amdgcn_readfirstlane(task), xch, erl, stab);
-        __syncthreads();  // LDS (xch, erl, stab) is reused by the next task
+        decode_split_task<NW, true>(ds, __builtin_amdgcn_readfirstlane(task), xch, ptab, stab);
+        __syncthreads();  // LDS (xch, ptab, stab) is reused by the next task
     }
 }
 
