@@ -21,8 +21,15 @@ struct alignas(16) PermTab16 {
 // dependent skew lookup and no branch.  Indices < kSkewPermN cover m <= 1024.
 constexpr uint32_t kSkewPermN = 2048;
 
+// The device LogWalsh buffer holds the 65536-entry table, then at kLwFoldOff + N - 512
+// the table folded to N = 512 .. 32768 points: fold_N[r] = sum_q logwalsh[qN + r] (mod
+// 65535), which the decoders' N-point error locators use (kernels_gf16.hip; N = 65536
+// reads the table itself).
+constexpr uint32_t kLwFoldOff = 65536;
+
 struct Gf16Host {
     std::vector<uint16_t> exp, log, skew, logwalsh;
+    std::vector<uint16_t> lwfold;     // fold_512, fold_1024, ..., fold_32768
     std::vector<PermTab16> perm;      // 65536 entries
     std::vector<PermTab16> skewperm;  // kSkewPermN entries
 };

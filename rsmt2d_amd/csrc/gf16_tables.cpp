@@ -74,6 +74,14 @@ const Gf16Host& gf16_host() {
                     t.logwalsh[i] = (uint16_t)add_mod(a, b);
                     t.logwalsh[i + dist] = (uint16_t)sub_mod(a, b);
                 }
+        // LogWalsh folded to N points (gf16.hpp kLwFoldOff)
+        t.lwfold.assign(kOrder - 512, 0);
+        for (unsigned N = 512; N < kOrder; N <<= 1)
+            for (unsigned r = 0; r < N; ++r) {
+                unsigned s = 0;
+                for (unsigned q = r; q < kOrder; q += N) s = add_mod(s, t.logwalsh[q]);
+                t.lwfold[N - 512 + r] = (uint16_t)s;
+            }
         // v_perm tables: PermTab16 per log value L
         t.perm.assign(kOrder, PermTab16{});
         for (unsigned L = 0; L < kOrder; ++L) {

@@ -569,44 +569,48 @@ __device__ __forceinline__ uint64_t cell_of(const DecodeSet& ds, uint32_t q, uin
     return ds.axis == 0 ? vec * W + e : (uint64_t)e * W + vec;
 }
 
-// Error locator of one codeword (klauspost reconstruct): FWHT over the
-// full 65536-entry table in LDS, times LogWalsh, FWHT again; writes err[0..n).
+// Error locator of one codeword (klauspost reconstruct, SURVEY A.5: FWHT of the
+// erasure indicator over all 65536 entries, times LogWalsh, FWHT again; err[0..N)),
+// computed on N = 2M points.  The indicator is zero past N, so the first 65536-point
+// FWHT is its N-point FWHT repeated 65536 / N times (the layers d >= N add zeros:
+// a + 0, a - 0), and outputs j < N of the second only see i mod N (popcount(i & j) =
+// popcount((i mod N) & j)): err = FWHT_N(FWHT_N(ind) * fold_N) with fold_N[r] =
+// sum_q LogWalsh[qN + r] (host table, gf16.hpp kLwFoldOff).  The same residues mod
+// 65535 as the full transforms; a result of 0 may come out as 65535 (or back), which
+// every consumer reads alike (perm[65535] == perm[0]: exp(65535) = exp(0)).
+// 2 x log2(N) layers of N / 2 butterflies instead of 2 x 16 x 32768.
 template <int M>
-__global__ __launch_bounds__(1024) void errloc16_kernel(Dec16 p) {
+__global__ __launch_bounds__(M) void errloc16_kernel(Dec16 p) {
     constexpr int N = 2 * M;
-    __shared__ uint16_t err[65536];
+    __shared__ uint32_t err[N];
     const uint32_t q = blockIdx.x;
     const uint32_t k = p.ds.k;
-#pragma unroll 2
-    for (uint32_t i = threadIdx.x; i < 65536u; i += 1024u) {
+    for (uint32_t i = threadIdx.x; i < (uint32_t)N; i += M) {
         uint32_t v = 0;
         if (i < k) v = p.ds.presence[cell_of(p.ds, p.q0 + q, k + i)] ? 0u : 1u;
         else if (i < (uint32_t)M) v = 1u;
         else if (i < (uint32_t)M + k) v = p.ds.presence[cell_of(p.ds, p.q0 + q, i - M)] ? 0u : 1u;
-        err[i] = (uint16_t)v;
+        err[i] = v;
     }
     __syncthreads();
+    const uint16_t* fold = p.logwalsh + kLwFoldOff + (N - 512);
 #pragma unroll 1
     for (int pass = 0; pass < 2; ++pass) {
-#pragma unroll 1
-        for (uint32_t d = 1; d < 65536u; d <<= 1) {
-#pragma unroll 4
-            for (uint32_t b = threadIdx.x; b < 32768u; b += 1024u) {
-                const uint32_t i = (b / d) * 2 * d + (b % d);
-                const uint32_t a = err[i], c = err[i + d];
-                err[i] = (uint16_t)addm(a, c);
-                err[i + d] = (uint16_t)subm(a, c);
-            }
+#pragma unroll
+        for (uint32_t d = 1; d < (uint32_t)N; d <<= 1) {
+            const uint32_t b = threadIdx.x;  // one butterfly per thread
+            const uint32_t i = (b / d) * 2 * d + (b % d);
+            const uint32_t a = err[i], c = err[i + d];
+            err[i] = addm(a, c);
+            err[i + d] = subm(a, c);
             __syncthreads();
         }
         if (pass == 0) {
-#pragma unroll 4
-            for (uint32_t i = threadIdx.x; i < 65536u; i += 1024u)
-                err[i] = (uint16_t)(((uint32_t)err[i] * p.logwalsh[i]) % kMod16);
+            for (uint32_t i = threadIdx.x; i < (uint32_t)N; i += M) err[i] = (err[i] * fold[i]) % kMod16;
             __syncthreads();
         }
     }
-    for (uint32_t i = threadIdx.x; i < (uint32_t)N; i += 1024u) p.errs[(uint64_t)q * N + i] = err[i];
+    for (uint32_t i = threadIdx.x; i < (uint32_t)N; i += M) p.errs[(uint64_t)q * N + i] = (uint16_t)err[i];
 }
 
 __device__ __forceinline__ uint32_t err_of(const Dec16& p, uint32_t q, uint32_t i, uint32_t n) {
@@ -960,13 +964,15 @@ __global__ __launch_bounds__(256) void g16_deriv_kernel(G16Pass p) {
     });
 }
 
-// Error locator for any m (the m <= 512 kernel with m a runtime value).
+// Error locator for any m: the m <= 512 kernel with n = npts = 2m a runtime value
+// (n <= 65536; n = 65536 folds nothing: the table itself).
 __global__ __launch_bounds__(1024) void errloc16g_kernel(G16Pass p) {
     __shared__ uint16_t err[65536];
     const uint32_t qi = blockIdx.x, q = p.q0 + qi;
-    const uint32_t k = p.k, M = p.m;
+    const uint32_t k = p.k, M = p.m, n = p.npts;
+    const uint16_t* fold = n >= 65536u ? p.logwalsh : p.logwalsh + kLwFoldOff + (n - 512u);
 #pragma unroll 2
-    for (uint32_t i = threadIdx.x; i < 65536u; i += 1024u) {
+    for (uint32_t i = threadIdx.x; i < n; i += 1024u) {
         uint32_t v = 0;
         if (i < k) v = p.ds.presence[cell_of(p.ds, q, k + i)] ? 0u : 1u;
         else if (i < M) v = 1u;
@@ -977,9 +983,9 @@ __global__ __launch_bounds__(1024) void errloc16g_kernel(G16Pass p) {
 #pragma unroll 1
     for (int pass = 0; pass < 2; ++pass) {
 #pragma unroll 1
-        for (uint32_t d = 1; d < 65536u; d <<= 1) {
+        for (uint32_t d = 1; d < n; d <<= 1) {
 #pragma unroll 4
-            for (uint32_t b = threadIdx.x; b < 32768u; b += 1024u) {
+            for (uint32_t b = threadIdx.x; b < n / 2u; b += 1024u) {
                 const uint32_t i = (b / d) * 2 * d + (b % d);
                 const uint32_t a = err[i], c = err[i + d];
                 err[i] = (uint16_t)addm(a, c);
@@ -989,12 +995,12 @@ __global__ __launch_bounds__(1024) void errloc16g_kernel(G16Pass p) {
         }
         if (pass == 0) {
 #pragma unroll 4
-            for (uint32_t i = threadIdx.x; i < 65536u; i += 1024u)
-                err[i] = (uint16_t)(((uint32_t)err[i] * p.logwalsh[i]) % kMod16);
+            for (uint32_t i = threadIdx.x; i < n; i += 1024u)
+                err[i] = (uint16_t)(((uint32_t)err[i] * fold[i]) % kMod16);
             __syncthreads();
         }
     }
-    for (uint32_t i = threadIdx.x; i < p.npts; i += 1024u) p.errs_out[(uint64_t)qi * p.npts + i] = err[i];
+    for (uint32_t i = threadIdx.x; i < n; i += 1024u) p.errs_out[(uint64_t)qi * n + i] = err[i];
 }
 
 inline uint32_t blocks_for(uint64_t tasks) { return (uint32_t)((tasks + 3) / 4); }
@@ -1044,7 +1050,7 @@ hipError_t run_decode(const DecodeSet& ds, const Gf16Dev& g, const uint16_t* log
     for (uint32_t q0 = 0; q0 < ds.count; q0 += batch) {
         Dec16 p{ds, Res{g.perm, g.skew}, logwalsh, g.errs, g.scratch, q0,
                 ds.count - q0 < batch ? ds.count - q0 : batch, chunks};
-        hipLaunchKernelGGL(errloc16_kernel<M>, dim3(p.count), dim3(1024), 0, st, p);
+        hipLaunchKernelGGL(errloc16_kernel<M>, dim3(p.count), dim3(M), 0, st, p);
         hipLaunchKernelGGL(dec16_p1<M>, dim3(blocks_for((uint64_t)p.count * chunks * (N / 16))), dim3(256), 0, st, p);
         hipLaunchKernelGGL(dec16_p2<M>, dim3(blocks_for((uint64_t)p.count * chunks * 16)), dim3(256), 0, st, p);
         hipLaunchKernelGGL(dec16_p3<M>, dim3(blocks_for((uint64_t)p.count * chunks * (N / 16))), dim3(256), 0, st, p);

@@ -167,7 +167,7 @@ int ensure_gf16_tables(rsm_ctx* ctx) {
     std::lock_guard<std::mutex> lk(ctx->gf16_mu);
     if (ctx->gf16_ready) return RSM_OK;
     const Gf16Host& t = gf16_host();
-    const size_t pb = t.perm.size() * sizeof(PermTab16), sb = t.skew.size() * 2, lb = t.logwalsh.size() * 2;
+    const size_t pb = t.perm.size() * sizeof(PermTab16), sb = t.skew.size() * 2, lb = (kLwFoldOff + t.lwfold.size()) * 2;
     const size_t kb = t.skewperm.size() * sizeof(PermTab16);
     hipError_t e;
     if ((e = ctx->gf16_perm.ensure(pb)) != hipSuccess || (e = ctx->gf16_skew.ensure(sb)) != hipSuccess ||
@@ -175,7 +175,9 @@ int ensure_gf16_tables(rsm_ctx* ctx) {
         return hip_fail(e, "hipMalloc (GF16 tables)");
     if ((e = hipMemcpy(ctx->gf16_perm.ptr, t.perm.data(), pb, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipMemcpy(ctx->gf16_skew.ptr, t.skew.data(), sb, hipMemcpyHostToDevice)) != hipSuccess ||
-        (e = hipMemcpy(ctx->gf16_logwalsh.ptr, t.logwalsh.data(), lb, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(ctx->gf16_logwalsh.ptr, t.logwalsh.data(), kLwFoldOff * 2, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(static_cast<uint16_t*>(ctx->gf16_logwalsh.ptr) + kLwFoldOff, t.lwfold.data(),
+                       t.lwfold.size() * 2, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipMemcpy(ctx->gf16_skewperm.ptr, t.skewperm.data(), kb, hipMemcpyHostToDevice)) != hipSuccess)
         return hip_fail(e, "upload GF16 tables");
     ctx->gf16.skewperm = static_cast<const PermTab16*>(ctx->gf16_skewperm.ptr);
