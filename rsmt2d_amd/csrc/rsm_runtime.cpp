@@ -615,15 +615,18 @@ int rsm_codec_validate_chunk_size(int64_t share_size) { return validate_chunk_si
 int rsm_codec_field_bits(uint32_t k) { return field_bits(k); }
 
 // Device address of a lane's pinned staging: the Codec calls of GF(2^8) codewords with
-// 65 <= k <= 128 run zero-copy -- the kernel reads the shares from the pinned buffer
-// over PCIe and writes its results back there (one launch and one stream wait per
-// call, no DMA copies); nullptr where the runtime cannot map it (the copy path then).
+// 65 <= k <= 128 and of GF(2^16) codewords with k <= 512 (the single-pass kernels) run
+// zero-copy -- the kernels read the shares from the pinned buffer over PCIe and write
+// their results back there (no DMA copies; the GF(2^16) decoder's intermediate passes
+// stay in device scratch); nullptr where the runtime cannot map it (the copy path then).
 static void* lane_host_dev(Lane& L) {
     void* p = nullptr;
     if (hipHostGetDevicePointer(&p, L.host.ptr, 0) != hipSuccess) return nullptr;
     return p;
 }
-static bool codec_zero_copy(uint32_t k) { return field_bits(k) == 8 && ceil_pow2(k) == 128; }
+static bool codec_zero_copy(uint32_t k) {
+    return (field_bits(k) == 8 && ceil_pow2(k) == 128) || (field_bits(k) == 16 && !gf16_generic(k));
+}
 
 int rsm_encode(rsm_ctx* ctx, const uint8_t* const* data, uint32_t k, uint32_t share_size,
                uint8_t* const* parity) {
@@ -646,8 +649,9 @@ int rsm_encode(rsm_ctx* ctx, const uint8_t* const* data, uint32_t k, uint32_t sh
     for (uint32_t i = 0; i < k; ++i) memcpy(h + i * S, data[i], S);
     if (codec_zero_copy(k))
         if (uint8_t* hd = static_cast<uint8_t*>(lane_host_dev(L))) {
-            // latency form (the split byte-table encoder: one 8-wave workgroup per 256-B
-            // chunk) straight on the pinned buffer
+            // GF(2^8): the latency form (the split byte-table encoder: one 8-wave
+            // workgroup per 256-B chunk); GF(2^16): the single-pass encoder -- straight on
+            // the pinned buffer
             CodewordSet cs{};
             cs.base = cs.out_base = hd;
             cs.elem_stride = S;
@@ -657,7 +661,12 @@ int rsm_encode(rsm_ctx* ctx, const uint8_t* const* data, uint32_t k, uint32_t sh
             cs.k = k;
             cs.S = share_size;
             cs.pass = 1;
-            if ((e = launch_encode_gf8_split(cs, nullptr, L.stream)) != hipSuccess) return hip_fail(e, "encode kernel launch");
+            if (field_bits(k) == 8) {
+                if ((e = launch_encode_gf8_split(cs, nullptr, L.stream)) != hipSuccess)
+                    return hip_fail(e, "encode kernel launch");
+            } else if (int rc = launch_encode(ctx, cs, L.stream)) {
+                return rc;
+            }
             if ((e = hipStreamSynchronize(L.stream)) != hipSuccess) return hip_fail(e, "encode");
             for (uint32_t i = 0; i < k; ++i) memcpy(parity[i], h + (k + i) * S, S);
             return RSM_OK;
@@ -713,8 +722,8 @@ int rsm_decode(rsm_ctx* ctx, uint8_t* const* shares, const uint8_t* present, uin
     for (uint32_t i = 0; i < n; ++i) hp[i] = present[i] ? 1 : 0;
     if (codec_zero_copy(k))
         if (uint8_t* hd = static_cast<uint8_t*>(lane_host_dev(L))) {
-            // the split decoder straight on the pinned buffer: it reads every point and
-            // the presence bytes over PCIe and writes only the missing shares back
+            // the decoder straight on the pinned buffer: it reads the points and the
+            // presence bytes over PCIe and writes only the missing shares back
             DecodeSet ds{};
             ds.base = hd;
             ds.presence = hd + bytes;
