@@ -889,7 +889,7 @@ def main():
     pmc_path = os.path.join(ROOT, "profiles", "pmc_latest.json")
     if bitsliced and os.path.exists(pmc_path):
         if single:
-            want = "extend_gf8_bs128s_kernel<0>"
+            want = "extend_gf8_bs128s_kernel<"  # any mode (production: <16777216>, fixed lane offsets)
             sets = 3 * k * B * S // 2048
         else:
             want = "encode_gf8_bs128u_kernel<%d, %d>" % ((184, 1) if col_dom else (104, 0))
