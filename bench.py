@@ -8,10 +8,9 @@ A "step" = ComputeExtendedDataSquare's arithmetic (erasureExtendSquare,
 extendeddatasquare.go:154-227) over one batch of `--batch` independent squares
 already resident in HBM (the EDS buffer holds each ODS in its top-left quadrant,
 as the Go EDS aliases its input).  c2 default: 256 squares (8 GiB of EDS) per step
-as ONE queue-driven launch (both passes, extend_gf8_bs128q_kernel), steps rotating
-over 3 streams and 3 buffers (24 GiB of the 288 GB), so no step finds its squares in
-the 256 MiB Infinity Cache.  (Per launch the schedule pays ~64 us of start-up and tail:
-8.84 / 8.68 / 8.59 us per square at 128 / 192 / 256 squares, profiles/r02g_queue_ab.jsonl.)
+as ONE queue-driven launch (both passes, extend_gf8_bs128s_kernel: half-split
+bit-sliced sets), steps rotating over 3 streams and 3 buffers
+(24 GiB of the 288 GB), so no step finds its squares in the 256 MiB Infinity Cache.
 value = ODS bytes encoded per second over all ranks (GiB/s).
 
 N > 1 GPUs (one process per GPU, torch.distributed): every rank encodes its own
@@ -20,7 +19,8 @@ exchange, so scaling is "weak".
 
 Extra JSON objects: "roofline" (dominant kernel, HIP-event timed on the launch
 stream), "step_roofline" (whole 2D encode vs SURVEY's algorithmic bytes 4k^2 S),
-"cpu_baseline" (AVX2 restatement of the reference path -- kind "port" -- on this host's cores),
+"cpu_baseline" (the C restatement of the reference path -- AVX-512 + GFNI where the host has
+it, else AVX2 -- kind "port", on every CPU this process may run on: sched_getaffinity),
 "host_path" (PCIe-inclusive rates, pinned+overlapped and pageable; never `value`),
 "codec" (per-codeword Encode latency and 64-thread concurrent rate).
 """
@@ -97,14 +97,18 @@ def cpu_baseline(k, S, seconds):
     GF2P8AFFINEQB multiplies, fused butterflies -- libleopard_gfni.so; else the AVX2
     pshufb build), multithreaded over codewords with the reference's two-phase
     schedule, writing into a reused EDS buffer (no page faults in the timed loop).
-    Threads: this job's CPU share on the GPU box (16 per GPU: the harness sizes every
-    worker pool to it; os.cpu_count() reports the whole machine); the single-thread
-    rate is reported beside it.  Not the reference: its Go/klauspost code cannot run
-    here."""
+    Threads: one per CPU of this process's affinity mask (os.sched_getaffinity -- the
+    CPUs the job may actually run on; os.cpu_count() is the whole machine); the mask is
+    recorded, and the single-thread rate plus its linear all-host-CPUs extrapolation are
+    reported beside it.  Not the reference: its Go/klauspost code cannot run here."""
     import numpy as np
     import oracle
     ncpu = os.cpu_count() or 1
-    threads = min(16, ncpu)
+    try:
+        mask = sorted(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        mask = list(range(ncpu))
+    threads = max(1, len(mask))
     gfni = oracle.gfni_supported() and k <= 128
     ext = oracle.extend_square_gfni if gfni else oracle.extend_square_simd if k <= 128 else None
     ods = oracle.splitmix64_bytes(k * k * S).reshape(k, k, S)
@@ -144,14 +148,25 @@ def cpu_baseline(k, S, seconds):
     tech = ("AVX-512 + GFNI (GF2P8AFFINEQB multiplies, fused butterflies)" if gfni
             else "AVX2 pshufb nibble tables" if ext else "scalar tables")
     return {"value": round(n * k * k * S / dt / 2**30, 4), "unit": "GiB/s", "cores": threads,
-            "kind": "port", "cpu_model": model, "host_cpus": ncpu,
+            "kind": "port", "cpu_model": model, "host_cpus": ncpu, "affinity": _ranges(mask),
             "single_thread_GiB_s": round(n1 * k * k * S / dt1 / 2**30, 4),
             "all_cores_estimate_GiB_s": round(n1 * k * k * S / dt1 / 2**30 * ncpu, 1),
             "sample": f"{n} squares k={k} S={S} ({dt:.1f} s) through oracle/leopard_oracle.c ({tech}; restatement "
-                      f"of klauspost leopard8, not the reference), {threads} threads each extending whole squares = "
-                      f"this job's CPU share of the {ncpu}-CPU host; single thread: {n1} squares in {dt1:.1f} s; "
-                      f"all_cores_estimate = single-thread rate x {ncpu} (linear, not measured: the box's share is "
-                      f"{threads} CPUs)"}
+                      f"of klauspost leopard8, not the reference), {threads} threads (one per CPU of the affinity "
+                      f"mask) each extending whole squares; single thread: {n1} squares in {dt1:.1f} s; "
+                      f"all_cores_estimate = single-thread rate x {ncpu} host CPUs (linear, not measured)"}
+
+
+def _ranges(cpus):
+    """[0, 1, 2, 5] -> "0-2,5" (an affinity mask as taskset prints it)."""
+    out, i = [], 0
+    while i < len(cpus):
+        j = i
+        while j + 1 < len(cpus) and cpus[j + 1] == cpus[j] + 1:
+            j += 1
+        out.append(str(cpus[i]) if i == j else f"{cpus[i]}-{cpus[j]}")
+        i = j + 1
+    return ",".join(out)
 
 
 def pct(xs, q):
@@ -304,6 +319,110 @@ def bench_host_path(local, L, R, k, S, squares=8, seconds=2.0):
                     "D2H of different squares overlap; Q0 is not copied back); pageable = rsm_extend_square per square"}
 
 
+def bench_c5_c_abi(G, L, R, steps, k=512, S=512):
+    """Config 5 through the C ABI a cgo ComputeExtendedDataSquare would call
+    (rsm_multi_*: ONE process drives all G GPUs, an RCCL clique from ncclCommInitAll,
+    extendeddatasquare.go:50-77): (1) device-resident rsm_multi_extend_dev (row pass of
+    each GPU's k/G rows, RCCL exchange, column pass of its 2k/G columns; per-GPU HIP
+    events on the context streams, the slowest GPU's span), both schedules; (2) host to
+    host from a pinned arena (rsm_multi_extend_square_inplace on rsm_multi_host_alloc
+    memory: Q0 rows up, Q1 rows and the bottom-half column slice down, one DMA each per
+    GPU) and from pageable numpy memory (rsm_multi_extend_square); the pinned EDS is
+    checked against the oracle at G = 1 and through the square's parity identity (every
+    column of the result re-encodes to itself: Q3 from Q1 columns) otherwise."""
+    import ctypes
+    import numpy as np
+    W = 2 * k
+    steps = max(3, min(steps, 10))
+    m = ctypes.c_void_p()
+    devs = (ctypes.c_int * G)(*range(G))
+    R._check(L.rsm_multi_create(devs, G, ctypes.byref(m)))
+    out = {"workload": f"c5 through the C ABI: one process, {G} GPU(s), RCCL clique (ncclCommInitAll)",
+           "n_gpus": G}
+    try:
+        ctxs = [L.rsm_multi_context(m, g) for g in range(G)]
+        bufs = []
+        for g in range(G):
+            p = ctypes.c_void_p()
+            R._check(L.rsm_dev_alloc(ctxs[g], W * W * S, ctypes.byref(p)))
+            R._check(L.rsm_dev_fill_random(ctxs[g], p, W * W * S, 0xC5C5 + g))
+            bufs.append(p.value)
+        arr = (ctypes.c_void_p * G)(*bufs)
+        ev = [[ctypes.c_void_p(), ctypes.c_void_p()] for _ in range(G)]
+        for g in range(G):
+            for e in ev[g]:
+                R._check(L.rsm_event_create(ctxs[g], ctypes.byref(e)))
+        for name, sched in (("allgather", 0), ("alltoall", 1)):
+            R._check(L.rsm_multi_extend_dev(m, arr, k, S, sched))  # warm (RCCL connections)
+            R._check(L.rsm_multi_sync(m))
+            t0 = time.perf_counter()
+            for g in range(G):
+                R._check(L.rsm_event_record(ctxs[g], ev[g][0], None))
+            for _ in range(steps):
+                R._check(L.rsm_multi_extend_dev(m, arr, k, S, sched))
+            for g in range(G):
+                R._check(L.rsm_event_record(ctxs[g], ev[g][1], None))
+            R._check(L.rsm_multi_sync(m))
+            wall = (time.perf_counter() - t0) / steps
+            spans = []
+            ms = ctypes.c_float()
+            for g in range(G):
+                R._check(L.rsm_event_elapsed_ms(ev[g][0], ev[g][1], ctypes.byref(ms)))
+                spans.append(ms.value / steps)
+            dt = max(spans) / 1e3
+            out[f"dev_{name}_ms_per_square"] = round(dt * 1e3, 4)
+            out[f"dev_{name}_ods_GiB_s"] = round(k * k * S / dt / 2**30, 3)
+            out[f"dev_{name}_host_wall_ms"] = round(wall * 1e3, 4)
+        for g in range(G):
+            for e in ev[g]:
+                L.rsm_event_destroy(e)
+            R._check(L.rsm_dev_free(ctxs[g], ctypes.c_void_p(bufs[g])))
+        # host to host: pinned in place, then pageable
+        import oracle
+        ods = oracle.splitmix64_bytes(k * k * S, seed=0xC5).reshape(k, k, S)
+        hp = ctypes.c_void_p()
+        R._check(L.rsm_multi_host_alloc(m, W * W * S, ctypes.byref(hp)))
+        try:
+            eds = np.ctypeslib.as_array((ctypes.c_uint8 * (W * W * S)).from_address(hp.value)).reshape(W, W, S)
+            eds[:k, :k] = ods
+            R._check(L.rsm_multi_extend_square_inplace(m, hp, k, S, 1))
+            if G == 1:
+                ok = np.array_equal(eds, oracle.extend_square(ods, nthreads=16))
+            else:
+                # rows of the result re-encode to themselves (an independent check of Q1 and,
+                # with the column identity below, of Q2/Q3) -- the oracle's whole square
+                # takes ~1 s of host CPU per 16 threads, spent once at G = 1
+                def reenc(v):  # the parity half the oracle's Encode gives for the first half of v
+                    return np.frombuffer(b"".join(oracle.encode(list(v[:k]))), np.uint8).reshape(k, S)
+                ok = all(np.array_equal(reenc(eds[r]), eds[r, k:]) for r in (0, k - 1, k, W - 1)) and \
+                    all(np.array_equal(reenc(eds[:, c]), eds[k:, c]) for c in (0, W - 1))
+            if not ok:
+                raise SystemExit("bench c5 c_abi: pinned in-place EDS differs from the oracle")
+            t0 = time.perf_counter()
+            for _ in range(3):
+                R._check(L.rsm_multi_extend_square_inplace(m, hp, k, S, 1))
+            pinned = (time.perf_counter() - t0) / 3
+        finally:
+            R._check(L.rsm_multi_host_free(m, hp))
+        e2 = np.empty((W, W, S), np.uint8)
+        R._check(L.rsm_multi_extend_square(m, ods.ctypes.data, k, S, e2.ctypes.data, 1))
+        t0 = time.perf_counter()
+        for _ in range(3):
+            R._check(L.rsm_multi_extend_square(m, ods.ctypes.data, k, S, e2.ctypes.data, 1))
+        pageable = (time.perf_counter() - t0) / 3
+        pcie = k * k * S + 3 * k * k * S
+        out["pinned_host_ms_per_square"] = round(pinned * 1e3, 3)
+        out["pinned_host_pcie_GB_s"] = round(pcie / pinned / 1e9, 2)
+        out["pageable_host_ms_per_square"] = round(pageable * 1e3, 3)
+        out["pcie_bytes_per_square"] = pcie
+        out["note"] = ("dev_* = rsm_multi_extend_dev (device-resident, slowest GPU's event span); pinned = "
+                       "rsm_multi_extend_square_inplace on an rsm_multi_host_alloc arena (all-to-all schedule; Q0 up, "
+                       "Q1..Q3 down: pcie_bytes over all GPUs' links); pageable = rsm_multi_extend_square")
+    finally:
+        L.rsm_multi_destroy(m)
+    return out
+
+
 def bench_c5(world, rank, local, dist, steps, L, R):
     """Config 5: one 512x512 -> 1024x1024 square (GF(2^16), 512 B shares).  N=1: the
     whole square on one GPU; N>1: rows sharded over the N GPUs, then an RCCL
@@ -325,23 +444,8 @@ def bench_c5(world, rank, local, dist, steps, L, R):
         R._check(L.rsm_sync(ctx))
         dt = (time.perf_counter() - t0) / steps
         buf.free()
-        # the C-ABI multi-GPU entry point (rsm_multi_extend_square) with a clique of one,
-        # host memory to host memory, both exchange schedules
-        import ctypes
-        import numpy as np
-        m = ctypes.c_void_p()
-        devs = (ctypes.c_int * 1)(local)
-        R._check(L.rsm_multi_create(devs, 1, ctypes.byref(m)))
-        ods = np.random.default_rng(5).integers(0, 256, (k, k, S), dtype=np.uint8)
-        eds = np.empty((W, W, S), np.uint8)
-        multi = {}
-        for name, sched in (("allgather", 0), ("alltoall", 1)):
-            R._check(L.rsm_multi_extend_square(m, ods.ctypes.data, k, S, eds.ctypes.data, sched))
-            t1 = time.perf_counter()
-            for _ in range(3):
-                R._check(L.rsm_multi_extend_square(m, ods.ctypes.data, k, S, eds.ctypes.data, sched))
-            multi[name + "_host_ms"] = round((time.perf_counter() - t1) / 3 * 1e3, 3)
-        L.rsm_multi_destroy(m)
+        # the C-ABI multi-GPU entry point with a clique of one
+        multi = bench_c5_c_abi(1, L, R, steps)
     else:
         import torch
         from rsmt2d_amd.distributed import (RowShardedExtender, TransposeShardedExtender, hip_backend,
@@ -381,13 +485,31 @@ def bench_c5(world, rank, local, dist, steps, L, R):
         torch.cuda.synchronize()
         dt_ag = timed(lambda: ext.extend(eds))
         del eds
+        torch.cuda.synchronize()
+        # the C-ABI path a cgo caller uses (one process drives every GPU): rank 0 runs it
+        # over all `world` GPUs while the other ranks wait at a CPU (gloo) barrier, so no
+        # collective of theirs occupies the GPUs meanwhile
+        cpu_group = dist.new_group(backend="gloo")
+        c_abi = None
+        if rank == 0:
+            try:
+                if torch.cuda.device_count() < world:
+                    c_abi = {"error": f"rank 0 sees {torch.cuda.device_count()} of the {world} GPUs "
+                                      "(HIP_VISIBLE_DEVICES): the one-process clique cannot be formed"}
+                else:
+                    c_abi = bench_c5_c_abi(world, L, R, steps)
+            except Exception as e:  # noqa: BLE001 -- reported in the line, the headline stands
+                c_abi = {"error": f"{type(e).__name__}: {e}"}
+        dist.barrier(group=cpu_group)
     out = {"workload": "c5: 512x512->1024x1024 square, 512 B shares, GF(2^16)"
                        + ("" if world == 1 else f", rows sharded over {world} GPUs + RCCL all-to-all of column slices"),
            "n_gpus": world, "ms_per_square": round(dt * 1e3, 4), "ods_GiB_s": round(k * k * S / dt / 2**30, 3),
            "scaling": "strong (one square)"}
     if dist is None:
-        out["c_abi_multi_gpu_1"] = multi
+        out["c_abi"] = multi
     if dist is not None:
+        if rank == 0:
+            out["c_abi"] = c_abi
         out["received_bytes_per_gpu"] = (world - 1) * (k // world) * (W // world) * S
         out["allgather_ms_per_square"] = round(dt_ag * 1e3, 4)
         out["allgather_received_bytes_per_gpu"] = (world - 1) * (k // world) * W * S
@@ -555,14 +677,15 @@ def bench_single_square(local, L, R, k=128, S=512, reps=200):
                     "launch (rsm_ctx_set_split_max 0)"}
 
 
-def bench_c4(local, L, R, steps, B=2):
+def bench_c4(local, L, R, steps, B=2, k=256, S=2048):
     """Config 4: 256x256 -> 512x512 squares of 2048 B shares (GF(2^16), enc16_kernel<256>),
     device-resident, B squares (1 GiB of EDS) per step, steps alternating over two
-    buffers so no step finds its squares in the 256 MiB Infinity Cache."""
+    buffers so no step finds its squares in the 256 MiB Infinity Cache.  With S = 512
+    the same code times BenchmarkExtensionEncoding's own k = 256 shape
+    (extendeddatasquare_test.go:282-305, shareSize 512; B = 8 squares = 1 GiB)."""
     import ctypes
     import numpy as np
     import oracle
-    k, S = 256, 2048
     W = 2 * k
     sq = W * W * S
     ctx = R.device_context(local)
@@ -592,10 +715,11 @@ def bench_c4(local, L, R, steps, B=2):
     for b in bufs:
         b.free()
     algo = 4 * k * k * S * B
-    return {"workload": "c4: 256x256->512x512 squares, 2048 B shares, GF(2^16)", "squares_per_step": B,
+    return {"workload": (f"{'c4: ' if (k, S) == (256, 2048) else ''}{k}x{k}->{W}x{W} squares, {S} B shares, "
+                         "GF(2^16)"), "squares_per_step": B,
             "ms_per_square": round(dt / B * 1e3, 4), "ods_GiB_s": round(k * k * S * B / dt / 2**30, 3),
             "frac": round(algo / dt / 1e9 / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_square": 4 * k * k * S,
-            "kernel": "enc16_kernel<256> (row pass, column pass)"}
+            "kernel": f"enc16_kernel<{1 << (k - 1).bit_length()}> (row pass, column pass)"}
 
 
 def bench_nmt_roots(local, L, R, k, S, squares=32, reps=5, ns=29):
@@ -784,9 +908,11 @@ def main():
         R._check(L.rsm_event_record(ctx, ev[2], st))
 
     def sync_all():
+        # every stream's stuck-wait report is checked at each sync point (rsm_sync covers
+        # the context stream, rsm_stream_check the extra ones)
         R._check(L.rsm_sync(ctx))
         for st in streams[1:]:
-            R._check(L.rsm_stream_sync(st))
+            R._check(L.rsm_stream_check(ctx, st))
 
     # the first warmup step, then the correctness gate on its output (the oracle is the
     # checker only), then the remaining warmup steps: the timed steps follow warm steps
@@ -953,6 +1079,12 @@ def main():
                 out["codec"] = bench_codec(local, L, R)
                 out["fraud_proof"] = bench_fraud_proof(local, L, R)
         out["cpu_baseline"] = None if a.no_cpu_baseline else cpu_baseline(k, S, a.cpu_seconds)
+        cb = out["cpu_baseline"]
+        if cb:
+            # GPU / CPU against the measured affinity-wide run and against the linear
+            # all-host-CPUs extrapolation of the single-thread rate
+            cb["gpu_over_cpu"] = round(value / cb["value"], 2)
+            cb["gpu_over_cpu_all_cores_estimate"] = round(value / cb["all_cores_estimate_GiB_s"], 2)
     if rank == 0 and world == 1 and not a.no_roots:
         out["with_roots"] = bench_roots(local, L, R, buf, k, S, B, a.steps)
         out["with_nmt_roots"] = bench_nmt_roots(local, L, R, k, S)
@@ -964,6 +1096,8 @@ def main():
         out["single_square"] = bench_single_square(local, L, R)
         if not a.no_c4:
             out["c4"] = bench_c4(local, L, R, a.steps)
+            # BenchmarkExtensionEncoding's k = 256 square at its shareSize 512 (GF(2^16))
+            out["gf16_k256_s512"] = bench_c4(local, L, R, a.steps, B=8, k=256, S=512)
     if rank == 0 and world == 1 and not a.no_c3:
         out["c3"] = bench_c3(local, L, R)
         if not a.no_gf16_repair:

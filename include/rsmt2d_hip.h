@@ -171,6 +171,17 @@ rsm_ctx* rsm_multi_context(rsm_multi* m, int i);
  * k must be a multiple of G.  Synchronous. */
 int rsm_multi_extend_square(rsm_multi* m, const uint8_t* ods, uint32_t k, uint32_t share_size, uint8_t* eds,
                             int schedule);
+/* Pinned host memory for the multi-GPU host path (hipHostMalloc, portable: every GPU
+ * of the clique DMAs it directly). */
+int rsm_multi_host_alloc(rsm_multi* m, uint64_t bytes, void** p);
+int rsm_multi_host_free(rsm_multi* m, void* p);
+/* In-place host form (what the cgo ComputeExtendedDataSquare fast path calls on a
+ * pinned arena): eds is (2k)^2*S row-major whose top-left k x k quadrant already
+ * holds the ODS (Go's EDS aliases its input); only Q1, Q2, Q3 are written.  From
+ * rsm_multi_host_alloc memory every copy is one DMA per GPU (Q0 rows up, Q1 rows and
+ * the bottom-half column slice down; the Q1 download overlaps the exchange and the
+ * column pass); pageable memory also works (staged by HIP).  Synchronous. */
+int rsm_multi_extend_square_inplace(rsm_multi* m, uint8_t* eds, uint32_t k, uint32_t share_size, int schedule);
 /* Device-resident form: d_eds[g] is a full [2k][2k][S] buffer on GPU g holding Q0
  * rows of shard g; afterwards it holds shard g's rows of the top half and its
  * column slice [g 2k/G, (g+1) 2k/G) of the whole square (all-gather: the whole top
@@ -189,7 +200,8 @@ int rsm_memcpy(rsm_ctx* ctx, void* dst, const void* src, uint64_t bytes, int kin
 /* SplitMix64 byte stream (seeded synthetic shares), asynchronous on the ctx stream. */
 int rsm_dev_fill_random(rsm_ctx* ctx, void* d, uint64_t bytes, uint64_t seed);
 int rsm_sync(rsm_ctx* ctx);
-/* *equal = 1 iff the device buffers a and b (bytes a multiple of 16) are equal,
+/* *equal = 1 iff the device buffers a and b (bytes a multiple of 16, both pointers
+ * 16-byte aligned: the kernel reads them as uint4; RSM_EINVAL otherwise) are equal,
  * compared on the device (a kernel on `stream`, NULL = context stream); synchronous. */
 int rsm_dev_equal(rsm_ctx* ctx, const void* a, const void* b, uint64_t bytes, void* stream, int* equal);
 /* Extra HIP streams on the context's device, for callers that pipeline independent

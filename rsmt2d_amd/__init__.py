@@ -138,6 +138,9 @@ SIGNATURES = {
     "rsm_multi_extend_square": (_I32, [_VP, _VP, _U32, _U32, _VP, ctypes.c_int]),
     "rsm_multi_extend_dev": (_I32, [_VP, _VP, _U32, _U32, ctypes.c_int]),
     "rsm_multi_sync": (_I32, [_VP]),
+    "rsm_multi_host_alloc": (_I32, [_VP, _U64, ctypes.POINTER(_VP)]),
+    "rsm_multi_host_free": (_I32, [_VP, _VP]),
+    "rsm_multi_extend_square_inplace": (_I32, [_VP, _VP, _U32, _U32, ctypes.c_int]),
     "rsm_extend_squares_dev": (_I32, [_VP, _VP, _U32, _U32, _U32, _VP]),
     "rsm_extend_squares_phase_dev": (_I32, [_VP, _VP, _U32, _U32, _U32, _I32, _VP]),
     "rsm_extend_rows_dev": (_I32, [_VP, _VP, _U32, _U32, _U32, _U32, _VP]),

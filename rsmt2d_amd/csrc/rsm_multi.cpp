@@ -28,6 +28,8 @@ struct rsm_multi {
     std::vector<ncclComm_t> comm;
     std::vector<DevBuf> eds;       // per GPU: a full [2k][2k][S] square (host path)
     std::vector<DevBuf> pack[2];   // per GPU: all-to-all send / receive staging
+    std::vector<hipStream_t> side; // per GPU: the host path's Q1 download (overlaps the column pass)
+    std::vector<hipEvent_t> rows_done;  // per GPU: recorded after its row pass (host path)
     std::mutex mu;                 // one multi-GPU extension at a time
 };
 
@@ -41,7 +43,11 @@ int nccl_fail(ncclResult_t r, const char* what) {
 // on GPU g whose Q0 rows of shard g are valid).  Leaves on GPU g: its rows of the
 // top half and its column slice of the whole square (all-gather: the whole top
 // half too).
-int extend_sharded(rsm_multi* m, uint8_t* const* d_eds, uint32_t k, uint32_t S, int schedule) {
+// rows_done (host path): an event per GPU recorded on its stream right after its row
+// pass, so the download of its Q1 rows can start on a side stream while the exchange
+// and the column pass run.
+int extend_sharded(rsm_multi* m, uint8_t* const* d_eds, uint32_t k, uint32_t S, int schedule,
+                   const hipEvent_t* rows_done = nullptr) {
     const int G = m->n;
     const size_t W = 2ull * k, row = W * S;
     const uint32_t rk = k / G, ck = (uint32_t)(W / G);
@@ -49,6 +55,9 @@ int extend_sharded(rsm_multi* m, uint8_t* const* d_eds, uint32_t k, uint32_t S, 
     for (int g = 0; g < G; ++g) {
         if (int rc = use_device(m->ctx[g])) return rc;
         if (int rc = rsm_extend_rows_dev(m->ctx[g], d_eds[g], k, S, g * rk, rk, nullptr)) return rc;
+        if (rows_done) {
+            if (hipError_t e = hipEventRecord(rows_done[g], m->ctx[g]->stream)) return hip_fail(e, "hipEventRecord");
+        }
     }
     // 2. exchange
     ncclResult_t r;
@@ -120,6 +129,52 @@ int check_shape(const rsm_multi* m, uint32_t k, uint32_t S, int schedule) {
     return RSM_OK;
 }
 
+// One square from host memory over the clique: GPU g uploads its Q0 rows (from `ods`
+// with row pitch `opitch`), the sharded extension runs, GPU g downloads its rows of Q1
+// (side stream, behind its row pass) and its column slice of the bottom half [Q2|Q3]
+// (its stream, behind its column pass) into `eds`.  Q0 of `eds` is not written.  With
+// pinned host buffers every copy is a DMA of the GPU's copy engines; caller holds m->mu.
+int host_extend(rsm_multi* m, const uint8_t* ods, size_t opitch, uint8_t* eds, uint32_t k, uint32_t share_size,
+                int schedule) {
+    const int G = m->n;
+    const size_t S = share_size, W = 2ull * k, row = W * S, half = (size_t)k * S;
+    const uint32_t rk = k / G, ck = (uint32_t)(W / G);
+    std::vector<uint8_t*> d(G);
+    hipError_t e;
+    for (int g = 0; g < G; ++g) {
+        if (int rc = use_device(m->ctx[g])) return rc;
+        if ((e = m->eds[g].ensure(W * W * S)) != hipSuccess) return hip_fail(e, "hipMalloc (sharded square)");
+        d[g] = static_cast<uint8_t*>(m->eds[g].ptr);
+        const size_t r0 = (size_t)g * rk;
+        if ((e = hipMemcpy2DAsync(d[g] + r0 * row, row, ods + r0 * opitch, opitch, half, rk, hipMemcpyHostToDevice,
+                                  m->ctx[g]->stream)) != hipSuccess)
+            return hip_fail(e, "H2D (Q0 rows)");
+    }
+    if (int rc = extend_sharded(m, d.data(), k, share_size, schedule, m->rows_done.data())) return rc;
+    for (int g = 0; g < G; ++g) {
+        if (int rc = use_device(m->ctx[g])) return rc;
+        const size_t r0 = (size_t)g * rk;
+        if ((e = hipStreamWaitEvent(m->side[g], m->rows_done[g], 0)) != hipSuccess ||
+            (e = hipMemcpy2DAsync(eds + r0 * row + half, row, d[g] + r0 * row + half, row, half, rk,
+                                  hipMemcpyDeviceToHost, m->side[g])) != hipSuccess)
+            return hip_fail(e, "D2H (Q1 rows)");
+        const size_t c0 = (size_t)g * ck * S;
+        if ((e = hipMemcpy2DAsync(eds + (size_t)k * row + c0, row, d[g] + (size_t)k * row + c0, row, (size_t)ck * S, k,
+                                  hipMemcpyDeviceToHost, m->ctx[g]->stream)) != hipSuccess)
+            return hip_fail(e, "D2H (bottom-half columns)");
+    }
+    return RSM_OK;
+}
+
+int sync_all(rsm_multi* m) {
+    for (int g = 0; g < m->n; ++g) {
+        if (int rc = rsm_sync(m->ctx[g])) return rc;
+        if (int rc = use_device(m->ctx[g])) return rc;
+        if (hipError_t e = hipStreamSynchronize(m->side[g])) return hip_fail(e, "hipStreamSynchronize (side)");
+    }
+    return RSM_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -146,6 +201,20 @@ int rsm_multi_create(const int* devices, int n, rsm_multi** out) {
     m->eds = std::vector<DevBuf>(n);
     m->pack[0] = std::vector<DevBuf>(n);
     m->pack[1] = std::vector<DevBuf>(n);
+    m->side.assign(n, nullptr);
+    m->rows_done.assign(n, nullptr);
+    for (int g = 0; g < n; ++g) {
+        hipError_t e;
+        if (int rc = use_device(m->ctx[g])) {
+            rsm_multi_destroy(m);
+            return rc;
+        }
+        if ((e = hipStreamCreateWithFlags(&m->side[g], hipStreamNonBlocking)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&m->rows_done[g], hipEventDisableTiming)) != hipSuccess) {
+            rsm_multi_destroy(m);
+            return hip_fail(e, "rsm_multi_create: side stream / event");
+        }
+    }
     *out = m;
     return RSM_OK;
 }
@@ -169,6 +238,11 @@ void rsm_multi_destroy(rsm_multi* m) {
         drop(m->eds[g]);
         drop(m->pack[0][g]);
         drop(m->pack[1][g]);
+        if (g < m->side.size() && m->side[g]) {
+            (void)hipStreamSynchronize(m->side[g]);
+            (void)hipStreamDestroy(m->side[g]);
+        }
+        if (g < m->rows_done.size() && m->rows_done[g]) (void)hipEventDestroy(m->rows_done[g]);
     }
     for (auto* c : m->ctx)
         if (c) rsm_ctx_destroy(c);
@@ -190,9 +264,23 @@ int rsm_multi_extend_dev(rsm_multi* m, void* const* d_eds, uint32_t k, uint32_t 
 
 int rsm_multi_sync(rsm_multi* m) {
     if (!m) return fail(RSM_EINVAL, "rsm_multi_sync: NULL");
-    for (auto* c : m->ctx)
-        if (int rc = rsm_sync(c)) return rc;
-    return RSM_OK;
+    return sync_all(m);
+}
+
+int rsm_multi_host_alloc(rsm_multi* m, uint64_t bytes, void** out) {
+    if (!m || !out) return fail(RSM_EINVAL, "rsm_multi_host_alloc: bad arguments");
+    *out = nullptr;
+    if (int rc = use_device(m->ctx[0])) return rc;
+    // portable: pinned for (and DMA-able by) every GPU of the clique, not just GPU 0
+    hipError_t e = hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocPortable);
+    return e == hipSuccess ? RSM_OK : hip_fail(e, "hipHostMalloc (portable)");
+}
+
+int rsm_multi_host_free(rsm_multi* m, void* p) {
+    if (!m) return fail(RSM_EINVAL, "rsm_multi_host_free: NULL");
+    if (!p) return RSM_OK;
+    hipError_t e = hipHostFree(p);
+    return e == hipSuccess ? RSM_OK : hip_fail(e, "hipHostFree");
 }
 
 // ComputeExtendedDataSquare of one square from host memory over all GPUs: GPU g
@@ -204,35 +292,22 @@ int rsm_multi_extend_square(rsm_multi* m, const uint8_t* ods, uint32_t k, uint32
     if (!m || !ods || !eds) return fail(RSM_EINVAL, "rsm_multi_extend_square: bad arguments");
     if (int rc = check_shape(m, k, share_size, schedule)) return rc;
     std::lock_guard<std::mutex> lk(m->mu);
-    const int G = m->n;
-    const size_t S = share_size, W = 2ull * k, row = W * S, half = (size_t)k * S;
-    const uint32_t rk = k / G, ck = (uint32_t)(W / G);
-    std::vector<uint8_t*> d(G);
-    hipError_t e;
-    for (int g = 0; g < G; ++g) {
-        if (int rc = use_device(m->ctx[g])) return rc;
-        if ((e = m->eds[g].ensure(W * W * S)) != hipSuccess) return hip_fail(e, "hipMalloc (sharded square)");
-        d[g] = static_cast<uint8_t*>(m->eds[g].ptr);
-        const size_t r0 = (size_t)g * rk;
-        if ((e = hipMemcpy2DAsync(d[g] + r0 * row, row, ods + r0 * half, half, half, rk, hipMemcpyHostToDevice,
-                                  m->ctx[g]->stream)) != hipSuccess)
-            return hip_fail(e, "H2D (Q0 rows)");
+    const size_t S = share_size, row = 2ull * k * S, half = (size_t)k * S;
+    if (int rc = host_extend(m, ods, half, eds, k, share_size, schedule)) {
+        (void)sync_all(m);  // no copy may still target the caller's buffers
+        return rc;
     }
-    if (int rc = extend_sharded(m, d.data(), k, share_size, schedule)) return rc;
-    for (int g = 0; g < G; ++g) {
-        if (int rc = use_device(m->ctx[g])) return rc;
-        const size_t r0 = (size_t)g * rk;
-        hipStream_t st = m->ctx[g]->stream;
-        if ((e = hipMemcpy2DAsync(eds + r0 * row + half, row, d[g] + r0 * row + half, row, half, rk,
-                                  hipMemcpyDeviceToHost, st)) != hipSuccess)
-            return hip_fail(e, "D2H (Q1 rows)");
-        const size_t c0 = (size_t)g * ck * S;
-        if ((e = hipMemcpy2DAsync(eds + (size_t)k * row + c0, row, d[g] + (size_t)k * row + c0, row, (size_t)ck * S, k,
-                                  hipMemcpyDeviceToHost, st)) != hipSuccess)
-            return hip_fail(e, "D2H (bottom-half columns)");
-    }
-    for (uint32_t r = 0; r < k; ++r) memcpy(eds + r * row, ods + r * half, half);
-    return rsm_multi_sync(m);
+    for (uint32_t r = 0; r < k; ++r) memcpy(eds + r * row, ods + r * half, half);  // Q0 (host, beside the GPUs)
+    return sync_all(m);
+}
+
+int rsm_multi_extend_square_inplace(rsm_multi* m, uint8_t* eds, uint32_t k, uint32_t share_size, int schedule) {
+    if (!m || !eds) return fail(RSM_EINVAL, "rsm_multi_extend_square_inplace: bad arguments");
+    if (int rc = check_shape(m, k, share_size, schedule)) return rc;
+    std::lock_guard<std::mutex> lk(m->mu);
+    int rc = host_extend(m, eds, 2ull * k * share_size, eds, k, share_size, schedule);
+    const int rs = sync_all(m);
+    return rc ? rc : rs;
 }
 
 }  // extern "C"

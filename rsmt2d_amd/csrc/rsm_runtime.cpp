@@ -143,7 +143,9 @@ void release_lane(rsm_ctx* ctx, Lane* l) {
         std::lock_guard<std::mutex> lk(ctx->lane_mu);
         ctx->free_lanes.push_back(l);
     }
-    ctx->lane_cv.notify_one();
+    // notify_all: a multi-lane waiter (acquire_lanes) woken by a single release may
+    // still lack lanes and sleep again; it must not swallow a single-lane caller's wakeup
+    ctx->lane_cv.notify_all();
 }
 
 StreamScratch& stream_scratch(rsm_ctx* ctx, hipStream_t st) {
@@ -319,6 +321,10 @@ int check_queue_reports(rsm_ctx* ctx, hipStream_t st) {
         if (w && *w) {
             *w = 0;
             stuck = true;
+            // a timed-out wait may leave the stream's shared hand-off words non-zero (the
+            // launch drains without its final re-zeroing): clear them, in stream order
+            // behind that launch, before any later launch on this stream reads them
+            if (kv.second->queue.ptr) (void)hipMemsetAsync(kv.second->queue.ptr, 0, kv.second->queue.cap, kv.first);
         }
     }
     return stuck ? fail(RSM_EDEVICE, "single-launch extension: a column set timed out waiting for its rows "
@@ -1084,7 +1090,8 @@ int rsm_stream_destroy(rsm_ctx* ctx, void* stream) {
 // Device-side equality of two device buffers (a compare kernel on `stream`, then
 // one word back): checks of large device-resident results without downloading them.
 int rsm_dev_equal(rsm_ctx* ctx, const void* a, const void* b, uint64_t bytes, void* stream, int* equal) {
-    if (!ctx || !a || !b || !equal || bytes % 16 != 0) return fail(RSM_EINVAL, "rsm_dev_equal: bad arguments");
+    if (!ctx || !a || !b || !equal || bytes % 16 != 0 || (((uintptr_t)a | (uintptr_t)b) & 15u) != 0)
+        return fail(RSM_EINVAL, "rsm_dev_equal: bad arguments (bytes and both pointers must be 16-byte multiples)");
     *equal = 0;
     if (int rc = use_device(ctx)) return rc;
     LaneGuard g(ctx);

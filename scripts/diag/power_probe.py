@@ -32,11 +32,13 @@ def sample():
         num = re.search(r"([0-9.]+)", str(v))
         if not num:
             continue
+        # rocm-smi reports "<clk> clock speed:" = "(1500Mhz)" and "<clk> clock level:" = "1":
+        # only the speed entries are clocks (the level index once overwrote them)
         if "power" in kl and "w" in kl:
             out["power_W"] = float(num.group(1))
-        elif kl.startswith("sclk"):
+        elif kl.startswith("sclk") and "speed" in kl:
             out["sclk_MHz"] = float(num.group(1))
-        elif kl.startswith("mclk"):
+        elif kl.startswith("mclk") and "speed" in kl:
             out["mclk_MHz"] = float(num.group(1))
     return out
 

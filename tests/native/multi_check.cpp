@@ -3,8 +3,9 @@
 // over the RCCL stub (rccl_stub.cpp) and oracle-backed encode launches
 // (hip_stub.cpp built with RSM_STUB_ORACLE), against the oracle's whole-square
 // extension (oracle/leopard_oracle.c, the reference 2D schedule).
-//   1. rsm_multi_extend_square (host memory in and out), both schedules: the whole
-//      EDS bit-exact;
+//   1. rsm_multi_extend_square (host memory in and out) and the in-place pinned form
+//      rsm_multi_extend_square_inplace (an rsm_multi_host_alloc EDS whose Q0 quadrant
+//      holds the ODS), both schedules: the whole EDS bit-exact;
 //   2. rsm_multi_extend_dev (per-GPU buffers holding only their Q0 rows), both
 //      schedules: on GPU g its rows of the top half, its column slice of the
 //      whole square and (all-gather) the whole top half, bit-exact -- the
@@ -14,6 +15,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <thread>
 #include <vector>
@@ -70,6 +72,19 @@ void check_case(int G, uint32_t k, uint32_t S, uint64_t seed) {
         int rc = rsm_multi_extend_square(m, ods.data(), k, S, got.data(), sched);
         CHECK(rc == RSM_OK, "extend_square G=%d k=%u sched=%d rc=%d (%s)", G, k, sched, rc, rsm_last_error());
         CHECK(got == want, "host EDS differs G=%d k=%u S=%u sched=%d", G, k, S, sched);
+        // 1b. in place, pinned arena
+        void* pin = nullptr;
+        CHECK(rsm_multi_host_alloc(m, W * W * S, &pin) == RSM_OK && pin, "rsm_multi_host_alloc");
+        if (pin) {
+            uint8_t* e = static_cast<uint8_t*>(pin);
+            memset(e, 0xA5, W * W * S);
+            for (uint32_t r = 0; r < k; ++r) memcpy(e + r * row, ods.data() + r * half, half);
+            rc = rsm_multi_extend_square_inplace(m, e, k, S, sched);
+            CHECK(rc == RSM_OK, "extend_square_inplace G=%d k=%u sched=%d rc=%d (%s)", G, k, sched, rc, rsm_last_error());
+            CHECK(memcmp(e, want.data(), W * W * S) == 0, "in-place pinned EDS differs G=%d k=%u S=%u sched=%d", G, k,
+                  S, sched);
+            CHECK(rsm_multi_host_free(m, pin) == RSM_OK, "rsm_multi_host_free");
+        }
         // 2. device-resident: buffer g holds only the Q0 rows of shard g
         std::vector<void*> d(G);
         for (int g = 0; g < G; ++g) {
@@ -95,6 +110,8 @@ void check_case(int G, uint32_t k, uint32_t S, uint64_t seed) {
     // contract: k not a multiple of G, unknown schedule
     if (G > 1) CHECK(rsm_multi_extend_square(m, ods.data(), k + 1, S, got.data(), 0) == RSM_ESHAPE, "k %% G check");
     CHECK(rsm_multi_extend_square(m, ods.data(), k, S, got.data(), 7) == RSM_EINVAL, "schedule check");
+    if (G > 1) CHECK(rsm_multi_extend_square_inplace(m, got.data(), k + 1, S, 0) == RSM_ESHAPE, "in-place k %% G check");
+    CHECK(rsm_multi_extend_square_inplace(m, nullptr, k, S, 0) == RSM_EINVAL, "in-place NULL check");
     rsm_multi_destroy(m);
 }
 
@@ -120,7 +137,13 @@ void hammer() {
             std::vector<uint8_t> out(W * W * S);
             for (int i = 0; i < 6; ++i) {
                 rsm_multi* m = own ? own : shared;
-                if (rsm_multi_extend_square(m, ods.data(), k, S, out.data(), i & 1) != RSM_OK || out != want) bad[t] = 1;
+                if (i % 3 == 2) {  // the in-place form on a buffer holding only the ODS
+                    std::fill(out.begin(), out.end(), 0);
+                    for (uint32_t r = 0; r < k; ++r) memcpy(out.data() + r * W * S, ods.data() + r * k * S, k * S);
+                    if (rsm_multi_extend_square_inplace(m, out.data(), k, S, i & 1) != RSM_OK || out != want) bad[t] = 1;
+                } else if (rsm_multi_extend_square(m, ods.data(), k, S, out.data(), i & 1) != RSM_OK || out != want) {
+                    bad[t] = 1;
+                }
             }
             rsm_multi_destroy(own);
         });

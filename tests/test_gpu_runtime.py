@@ -166,7 +166,7 @@ def test_single_launch_batch_matches_two_launch(lib, S, count):
 @pytest.mark.parametrize("k,S,count", [(128, 512, 1), (128, 512, 4), (65, 64, 2), (100, 1024, 1), (128, 64, 3),
                                        (127, 320, 1)])
 def test_split_latency_form(lib, k, S, count):
-    """Up to rsm_ctx_set_split_max squares per call (default 4) with 65 <= k <= 128 take
+    """Up to rsm_ctx_set_split_max squares per call (default 12) with 65 <= k <= 128 take
     the latency form (encode_gf8_split_kernel: rows + Q0 columns in one launch, Q1
     columns in a second): every square bit-exact with the oracle and with the
     queue-driven launch of the same batch."""
@@ -380,3 +380,23 @@ def test_multi_gpu_shape_errors(lib, multi):
     eds = np.zeros(16, np.uint8)
     assert lib.rsm_multi_extend_square(multi, eds.ctypes.data, 4, 100, eds.ctypes.data, 0) == R.RSM_ESHARESIZE
     assert lib.rsm_multi_extend_square(multi, eds.ctypes.data, 4, 64, eds.ctypes.data, 7) == R.RSM_EINVAL
+
+
+@pytest.mark.parametrize("sched", [0, 1])
+def test_multi_gpu_inplace_pinned_world1(lib, multi, sched):
+    """The pinned in-place host form (rsm_multi_extend_square_inplace on an
+    rsm_multi_host_alloc arena whose Q0 quadrant holds the ODS) at config 5's k = 512,
+    S = 512: only Q1..Q3 written, the whole EDS bit-exact against the oracle."""
+    k, S = 512, 512
+    W = 2 * k
+    ods = oracle.splitmix64_bytes(k * k * S, seed=0x5C + sched).reshape(k, k, S)
+    p = ctypes.c_void_p()
+    R._check(lib.rsm_multi_host_alloc(multi, W * W * S, ctypes.byref(p)))
+    try:
+        eds = np.ctypeslib.as_array((ctypes.c_uint8 * (W * W * S)).from_address(p.value)).reshape(W, W, S)
+        eds[:] = 0x3C
+        eds[:k, :k] = ods
+        R._check(lib.rsm_multi_extend_square_inplace(multi, p, k, S, sched))
+        assert np.array_equal(eds, oracle.extend_square(ods, nthreads=8))
+    finally:
+        R._check(lib.rsm_multi_host_free(multi, p))
