@@ -549,8 +549,9 @@ struct Dec16 {
     Res r;
     const uint16_t* logwalsh;
     uint16_t* errs;     // [count][n]
-    uint8_t* scratch;   // [count][2][n][S]
+    uint8_t* scratch;   // [count][2][n][S] (the five-pass form)
     uint32_t q0, count, chunks;
+    const PermTab16* tw;  // skewperm (the single-pass form)
 };
 
 __device__ __forceinline__ uint32_t addm(uint32_t a, uint32_t b) {
@@ -777,6 +778,111 @@ __global__ __launch_bounds__(256) void dec16_p5(Dec16 p) {  // group: FFT low + 
     });
 }
 
+
+// ---------------------------------------------------------------------------
+// Single-pass decoder for m = 256 (n = 512 points; 129 <= k <= 256): one workgroup
+// of 16 waves per (codeword, 512-byte chunk) keeps the whole n-point transform on
+// chip, as enc16_kernel<512> does for the encoder -- the work array of the five
+// passes above never touches memory:
+//   group layout   (wave w: elements 32 w .. 32 w + 31): scale by the error locator,
+//                  IFFT layers d = 1..16;
+//   residue layout (wave w: residues 2 w, 2 w + 1; elements r + 32 j, j < 16): IFFT
+//                  d = 32..256; the formal derivative out = in + L(in) + H(in) (H:
+//                  partners e + 2^t, t >= 5, in registers, updated in ascending j so
+//                  every term reads a pre-derivative value; L: partners t < 5, read
+//                  from the pre-derivative plane the waves leave in LDS); FFT d =
+//                  256..32;
+//   group layout   FFT d = 16..1; reveal the missing shares (times exp(-err)).
+// The error locators come from errloc16_kernel (one workgroup per codeword).
+// ---------------------------------------------------------------------------
+template <int E, int R>
+__device__ __forceinline__ void deriv_plane(uint32_t (&v)[E], uint32_t (*xch)[64], uint32_t w, uint32_t lane) {
+    constexpr int RPW = E / R;  // residues per wave; register s*R + j holds element RPW w + s + E j
+    sfor<E>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        xch[(RPW * w + i / R) + E * (i % R)][lane] = v[i];
+    });
+    __syncthreads();
+    sfor<RPW>([&](auto Sx) {
+        constexpr int sx = decltype(Sx)::value;
+        const uint32_t r = RPW * w + sx;  // residue = the element's low 5 bits
+        sfor<R>([&](auto J) {  // ascending j: v[s*R + j + 2^t] is still the pre-derivative value
+            constexpr int j = decltype(J)::value;
+            constexpr int i = sx * R + j;
+            uint32_t a = v[i];
+            sfor<12>([&](auto T) {  // H: the element's high bits (t >= 5) = bits of j
+                constexpr int t = decltype(T)::value;
+                if constexpr ((1 << t) < R && ((j >> t) & 1) == 0) a ^= v[i + (1 << t)];
+            });
+            sfor<5>([&](auto T) {  // L: bits of the residue, from the plane in LDS
+                constexpr uint32_t bit = 1u << decltype(T)::value;
+                if ((r & bit) == 0u) a ^= xch[(r + bit) + E * j][lane];
+            });
+            v[i] = a;
+        });
+    });
+    __syncthreads();
+}
+
+template <int M>
+__global__ __launch_bounds__(1024, 4) void dec16f_kernel(Dec16 p) {
+    constexpr int N = 2 * M, E = 32, R = N / E, WAVES = N / E;
+    static_assert(WAVES == 16 && R == 16, "n = 512: 16 waves of 32 elements, residues of 16");
+    __shared__ uint32_t xch[N][64];
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    const uint32_t task = blockIdx.x;
+    const uint32_t q = task / p.chunks, chunk = task - q * p.chunks;
+    const Lane ln = lane_of(chunk, p.ds.S);
+    const uint32_t k = p.ds.k, S = p.ds.S;
+    const auto sq = rsrc(p.ds.base);
+    const PermTab16* tw = p.tw;
+    // work slot e <- share: e < k parity k + e, M <= e < M + k data e - M, else zero
+    auto share_of = [&](uint32_t e) -> uint32_t {
+        return e < k ? k + e : (e >= (uint32_t)M && e < (uint32_t)M + k) ? e - (uint32_t)M : 0xFFFFFFFFu;
+    };
+    // presence of this wave's 32 slots first (uniform byte loads), then the present
+    // shares' loads all in flight together (an absent slot reads zeros)
+    uint32_t have = 0;
+    sfor<E>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        const uint32_t src = share_of(E * w + i);
+        const uint32_t pr = src != 0xFFFFFFFFu ? (uint32_t)p.ds.presence[cell_of(p.ds, p.q0 + q, src)] : 0u;
+        have |= (__builtin_amdgcn_readfirstlane(pr) != 0u ? 1u : 0u) << i;
+    });
+    uint32_t l[E], h[E];
+    sfor<E>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        const uint32_t src = share_of(E * w + i);
+        const uint32_t so = ((have >> i) & 1u) ? (uint32_t)(cell_of(p.ds, p.q0 + q, src) * S) : kOob16;
+        l[i] = ld(sq, ln.lo, so);
+        h[i] = ld(sq, ln.lo + 32, so);
+    });
+    sfor<E>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        if ((have >> i) & 1u) mul16(l[i], h[i], p.r.perm[err_of(p, q, E * w + i, N)]);
+    });
+    grp_xform_g<E, false>(l, h, tw, (int)(E * w), -1);
+    xch_plane<E, R, true>(l, xch, w, lane);
+    xch_plane<E, R, true>(h, xch, w, lane);
+    res_xform_g<E, R, false>(l, h, tw, -1);
+    deriv_plane<E, R>(l, xch, w, lane);
+    deriv_plane<E, R>(h, xch, w, lane);
+    res_xform_g<E, R, true>(l, h, tw, 0);
+    xch_plane<E, R, false>(l, xch, w, lane);
+    xch_plane<E, R, false>(h, xch, w, lane);
+    grp_xform_g<E, true>(l, h, tw, (int)(E * w), 0);
+    sfor<E>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        const uint32_t e = E * w + i;
+        const uint32_t dst = share_of(e);
+        if (dst != 0xFFFFFFFFu && !((have >> i) & 1u)) {
+            mul16(l[i], h[i], p.r.perm[kMod16 - err_of(p, q, e, N)]);
+            const uint32_t so = (uint32_t)(cell_of(p.ds, p.q0 + q, dst) * S);
+            st(sq, l[i], ln.lo, so);
+            st(sq, h[i], ln.lo + 32, so);
+        }
+    });
+}
 
 // ---------------------------------------------------------------------------
 // Generic multi-pass transforms for m = ceilPow2(k) >= 1024 (k up to 32768, the
@@ -1038,6 +1144,13 @@ hipError_t run_encode(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st) {
     return hipGetLastError();
 }
 
+#ifdef RSM_DIAG
+static std::atomic<bool> g_dec16_five{false};
+static bool dec16_five_pass() { return g_dec16_five.load(); }
+#else
+static bool dec16_five_pass() { return false; }
+#endif
+
 template <int M>
 hipError_t run_decode(const DecodeSet& ds, const Gf16Dev& g, const uint16_t* logwalsh, hipStream_t st) {
     constexpr int N = 2 * M;
@@ -1049,8 +1162,15 @@ hipError_t run_decode(const DecodeSet& ds, const Gf16Dev& g, const uint16_t* log
     if (batch == 0) return hipErrorOutOfMemory;
     for (uint32_t q0 = 0; q0 < ds.count; q0 += batch) {
         Dec16 p{ds, Res{g.perm, g.skew}, logwalsh, g.errs, g.scratch, q0,
-                ds.count - q0 < batch ? ds.count - q0 : batch, chunks};
+                ds.count - q0 < batch ? ds.count - q0 : batch, chunks, g.skewperm};
         hipLaunchKernelGGL(errloc16_kernel<M>, dim3(p.count), dim3(M), 0, st, p);
+        if constexpr (M == 256) {
+            if (!dec16_five_pass()) {  // the single-pass form (diagnostic builds can A/B the five passes)
+                hipLaunchKernelGGL(dec16f_kernel<M>, dim3(p.count * chunks), dim3(1024), 0, st, p);
+                if (hipError_t e = hipGetLastError()) return e;
+                continue;
+            }
+        }
         hipLaunchKernelGGL(dec16_p1<M>, dim3(blocks_for((uint64_t)p.count * chunks * (N / 16))), dim3(256), 0, st, p);
         hipLaunchKernelGGL(dec16_p2<M>, dim3(blocks_for((uint64_t)p.count * chunks * 16)), dim3(256), 0, st, p);
         hipLaunchKernelGGL(dec16_p3<M>, dim3(blocks_for((uint64_t)p.count * chunks * (N / 16))), dim3(256), 0, st, p);
@@ -1223,6 +1343,7 @@ static hipError_t run_decode_generic(const DecodeSet& ds, const Gf16Dev& g, hipS
 
 #ifdef RSM_DIAG
 void set_enc16_diag_e64(bool on) { g_enc16_e64.store(on); }
+void set_dec16_diag_five_pass(bool on) { g_dec16_five.store(on); }
 #endif
 
 hipError_t launch_encode_gf16(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st) {

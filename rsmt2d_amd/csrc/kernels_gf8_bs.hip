@@ -499,11 +499,11 @@ __device__ __forceinline__ uint32_t q_claim(const QueuePlan& p, const QClaim& c)
 // drops below the unclaimed items, so none is stranded, and the CUs of the others
 // go to the next launch on another stream); otherwise claim a Q1 item (it may have
 // to be waited for).  Returns kNone (leave) or the claimed Q1 item.
-__device__ __forceinline__ uint32_t q_leave_or_claim(const QueuePlan& p) {
+__device__ __forceinline__ uint32_t q_leave_or_claim(const QueuePlan& p, uint32_t G) {
     const uint32_t e = q_add(&p.ctr[kQLeft]);
     uint32_t qh = q_load(&p.ctr[kQHead1]);
     qh = qh < p.nq1 ? qh : p.nq1;
-    if (gridDim.x - e - 1u >= p.nq1 - qh) return kNone;
+    if (G - e - 1u >= p.nq1 - qh) return kNone;
     q_sub(&p.ctr[kQLeft]);
     return kQ1 | q_add(&p.ctr[kQHead1]);
 }
@@ -512,7 +512,8 @@ __device__ __forceinline__ uint32_t q_leave_or_claim(const QueuePlan& p) {
 // `wait` (the workgroup then holds no other item); otherwise rdy = 0 for a Q1 item
 // that is not ready (the slow path waits for it after the first set).
 __device__ __forceinline__ uint32_t q_wait(const QueuePlan& p, uint32_t it);
-__device__ __forceinline__ uint32_t q_take(const QueuePlan& p, QClaim& c, bool wait, uint32_t& sq, uint32_t& rdy) {
+__device__ __forceinline__ uint32_t q_take(const QueuePlan& p, QClaim& c, bool wait, uint32_t& sq, uint32_t& rdy,
+                                           uint32_t G) {
     sq = 0u;
     rdy = 1u;
     if (!c.main_done) {
@@ -520,7 +521,7 @@ __device__ __forceinline__ uint32_t q_take(const QueuePlan& p, QClaim& c, bool w
         if (u < p.nmain) return u;
         c.main_done = 1u;
     }
-    const uint32_t it = q_leave_or_claim(p);
+    const uint32_t it = q_leave_or_claim(p, G);
     if (it == kNone || (it & ~kQ1) >= p.nq1) return kNone;
     const uint32_t q = it & ~kQ1;
     if (wait) {
@@ -615,8 +616,8 @@ __device__ __forceinline__ void bs_queue_wave(const QueuePlan& p, uint32_t* lds,
     // prologue: the first two items, taken synchronously; the first one loaded
     if (t0) {
         uint32_t sq0 = 0, sq1 = 0, r0 = 1, r1 = 1;
-        const uint32_t c0 = q_take(p, qc, true, sq0, r0);
-        const uint32_t c1 = c0 == kNone ? kNone : q_take(p, qc, false, sq1, r1);
+        const uint32_t c0 = q_take(p, qc, true, sq0, r0, gridDim.x);
+        const uint32_t c1 = c0 == kNone ? kNone : q_take(p, qc, false, sq1, r1, gridDim.x);
         lds[0] = c0;
         lds[1] = sq0;
         lds[4] = c1;
@@ -729,7 +730,7 @@ __device__ __forceinline__ void bs_queue_wave(const QueuePlan& p, uint32_t* lds,
                     qc.main_done = 1u;
                     it = qc.res != kNone ? qc.res : kQExitCheck;
                 }
-                if (it == kQExitCheck) it = q_leave_or_claim(p);
+                if (it == kQExitCheck) it = q_leave_or_claim(p, gridDim.x);
                 if (it == kNone || ((it & kQ1) && (it & ~kQ1) >= p.nq1)) {
                     nn = kNone;
                 } else {
@@ -899,10 +900,20 @@ __device__ __forceinline__ void split_dma_h1(const CodewordSet& cs, const SetAdd
     });
 }
 // half G (registers 8G..8G+7) of a set into P (direct loads)
-template <bool NT, int G = 0>
+// The per-symbol offsets are loop-invariant, and hoisted out of the set loop they
+// outgrow the SGPR file: the compiler then parks them in VGPR lanes and reloads each
+// with a v_readlane (a VALU instruction) per use -- ~80 per set and wave.  Passing k,
+// the element stride and the wave index through an empty asm makes them opaque per
+// use, so each offset is recomputed right before its load / store by 2-3 scalar ALU
+// instructions, which issue beside the VALU work.
+__device__ __forceinline__ void opaque_sgpr(uint32_t& k, uint32_t& es, uint32_t& A) {
+    asm volatile("" : "+s"(k), "+s"(es), "+s"(A));
+}
+template <bool NT, int G = 0, bool OPQ = true>
 __device__ __forceinline__ void split_direct_h0(const CodewordSet& cs, const SetAddr& a, uint32_t A,
                                                 uint32_t (&P)[8][8]) {
-    const uint32_t k = cs.k, es = (uint32_t)cs.elem_stride;
+    uint32_t k = cs.k, es = (uint32_t)cs.elem_stride;
+    if constexpr (OPQ) opaque_sgpr(k, es, A);
     const __amdgpu_buffer_rsrc_t rs = as_rsrc(a.rs);
     bs8::sfor<8>([&](auto J) {
         constexpr int j = decltype(J)::value;
@@ -914,10 +925,14 @@ __device__ __forceinline__ void split_direct_h0(const CodewordSet& cs, const Set
     });
 }
 // planes -> bytes and the 16 stores of half G (Q1 write-through, Q2/Q3 non-temporal)
-template <int G, bool TRP, bool MEM_ON, bool OLDTP = false>
+template <int G, bool TRP, bool MEM_ON, bool OLDTP = false, bool PLAINQ1 = false, bool OPQ = true>
 __device__ __forceinline__ void split_store_h(uint32_t (&X)[16][8], const SetAddr& a, uint32_t A, uint32_t k,
                                               uint32_t oo, uint32_t es, bool row, bool mem) {
     const __amdgpu_buffer_rsrc_t ro = as_rsrc(a.ro);
+    if constexpr (OPQ) {
+        opaque_sgpr(k, es, A);
+        opaque_sgpr(oo, es, A);
+    }
     bs8::sfor<8>([&](auto J) {
         constexpr int j = 8 * G + decltype(J)::value;
         if constexpr (TRP && OLDTP) bs8::transpose8_dev(X[j]);
@@ -928,8 +943,8 @@ __device__ __forceinline__ void split_store_h(uint32_t (&X)[16][8], const SetAdd
         y.x = X[j][4]; y.y = X[j][5]; y.z = X[j][6]; y.w = X[j][7];
         if (!MEM_ON || !mem) {
         } else if (row) {
-            __builtin_amdgcn_raw_buffer_store_b128(x, ro, a.off[0], so, 16);
-            __builtin_amdgcn_raw_buffer_store_b128(y, ro, a.off[1], so, 16);
+            __builtin_amdgcn_raw_buffer_store_b128(x, ro, a.off[0], so, PLAINQ1 ? 0 : 16);
+            __builtin_amdgcn_raw_buffer_store_b128(y, ro, a.off[1], so, PLAINQ1 ? 0 : 16);
         } else {
             __builtin_amdgcn_raw_buffer_store_b128(x, ro, a.off[0], so, 2);
             __builtin_amdgcn_raw_buffer_store_b128(y, ro, a.off[1], so, 2);
@@ -957,8 +972,40 @@ __device__ __forceinline__ void trace_stamp(const QueuePlan& p, uint32_t it, int
 #endif
 }
 
+// XCD-affine queues (diagnostic, MODE bit 33554432): the workgroup reads the XCD it
+// runs on (HW_REG_XCC_ID) and serves only the squares s = 8 j + x of that XCD from
+// that XCD's own queue words, so a square's Q0 re-read and its Q1 hand-off stay in
+// one XCD's L2: Q1 is stored with the default policy (not write-through), and the
+// consumer's agent acquire (L1 invalidate) suffices because producer and consumer
+// share the L2.  Correct for any placement (each workgroup picks the queue of the XCD
+// it actually runs on); complete only when every XCD gets gridDim.x / 8 workgroups
+// (the round-robin placement, MI355X_MICROARCH.md) -- the diagnostic checks every
+// square.  The host zeroes all queue words before each such launch.
+__device__ __forceinline__ QueuePlan xcd_plan(const QueuePlan& p0, uint32_t x) {
+    QueuePlan p = p0;
+    p.count = p0.count / 8u;
+    p.nmain = p0.nmain / 8u;
+    p.nq1 = p0.nq1 / 8u;
+    for (CodewordSet* cs : {&p.rows, &p.cols}) {
+        cs->base += (uint64_t)x * cs->square_stride;
+        cs->out_base += (uint64_t)x * cs->square_stride;
+        cs->square_stride *= 8u;
+        cs->count /= 8u;
+    }
+    p.ctr = p0.ctr + x * (kQueueFixedWords + 2u * p.count);
+    return p;
+}
+
 template <int MODE>
-__device__ __forceinline__ void bs_split_wave(const QueuePlan& p, uint32_t* lds, uint32_t lds_base, uint32_t A) {
+__device__ __forceinline__ void bs_split_wave(const QueuePlan& p_in, uint32_t* lds, uint32_t lds_base, uint32_t A) {
+    constexpr bool XCDQ = (MODE & 33554432) != 0;
+    // 67108864: the per-symbol offsets hoisted by the compiler (round-3 codegen: ~80
+    // v_readlane SGPR reloads per set) -- A/B against the opaque per-use form
+    constexpr bool OPQ = (MODE & 67108864) == 0;
+    uint32_t xcc = 0;
+    if constexpr (XCDQ) asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    const QueuePlan p = XCDQ ? xcd_plan(p_in, xcc & 7u) : p_in;
+    const uint32_t G = XCDQ ? gridDim.x / 8u : gridDim.x;  // workgroups serving this queue
     // diagnostics (wrong output by design): 2 no arithmetic, 4 no global memory,
     // 32768 no LDS exchange
     constexpr bool ARITH = !(MODE & 2), XCH = !(MODE & 32768), NTQ0 = false, NTQ1 = true;
@@ -1024,9 +1071,9 @@ __device__ __forceinline__ void bs_split_wave(const QueuePlan& p, uint32_t* lds,
     auto issue_dma = [&](uint32_t row, uint32_t q1, const SetAddr& a) {
         if (!MEM) return;
         if constexpr (NODMA) {
-            if (row) split_direct_h0<NTQ0, 1>(p.rows, a, A, Q);
-            else if (q1) split_direct_h0<NTQ1, 1>(p.cols, a, A, Q);
-            else split_direct_h0<NTQ0, 1>(p.cols, a, A, Q);
+            if (row) split_direct_h0<NTQ0, 1, OPQ>(p.rows, a, A, Q);
+            else if (q1) split_direct_h0<NTQ1, 1, OPQ>(p.cols, a, A, Q);
+            else split_direct_h0<NTQ0, 1, OPQ>(p.cols, a, A, Q);
             return;
         }
         if (row) split_dma_h1<NTQ0>(p.rows, a, lds_base, A);
@@ -1036,29 +1083,29 @@ __device__ __forceinline__ void bs_split_wave(const QueuePlan& p, uint32_t* lds,
     auto issue_direct = [&](uint32_t row, uint32_t q1, const SetAddr& a) {
         if (!MEM) return;
         if constexpr (XLOAD) {  // P = h1
-            if (row) split_direct_h0<NTQ0, 1>(p.rows, a, A, P);
-            else if (q1) split_direct_h0<NTQ1, 1>(p.cols, a, A, P);
-            else split_direct_h0<NTQ0, 1>(p.cols, a, A, P);
+            if (row) split_direct_h0<NTQ0, 1, OPQ>(p.rows, a, A, P);
+            else if (q1) split_direct_h0<NTQ1, 1, OPQ>(p.cols, a, A, P);
+            else split_direct_h0<NTQ0, 1, OPQ>(p.cols, a, A, P);
             return;
         }
-        if (row) split_direct_h0<NTQ0>(p.rows, a, A, P);
-        else if (q1) split_direct_h0<NTQ1>(p.cols, a, A, P);
-        else split_direct_h0<NTQ0>(p.cols, a, A, P);
+        if (row) split_direct_h0<NTQ0, 0, OPQ>(p.rows, a, A, P);
+        else if (q1) split_direct_h0<NTQ1, 0, OPQ>(p.cols, a, A, P);
+        else split_direct_h0<NTQ0, 0, OPQ>(p.cols, a, A, P);
     };
     // XLOAD: h0 of a set straight into X[0..7]
     auto issue_x0 = [&](uint32_t row, uint32_t q1, const SetAddr& a) {
         uint32_t (&X0)[8][8] = *reinterpret_cast<uint32_t (*)[8][8]>(&X[0][0]);
         if (!MEM) return;
-        if (row) split_direct_h0<NTQ0, 0>(p.rows, a, A, X0);
-        else if (q1) split_direct_h0<NTQ1, 0>(p.cols, a, A, X0);
-        else split_direct_h0<NTQ0, 0>(p.cols, a, A, X0);
+        if (row) split_direct_h0<NTQ0, 0, OPQ>(p.rows, a, A, X0);
+        else if (q1) split_direct_h0<NTQ1, 0, OPQ>(p.cols, a, A, X0);
+        else split_direct_h0<NTQ0, 0, OPQ>(p.cols, a, A, X0);
     };
 
     // prologue: the first two items, taken synchronously; the first one loaded
     if (t0) {
         uint32_t sq0 = 0, sq1 = 0, r0 = 1, r1 = 1;
-        const uint32_t c0 = q_take(p, qc, true, sq0, r0);
-        const uint32_t c1 = c0 == kNone ? kNone : q_take(p, qc, false, sq1, r1);
+        const uint32_t c0 = q_take(p, qc, true, sq0, r0, G);
+        const uint32_t c1 = c0 == kNone ? kNone : q_take(p, qc, false, sq1, r1, G);
         slot[0] = c0;
         slot[1] = sq0;
         slot[4] = c1;
@@ -1211,7 +1258,7 @@ __device__ __forceinline__ void bs_split_wave(const QueuePlan& p, uint32_t* lds,
                     qc.main_done = 1u;
                     it = qc.res != kNone ? qc.res : kQExitCheck;
                 }
-                if (it == kQExitCheck) it = q_leave_or_claim(p);
+                if (it == kQExitCheck) it = q_leave_or_claim(p, G);
                 if (it == kNone || ((it & kQ1) && (it & ~kQ1) >= p.nq1)) {
                     nn = kNone;
                 } else {
@@ -1279,7 +1326,7 @@ __device__ __forceinline__ void bs_split_wave(const QueuePlan& p, uint32_t* lds,
                 else
 #endif
                 bs8::ph_w1_tr0(X, xw, xw + 65536u);  // + planes -> bytes of h0
-                split_store_h<0, false, true>(X, a, A, k, oo, es, crow != 0, MEM);
+                split_store_h<0, false, true, false, XCDQ, OPQ>(X, a, A, k, oo, es, crow != 0, MEM);
                 if constexpr (XLOAD) {
                     if (pre) {
                         issue_x0(nrow, nxt & kQ1, an);
@@ -1291,7 +1338,7 @@ __device__ __forceinline__ void bs_split_wave(const QueuePlan& p, uint32_t* lds,
                 if constexpr (XCH) bs8::xch_write_h1(X, xw, xw + 65536u);
                 if constexpr (!LATE0) {
                     if constexpr (ARITH) bs8::small_fft_h0_all(X, A);
-                    split_store_h<0, ARITH, true, OLDTP>(X, a, A, k, oo, es, crow != 0, MEM);
+                    split_store_h<0, ARITH, true, OLDTP, XCDQ, OPQ>(X, a, A, k, oo, es, crow != 0, MEM);
                 }
             }
             RSM_LDS_SYNC;
@@ -1310,11 +1357,11 @@ __device__ __forceinline__ void bs_split_wave(const QueuePlan& p, uint32_t* lds,
             }
             if constexpr (LATE0) {
                 if constexpr (ARITH) bs8::small_fft_h0_all(X, A);
-                split_store_h<0, ARITH, true, OLDTP>(X, a, A, k, oo, es, crow != 0, MEM);
+                split_store_h<0, ARITH, true, OLDTP, XCDQ, OPQ>(X, a, A, k, oo, es, crow != 0, MEM);
             }
             stamp(9);
             if constexpr (ARITH) bs8::small_fft_h1_all(X, A);
-            split_store_h<1, ARITH, true, OLDTP>(X, a, A, k, oo, es, crow != 0, MEM);
+            split_store_h<1, ARITH, true, OLDTP, XCDQ, OPQ>(X, a, A, k, oo, es, crow != 0, MEM);
             stamp(10);
             if constexpr (TRACE) if (threadIdx.x == 0) trace_stamp(p, it_no, 11, (crow ? 1u : 0u) | ((cur & kQ1) ? 2u : 0u) | (pre ? 0u : 4u));
             ++it_no;
@@ -1358,7 +1405,7 @@ __device__ __forceinline__ void bs_split_wave(const QueuePlan& p, uint32_t* lds,
             q_signal(p, pend);
         }
         __builtin_amdgcn_s_waitcnt(0x0F70);
-        slot[0] = q_add(&p.ctr[kQExit]) == gridDim.x - 1u ? 1u : 0u;
+        slot[0] = q_add(&p.ctr[kQExit]) == G - 1u ? 1u : 0u;
     }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     if (__builtin_amdgcn_readfirstlane(slot[0])) {
@@ -1537,6 +1584,10 @@ void set_bs128_diag_mode(int mode, int rev_col, int xcd) {
     g_diag_xcd.store(xcd);
 }
 void set_bs128_diag_row_mode(int mode) { g_diag_row_mode.store(mode); }
+bool bs128_diag_xcd_queues() {
+    const int m = g_diag_mode.load();
+    return m == 55000 || m == 55002 || m == 55004;
+}
 #endif
 
 hipError_t launch_encode_gf8_bs128(const CodewordSet& cs, hipStream_t st) {
@@ -1647,6 +1698,11 @@ hipError_t launch_extend_gf8_bs128_queue(const QueuePlan& p0, hipStream_t st) {
         case 51004: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<262148>), dim3(grid), dim3(512), 0, st, p); break;
         case 52040: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<4194304>), dim3(grid), dim3(512), 0, st, p); break;
         case 53000: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<8388608>), dim3(grid), dim3(512), 0, st, p); break;
+        // XCD-affine queues (needs count % 8 == 0 and the host's zeroed 8-XCD queue words)
+        case 56000: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<16777216 | 67108864>), dim3(grid), dim3(512), 0, st, p); break;
+        case 55000: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<16777216 | 33554432>), dim3(grid), dim3(512), 0, st, p); break;
+        case 55002: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<16777216 | 33554432 | 2>), dim3(grid), dim3(512), 0, st, p); break;
+        case 55004: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<16777216 | 33554432 | 4>), dim3(grid), dim3(512), 0, st, p); break;
         case 51006: hipLaunchKernelGGL((extend_gf8_bs128s_kernel<262146>), dim3(grid), dim3(512), 0, st, p); break;
         // round-2 schedule (bs_queue_wave) for A/B
         case 18472: hipLaunchKernelGGL((extend_gf8_bs128q_kernel<18472>), dim3(grid), dim3(512), 0, st, p); break;

@@ -370,7 +370,17 @@ int extend_squares_queue(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, u
     p.margin = margin == ~0u ? p.rn / 2 : margin;
     StreamScratch& ss = stream_scratch(ctx, st);
     std::lock_guard<std::mutex> lk(ss.mu);
+#ifdef RSM_DIAG
+    // XCD-affine queues (diagnostic): 8 blocks of queue words, zeroed before each launch
+    const bool xcdq = bs128_diag_xcd_queues();
+    if (xcdq && count % 8 != 0) return fail(RSM_EINVAL, "XCD-affine queues need a multiple of 8 squares");
+    if (int rc = queue_words(ss, xcdq ? count + 7 * kQueueFixedWords / 2 : count, st)) return rc;
+    if (xcdq) {
+        if (hipError_t e = hipMemsetAsync(ss.queue.ptr, 0, ss.queue.cap, st)) return hip_fail(e, "queue words");
+    }
+#else
     if (int rc = queue_words(ss, count, st)) return rc;
+#endif
     p.ctr = static_cast<uint32_t*>(ss.queue.ptr);
     p.err = static_cast<uint32_t*>(ss.qerr.ptr);
     if (hipError_t e = launch_extend_gf8_bs128_queue(p, st)) return hip_fail(e, "single-launch extension");

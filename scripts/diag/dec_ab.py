@@ -1,0 +1,80 @@
+"""Decode sweep A/B (diagnostic library): the c3 scheme (k of the 2k cells of every row
+erased, BenchmarkRepair), S = 512, decoded by rsm_decode_vectors_dev:
+  k = 128 (c3, GF(2^8)): present points loaded after the presence mask (production) or
+          every valid point up front (rsm_diag_set_dec8_early_loads, round 3);
+  k = 256, 200 (GF(2^16), m = 256): the single-pass decoder (dec16f_kernel,
+          production) or the five global passes (rsm_diag_set_dec16_five_pass).
+Every rebuilt square compared with the original EDS.  One JSON line per configuration.
+usage: python3 scripts/diag/dec_ab.py"""
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+
+import rsmt2d_amd as R  # noqa: E402
+
+D = R.diag_library()
+
+
+def chk(rc):
+    R._check_with(D, rc)
+
+
+def main():
+    ctx = ctypes.c_void_p()
+    chk(D.rsm_ctx_create(0, ctypes.byref(ctx)))
+    for k in (128, 256, 200):
+        S = 512
+        W = 2 * k
+        n = W * W * S
+        buf, ref = ctypes.c_void_p(), ctypes.c_void_p()
+        chk(D.rsm_dev_alloc(ctx, n, ctypes.byref(buf)))
+        chk(D.rsm_dev_alloc(ctx, n, ctypes.byref(ref)))
+        chk(D.rsm_dev_fill_random(ctx, ref.value, n, 0xD16 + k))
+        chk(D.rsm_extend_squares_dev(ctx, ref.value, k, S, 1, None))
+        chk(D.rsm_sync(ctx))
+        full = np.empty(n, np.uint8)
+        chk(D.rsm_memcpy(ctx, full.ctypes.data, ref.value, n, 1))
+        rng = np.random.default_rng(k)
+        present = np.ones((W, W), np.uint8)
+        for r in range(W):
+            present[r, rng.choice(W, size=k, replace=False)] = 0
+        damaged = (full.reshape(W, W, S) * present[:, :, None]).reshape(-1)
+        pres = ctypes.c_void_p()
+        idx = ctypes.c_void_p()
+        chk(D.rsm_dev_alloc(ctx, W * W, ctypes.byref(pres)))
+        chk(D.rsm_dev_alloc(ctx, 4 * W, ctypes.byref(idx)))
+        chk(D.rsm_memcpy(ctx, pres.value, present.ctypes.data, W * W, 0))
+        ids = np.arange(W, dtype=np.uint32)
+        chk(D.rsm_memcpy(ctx, idx.value, ids.ctypes.data, 4 * W, 0))
+        setter = D.rsm_diag_set_dec8_early_loads if k <= 128 else D.rsm_diag_set_dec16_five_pass
+        for rep in range(2):
+            for five in (0, 1):
+                chk(setter(five))
+                chk(D.rsm_memcpy(ctx, buf.value, damaged.ctypes.data, n, 0))
+                chk(D.rsm_decode_vectors_dev(ctx, buf.value, pres.value, k, S, 0, idx.value, W, None))
+                chk(D.rsm_sync(ctx))
+                eq = ctypes.c_int(0)
+                chk(D.rsm_dev_equal(ctx, buf.value, ref.value, n, None, ctypes.byref(eq)))
+                reps = 50 if k <= 128 else 10
+                t0 = time.perf_counter()
+                for _ in range(reps):
+                    chk(D.rsm_decode_vectors_dev(ctx, buf.value, pres.value, k, S, 0, idx.value, W, None))
+                chk(D.rsm_sync(ctx))
+                dt = (time.perf_counter() - t0) / reps
+                print(json.dumps({"k": k, "S": S, ("early_loads" if k <= 128 else "five_pass"): five, "rep": rep,
+                                  "sweep_ms": round(dt * 1e3, 4),
+                                  "frac": round(W * W * S / dt / 8e12, 4), "rebuilt_equal": bool(eq.value)}),
+                      flush=True)
+        chk(setter(0))
+        for b in (buf, ref, pres, idx):
+            chk(D.rsm_dev_free(ctx, b))
+
+
+if __name__ == "__main__":
+    main()

@@ -3,7 +3,7 @@ diagnostic mode (40 production, 50002 memory-only, 50004 compute-only) a child p
 runs scripts/diag/queue_ab.py with many steps while this process samples
 `rocm-smi --showpower --showclocks --json` (a sysfs read, no GPU work); prints the
 median power / sclk / mclk over the samples taken while the child ran.
-usage: python3 scripts/diag/power_probe.py [steps] [mode[:steps] ...]
+usage: python3 scripts/diag/power_probe.py [steps] [mode[:steps[:delay]] ...]
 (modes: 40 production, 50002 no arithmetic, 50004 no global memory, 50768 no LDS exchange,
 50772 arithmetic only, 50770 global memory only; per-mode steps so each runs ~10 s)
 """
@@ -50,9 +50,10 @@ def main(steps, modes=("40", "50002", "50004")):
     idle = [s for s in (sample() for _ in range(3)) if s]
     print(json.dumps({"mode": "idle", "samples": idle}), flush=True)
     for m in modes:
-        mode, _, st = m.partition(":")
+        mode, _, rest = m.partition(":")
+        st, _, delay = rest.partition(":")
         env = dict(os.environ, QAB_STEPS=st or str(steps))
-        child = subprocess.Popen([sys.executable, os.path.join(HERE, "queue_ab.py"), f"queue,256,3,2,{mode}"],
+        child = subprocess.Popen([sys.executable, os.path.join(HERE, "queue_ab.py"), f"queue,256,3,{delay or 2},{mode}"],
                                  env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
         time.sleep(4.0)  # context creation, buffers, warmup
         got = []
@@ -65,7 +66,7 @@ def main(steps, modes=("40", "50002", "50004")):
         line = next((json.loads(l) for l in reversed(res) if l.startswith("{")), None)
         summ = {k: statistics.median([g[k] for g in got if k in g]) for k in ("power_W", "sclk_MHz", "mclk_MHz")
                 if any(k in g for g in got)}
-        print(json.dumps({"mode": mode, "samples": len(got), **summ, "run": line}), flush=True)
+        print(json.dumps({"mode": mode, "delay": int(delay or 2), "samples": len(got), **summ, "run": line}), flush=True)
         if child.returncode:
             print("\n".join(res[-20:]), file=sys.stderr)
             sys.exit(1)

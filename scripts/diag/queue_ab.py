@@ -98,13 +98,27 @@ def run(cfg, steps=STEPS, warmup=6):
     ok = True
     # diagnostic modes whose output is wrong by design (no arithmetic / memory / exchange)
     WRONG = {"2", "4", "32768", "65536", "131072", "98304", "32772", "50002", "50004", "50768", "50772",
-             "51004", "51006", "51012", "51014", "50770"}
+             "51004", "51006", "51012", "51014", "50770", "55002", "55004"}
     if mode in WRONG or (kind == "two" and mode != "40"):
         ok = None  # diagnostic mode: output wrong by design, not checked
     elif kind == "queue":
         for st in streams:
             ok &= D.rsm_diag_queue_check(ctx, st) == 0
     last = bufs[(n[0] - 1) % nb]
+    if ok is not None and os.environ.get("QAB_CHECK_ALL", "0") == "1":
+        # every square of the last step against the product's two-launch form of the
+        # same Q0, compared on the device (an XCD-affine launch leaves an XCD's squares
+        # undone if that XCD got fewer workgroups than gridDim / 8)
+        ref = ctypes.c_void_p()
+        chk(D.rsm_dev_alloc(ctx, B * SQ, ctypes.byref(ref)))
+        chk(D.rsm_memcpy(ctx, ref.value, last, B * SQ, 2))
+        chk(D.rsm_extend_squares_phase_dev(ctx, ref.value, k, S, B, 1, None))
+        chk(D.rsm_extend_squares_phase_dev(ctx, ref.value, k, S, B, 2, None))
+        chk(D.rsm_sync(ctx))
+        eq = ctypes.c_int(0)
+        chk(D.rsm_dev_equal(ctx, ref.value, last, B * SQ, None, ctypes.byref(eq)))
+        ok &= bool(eq.value)
+        chk(D.rsm_dev_free(ctx, ref.value))
     from refcheck import matches_two_launch
     for j in ((0, B - 1) if ok is not None else ()):
         got = np.empty(SQ, np.uint8)
