@@ -7,10 +7,10 @@ Metric (BASELINE.json): GiB/s of device-resident 2D RS encode, k=128 square,
 A "step" = ComputeExtendedDataSquare's arithmetic (erasureExtendSquare,
 extendeddatasquare.go:154-227) over one batch of `--batch` independent squares
 already resident in HBM (the EDS buffer holds each ODS in its top-left quadrant,
-as the Go EDS aliases its input).  c2 default: 256 squares (8 GiB of EDS) per step
+as the Go EDS aliases its input).  c2 default: 512 squares (16 GiB of EDS) per step
 as ONE queue-driven launch (both passes, extend_gf8_bs128s_kernel: half-split
 bit-sliced sets), steps rotating over 3 streams and 3 buffers
-(24 GiB of the 288 GB), so no step finds its squares in the 256 MiB Infinity Cache.
+(48 GiB of the 288 GB), so no step finds its squares in the 256 MiB Infinity Cache.
 value = ODS bytes encoded per second over all ranks (GiB/s).
 
 N > 1 GPUs (one process per GPU, torch.distributed): every rank encodes its own
@@ -849,7 +849,10 @@ def main():
     # k = 128: one queue-driven launch per step (both passes; rsm_extend_squares_dev
     # takes it for batches of >= 2 squares) unless --two-launch
     single = k == 128 and not a.two_launch and not a.one_stream
-    B = a.batch or (256 if single else max(1, (1 << 30) // sq_bytes))
+    # k = 128: 512 squares (16 GiB of EDS) per launch -- the launch's start-up and tail
+    # are paid once per 512 squares (7.90 us per square against 8.01 at 256, same box,
+    # profiles/r04d_c2_variants_qab.jsonl)
+    B = a.batch or (512 if single else max(1, (1 << 30) // sq_bytes))
     nstreams = 1 if a.one_stream else (a.streams or (3 if single else 2))
     L = R.library()
     ctx = R.device_context(local)

@@ -524,12 +524,7 @@ __device__ __forceinline__ void dec_stamp(const DecodeSet& ds, int i) {
 #endif
 }
 
-// EARLY (device-resident A/B, the round-3 form): every valid point's load is issued
-// right behind the presence bytes, before the mask is known.  Production (EARLY =
-// false, as the zero-copy form): the presence bytes first, then only the PRESENT
-// points -- half the bytes, and the presence loads no longer queue behind a
-// chip-wide burst of point loads; the point loads then overlap the error locator.
-template <int NW, bool ZC, bool EARLY = false>
+template <int NW, bool ZC>
 __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t task, uint32_t (&xch)[256][64],
                                                   PermTab (&ptab)[2][256], PermTab (&stab)[257]) {
     constexpr int PW = 256 / NW, HALF = NW / 2;
@@ -595,7 +590,7 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
         for (int i = 0; i < kTabWords; ++i) sv[i] = tw[i * 64 + lane];
     }
     asm volatile("" ::: "memory");
-    if constexpr (!ZC && EARLY) load_points(valid);
+    if constexpr (!ZC) load_points(valid);
     if (w == 0) {
         uint32_t* st = reinterpret_cast<uint32_t*>(&stab[0]);
 #pragma unroll
@@ -609,7 +604,7 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
     auto present = [&](uint32_t e) -> bool { return (pres[e >> 6] >> (e & 63u)) & 1u; };
     const uint64_t have = pres_bits(pres, w < HALF ? k + ib : ib) & valid;
     if constexpr (!ZC) dec_stamp(ds, 1);
-    if constexpr (ZC || !EARLY) load_points(have);
+    if constexpr (ZC) load_points(have);
 
     // error locator (log domain), as decode_gf8_kernel: entries 4 lane .. 4 lane + 3;
     // wave 0 alone: it resolves each point's multiply table (ptab: the staged table of
@@ -710,12 +705,12 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
 constexpr int kSplitWaves = 16;
 
 // one workgroup per task (device-resident square)
-template <int NW, bool EARLY = false>
+template <int NW>
 __global__ __launch_bounds__(64 * NW, NW / 2) void decode_gf8_split_kernel(DecodeSet ds) {
     __shared__ uint32_t xch[256][64];
     __shared__ PermTab ptab[2][256];
     __shared__ PermTab stab[257];
-    decode_split_task<NW, false, EARLY>(ds, blockIdx.x, xch, ptab, stab);
+    decode_split_task<NW, false>(ds, blockIdx.x, xch, ptab, stab);
 }
 
 // zero-copy form: a capped grid loops over the tasks
@@ -1024,13 +1019,9 @@ static hipError_t launch_dec(const DecodeSet& ds, hipStream_t st) {
 
 #ifdef RSM_DIAG
 static std::atomic<uint32_t*> g_dec_trace{nullptr};
-static std::atomic<bool> g_dec_early{false};
 void set_dec_diag_trace(uint32_t* d) { g_dec_trace.store(d); }
-void set_dec8_diag_early_loads(bool on) { g_dec_early.store(on); }
-static bool dec8_early() { return g_dec_early.load(); }
 #else
 void set_dec_diag_trace(uint32_t*) {}
-static bool dec8_early() { return false; }
 #endif
 
 hipError_t launch_decode_gf8(const DecodeSet& ds0, hipStream_t st) {
@@ -1049,10 +1040,7 @@ hipError_t launch_decode_gf8(const DecodeSet& ds0, hipStream_t st) {
             hipLaunchKernelGGL(decode_gf8_split_zc_kernel<4>, dim3(grid), dim3(256), 0, st, ds);
         } else {
             constexpr int NW = kSplitWaves;
-            if (dec8_early())
-                hipLaunchKernelGGL((decode_gf8_split_kernel<NW, true>), dim3((uint32_t)tasks), dim3(64 * NW), 0, st, ds);
-            else
-                hipLaunchKernelGGL((decode_gf8_split_kernel<NW, false>), dim3((uint32_t)tasks), dim3(64 * NW), 0, st, ds);
+            hipLaunchKernelGGL(decode_gf8_split_kernel<NW>, dim3((uint32_t)tasks), dim3(64 * NW), 0, st, ds);
         }
         return hipGetLastError();
     }

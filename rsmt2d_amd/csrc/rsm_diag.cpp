@@ -74,11 +74,6 @@ int rsm_diag_set_enc16_e64(int on) {
     return RSM_OK;
 }
 
-int rsm_diag_set_dec8_early_loads(int on) {
-    set_dec8_diag_early_loads(on != 0);
-    return RSM_OK;
-}
-
 int rsm_diag_set_dec16_five_pass(int on) {
     set_dec16_diag_five_pass(on != 0);
     return RSM_OK;

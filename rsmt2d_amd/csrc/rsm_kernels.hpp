@@ -79,7 +79,6 @@ void set_split_diag_waves(int first, int second);  // diagnostic builds only
 void set_split_diag_fused(bool on);                  // diagnostic builds only
 void set_enc16_diag_e64(bool on);                    // diagnostic builds only
 void set_dec16_diag_five_pass(bool on);              // diagnostic builds only
-void set_dec8_diag_early_loads(bool on);             // diagnostic builds only
 bool bs128_diag_xcd_queues();                        // diagnostic builds only: XCD-affine queue mode set
 bool split_fused_enabled();                          // product: always
 // One square in ONE launch of the split encoder (rows -> Q1, Q0 columns -> Q2, then

@@ -1,7 +1,5 @@
 """Decode sweep A/B (diagnostic library): the c3 scheme (k of the 2k cells of every row
 erased, BenchmarkRepair), S = 512, decoded by rsm_decode_vectors_dev:
-  k = 128 (c3, GF(2^8)): present points loaded after the presence mask (production) or
-          every valid point up front (rsm_diag_set_dec8_early_loads, round 3);
   k = 256, 200 (GF(2^16), m = 256): the single-pass decoder (dec16f_kernel,
           production) or the five global passes (rsm_diag_set_dec16_five_pass).
 Every rebuilt square compared with the original EDS.  One JSON line per configuration.
@@ -28,7 +26,7 @@ def chk(rc):
 def main():
     ctx = ctypes.c_void_p()
     chk(D.rsm_ctx_create(0, ctypes.byref(ctx)))
-    for k in (128, 256, 200):
+    for k in (256, 200):
         S = 512
         W = 2 * k
         n = W * W * S
@@ -52,7 +50,7 @@ def main():
         chk(D.rsm_memcpy(ctx, pres.value, present.ctypes.data, W * W, 0))
         ids = np.arange(W, dtype=np.uint32)
         chk(D.rsm_memcpy(ctx, idx.value, ids.ctypes.data, 4 * W, 0))
-        setter = D.rsm_diag_set_dec8_early_loads if k <= 128 else D.rsm_diag_set_dec16_five_pass
+        setter = D.rsm_diag_set_dec16_five_pass
         for rep in range(2):
             for five in (0, 1):
                 chk(setter(five))

@@ -232,7 +232,7 @@ def test_single_launch_batches_on_three_streams(lib):
 
 
 def test_single_launch_at_bench_scale(lib):
-    """The bench's exact configuration (bench.py c2: k = 128, S = 512, 256 squares per
+    """The bench's exact configuration (bench.py c2: k = 128, S = 512, 512 squares per
     launch, launches on 3 streams over 3 buffers, running concurrently): EVERY square
     of every launch equals the two-launch result, compared on the device
     (rsm_dev_equal), over several rounds.  The parity quadrants are re-poisoned
@@ -241,7 +241,7 @@ def test_single_launch_at_bench_scale(lib):
     accident; the two-launch references are themselves oracle-checked at their
     first and last square.  Reference: extendeddatasquare.go:154-227."""
     ctx = R.device_context(0)
-    k, S, B, NS = 128, 512, 256, 3
+    k, S, B, NS = 128, 512, 512, 3
     W = 2 * k
     sq = W * W * S
     n = sq * B
