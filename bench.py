@@ -97,10 +97,15 @@ def cpu_baseline(k, S, seconds):
     GF2P8AFFINEQB multiplies, fused butterflies -- libleopard_gfni.so; else the AVX2
     pshufb build), multithreaded over codewords with the reference's two-phase
     schedule, writing into a reused EDS buffer (no page faults in the timed loop).
-    Threads: one per CPU of this process's affinity mask (os.sched_getaffinity -- the
-    CPUs the job may actually run on; os.cpu_count() is the whole machine); the mask is
-    recorded, and the single-thread rate plus its linear all-host-CPUs extrapolation are
-    reported beside it.  Not the reference: its Go/klauspost code cannot run here."""
+    Threads: the CPUs this job may actually use -- its affinity mask
+    (os.sched_getaffinity; os.cpu_count() is the whole machine), capped by its cgroup
+    CPU share -- the cgroup quota (cpu.max) when one is set, else the share the
+    harness declares for worker pools (OMP_NUM_THREADS): on the GPU box the mask is all
+    256 host CPUs but the share is 16, and 256 threads there ran at 5.8 GiB/s against
+    18-19 for 16 (profiles/r04f_bench.json).  The mask, the quota, a short run with one
+    thread per CPU of the mask, the single-thread rate and its linear all-host-CPUs
+    extrapolation are reported beside it.  Not the reference: its Go/klauspost code
+    cannot run here."""
     import numpy as np
     import oracle
     ncpu = os.cpu_count() or 1
@@ -108,7 +113,12 @@ def cpu_baseline(k, S, seconds):
         mask = sorted(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         mask = list(range(ncpu))
-    threads = max(1, len(mask))
+    # the job's CPU share: its cgroup quota, else the share the harness declares for
+    # worker pools (OMP_NUM_THREADS), else the whole affinity mask
+    quota, share_src = _cgroup_cpu_quota(), "cgroup cpu.max"
+    if not quota and os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        quota, share_src = int(os.environ["OMP_NUM_THREADS"]), "OMP_NUM_THREADS"
+    threads = max(1, min(len(mask), quota) if quota else len(mask))
     gfni = oracle.gfni_supported() and k <= 128
     ext = oracle.extend_square_gfni if gfni else oracle.extend_square_simd if k <= 128 else None
     ods = oracle.splitmix64_bytes(k * k * S).reshape(k, k, S)
@@ -144,17 +154,40 @@ def cpu_baseline(k, S, seconds):
 
     n, dt = rate(threads, seconds)
     n1, dt1 = rate(1, max(2.0, seconds / 4))
+    nm, dtm = rate(len(mask), max(2.0, seconds / 4)) if len(mask) != threads else (n, dt)
     model, _ = cpu_info()
     tech = ("AVX-512 + GFNI (GF2P8AFFINEQB multiplies, fused butterflies)" if gfni
             else "AVX2 pshufb nibble tables" if ext else "scalar tables")
     return {"value": round(n * k * k * S / dt / 2**30, 4), "unit": "GiB/s", "cores": threads,
             "kind": "port", "cpu_model": model, "host_cpus": ncpu, "affinity": _ranges(mask),
+            "cpu_share": quota, "cpu_share_source": share_src if quota else None,
+            "affinity_threads_GiB_s": round(nm * k * k * S / dtm / 2**30, 4),
             "single_thread_GiB_s": round(n1 * k * k * S / dt1 / 2**30, 4),
             "all_cores_estimate_GiB_s": round(n1 * k * k * S / dt1 / 2**30 * ncpu, 1),
             "sample": f"{n} squares k={k} S={S} ({dt:.1f} s) through oracle/leopard_oracle.c ({tech}; restatement "
-                      f"of klauspost leopard8, not the reference), {threads} threads (one per CPU of the affinity "
-                      f"mask) each extending whole squares; single thread: {n1} squares in {dt1:.1f} s; "
-                      f"all_cores_estimate = single-thread rate x {ncpu} host CPUs (linear, not measured)"}
+                      f"of klauspost leopard8, not the reference), {threads} threads (the affinity mask of "
+                      f"{len(mask)} CPUs capped by the job's CPU share {quota} from {share_src}) each extending "
+                      f"whole squares; "
+                      f"affinity_threads: {len(mask)} threads, {nm} squares in {dtm:.1f} s; single thread: {n1} "
+                      f"squares in {dt1:.1f} s; all_cores_estimate = single-thread rate x {ncpu} host CPUs "
+                      f"(linear, not measured)"}
+
+
+def _cgroup_cpu_quota():
+    """CPUs of this job's cgroup CPU quota (cgroup v2 cpu.max "quota period", v1
+    cfs_quota_us / cfs_period_us), rounded up; None when unlimited or unreadable."""
+    import math
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else max(1, math.ceil(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else max(1, math.ceil(q / per))
+    except (OSError, ValueError):
+        return None
 
 
 def _ranges(cpus):
