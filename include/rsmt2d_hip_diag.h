@@ -35,8 +35,11 @@ int rsm_diag_set_split_waves(int first, int second);
 /* One square in the latency form: 1 = one launch with a device-side wait (A/B only:
  * slower), 0 = two launches (production). */
 int rsm_diag_set_split_fused(int on);
-/* GF(2^16) m = 512 encoder form: 1 = 8 waves x 64 elements (A/B), 0 = 16 x 32 (production). */
-int rsm_diag_set_enc16_e64(int on);
+/* GF(2^16) m = 512 encoder form: 0 = production (16 waves x 32 elements, persistent, LDS
+ * tables, half exchange buffer), 1 = 8 waves x 64 elements, 2 = the round-3 16-wave form
+ * (scalar tables), 3 = form 2 with the half exchange buffer, 5 = form 0 with just-in-time
+ * table reads. */
+int rsm_diag_set_enc16_e64(int mode);
 /* GF(2^16) m = 256 decoder: 1 = the five global passes (A/B), 0 = the single-pass kernel (production). */
 int rsm_diag_set_dec16_five_pass(int on);
 /* Both passes of `count` in-place k = 128 squares in ONE persistent launch

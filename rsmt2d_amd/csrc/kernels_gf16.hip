@@ -254,6 +254,28 @@ __device__ __forceinline__ void tab_load(const uint32_t* lds, uint32_t (&c)[kTab
         c[4 * q] = v.x; c[4 * q + 1] = v.y; c[4 * q + 2] = v.z; c[4 * q + 3] = v.w;
     });
 }
+// The same as ONE asm statement that waits for its own reads: the compiler can
+// neither hoist a later block's table above the butterflies nor keep several tables
+// live (the 128-register 16-wave kernels spilled ~700 dwords with tab_load).
+__device__ __forceinline__ void tab_load_jit(const uint32_t* lds, uint32_t (&c)[kTabW]) {
+    v4u16 a, b, e, f, g;
+    const uint32_t base = (uint32_t)(uintptr_t)lds;
+    asm volatile(
+        "ds_read_b128 %0, %5\n\t"
+        "ds_read_b128 %1, %5 offset:16\n\t"
+        "ds_read_b128 %2, %5 offset:32\n\t"
+        "ds_read_b128 %3, %5 offset:48\n\t"
+        "ds_read_b128 %4, %5 offset:64\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(a), "=&v"(b), "=&v"(e), "=&v"(f), "=&v"(g)
+        : "v"(base)
+        : "memory");
+    c[0] = a.x; c[1] = a.y; c[2] = a.z; c[3] = a.w;
+    c[4] = b.x; c[5] = b.y; c[6] = b.z; c[7] = b.w;
+    c[8] = e.x; c[9] = e.y; c[10] = e.z; c[11] = e.w;
+    c[12] = f.x; c[13] = f.y; c[14] = f.z; c[15] = f.w;
+    c[16] = g.x; c[17] = g.y; c[18] = g.z; c[19] = g.w;
+}
 // Butterflies with the twiddle table given directly (zero table = no multiply).
 __device__ __forceinline__ void ifft2t(uint32_t& xl, uint32_t& xh, uint32_t& yl, uint32_t& yh, const PermTab16& t) {
     yl ^= xl;
@@ -333,7 +355,7 @@ __device__ __forceinline__ void stage_res(uint32_t* tab, const PermTab16* tw, in
 
 // Group layout (E elements per wave): IFFT layers d = 1..E/2 ascending / FFT
 // d = E/2..1 descending; the table of (layer, block) from this wave's E-1 slots.
-template <int E, bool FFT>
+template <int E, bool FFT, bool JIT = false>
 __device__ __forceinline__ void grp_xform(uint32_t (&l)[E], uint32_t (&h)[E], const uint32_t* wtab) {
     constexpr int LN = ilog2c(E);
     sfor<LN>([&](auto LGi) {
@@ -342,11 +364,14 @@ __device__ __forceinline__ void grp_xform(uint32_t (&l)[E], uint32_t (&h)[E], co
         sfor<E / 2 / d>([&](auto Bk) {
             constexpr int block = decltype(Bk)::value;
             uint32_t c[kTabW];
-            tab_load(wtab + (E - (E >> L) + block) * kTabW, c);
+            if constexpr (JIT) tab_load_jit(wtab + (E - (E >> L) + block) * kTabW, c);
+            else tab_load(wtab + (E - (E >> L) + block) * kTabW, c);
             sfor<d>([&](auto Q) {
                 constexpr int i = block * 2 * d + decltype(Q)::value;
                 if constexpr (FFT) fft2v(l[i], h[i], l[i + d], h[i + d], c);
                 else ifft2v(l[i], h[i], l[i + d], h[i + d], c);
+                // JIT: pin the block's butterflies before the next block's table read
+                if constexpr (JIT) asm volatile("" : "+v"(l[i]), "+v"(h[i]), "+v"(l[i + d]), "+v"(h[i + d]));
             });
         });
     });
@@ -371,7 +396,14 @@ __device__ __forceinline__ void grp_xform_g(uint32_t (&l)[E], uint32_t (&h)[E], 
         });
     });
 }
-template <int E, int R, bool FFT, bool MERGED = false>
+// Residue-layout register of (residue s of the wave, j): s R + j (the full-buffer
+// exchange), or -- IL, the half-buffer exchange -- (E / R) j + s, so that the
+// registers a wave sends in one pass of xch_plane_half are exactly the ones it
+// receives into (element bit 0 = s picks the pass in both layouts).
+template <int E, int R, bool IL>
+constexpr int ridx(int s, int j) { return IL ? (E / R) * j + s : s * R + j; }
+
+template <int E, int R, bool FFT, bool MERGED = false, bool IL = false>
 __device__ __forceinline__ void res_xform_g(uint32_t (&l)[E], uint32_t (&h)[E], const PermTab16* tw, int off) {
     constexpr int LN = ilog2c(R), NL = MERGED ? LN - 1 : LN;  // MERGED: the top layer is res_mid
     sfor<NL>([&](auto LGi) {
@@ -383,9 +415,9 @@ __device__ __forceinline__ void res_xform_g(uint32_t (&l)[E], uint32_t (&h)[E], 
             sfor<dj>([&](auto Q) {
                 constexpr int j = bl + decltype(Q)::value;
                 sfor<E / R>([&](auto Sx) {
-                    constexpr int i = R * decltype(Sx)::value + j;
-                    if constexpr (FFT) fft2t(l[i], h[i], l[i + dj], h[i + dj], t);
-                    else ifft2t(l[i], h[i], l[i + dj], h[i + dj], t);
+                    constexpr int i = ridx<E, R, IL>(decltype(Sx)::value, j), i2 = ridx<E, R, IL>(decltype(Sx)::value, j + dj);
+                    if constexpr (FFT) fft2t(l[i], h[i], l[i2], h[i2], t);
+                    else ifft2t(l[i], h[i], l[i2], h[i2], t);
                 });
             });
         });
@@ -411,22 +443,24 @@ __device__ __forceinline__ void res_mid(uint32_t (&l)[E], uint32_t (&h)[E], cons
 // Residue layout: register s*R + j holds element r_s + E j; a layer over j at
 // distance dj joins elements E dj apart (block start E bl): one table per
 // (layer, block) for every residue of every wave.
-template <int E, int R, bool FFT>
+template <int E, int R, bool FFT, bool MERGED = true, bool JIT = false, bool IL = false>
 __device__ __forceinline__ void res_xform(uint32_t (&l)[E], uint32_t (&h)[E], const uint32_t* rtab) {
-    constexpr int LN = ilog2c(R);
-    sfor<LN - 1>([&](auto LGi) {  // the top layer (dj = R/2) is res_mid
-        constexpr int L = FFT ? LN - 2 - decltype(LGi)::value : decltype(LGi)::value;
+    constexpr int LN = ilog2c(R), NL = MERGED ? LN - 1 : LN;
+    sfor<NL>([&](auto LGi) {  // MERGED: the top layer (dj = R/2) is res_mid
+        constexpr int L = FFT ? NL - 1 - decltype(LGi)::value : decltype(LGi)::value;
         constexpr int dj = 1 << L;
         sfor<R / 2 / dj>([&](auto Bk) {
             constexpr int block = decltype(Bk)::value;
             uint32_t c[kTabW];
-            tab_load(rtab + ((FFT ? R - 1 : 0) + (R - (R >> L)) + block) * kTabW, c);
+            if constexpr (JIT) tab_load_jit(rtab + ((FFT ? R - 1 : 0) + (R - (R >> L)) + block) * kTabW, c);
+            else tab_load(rtab + ((FFT ? R - 1 : 0) + (R - (R >> L)) + block) * kTabW, c);
             sfor<dj>([&](auto Q) {
                 constexpr int j = block * 2 * dj + decltype(Q)::value;
                 sfor<E / R>([&](auto Sx) {
-                    constexpr int i = R * decltype(Sx)::value + j;
-                    if constexpr (FFT) fft2v(l[i], h[i], l[i + dj], h[i + dj], c);
-                    else ifft2v(l[i], h[i], l[i + dj], h[i + dj], c);
+                    constexpr int i = ridx<E, R, IL>(decltype(Sx)::value, j), i2 = ridx<E, R, IL>(decltype(Sx)::value, j + dj);
+                    if constexpr (FFT) fft2v(l[i], h[i], l[i2], h[i2], c);
+                    else ifft2v(l[i], h[i], l[i2], h[i2], c);
+                    if constexpr (JIT) asm volatile("" : "+v"(l[i]), "+v"(h[i]), "+v"(l[i2]), "+v"(h[i2]));
                 });
             });
         });
@@ -452,6 +486,36 @@ __device__ __forceinline__ void xch_plane(uint32_t (&v)[E], uint32_t (*xch)[64],
     __syncthreads();
 }
 
+// One plane of the layout switch through HALF an element-indexed buffer xch[N/2][64]
+// (the other half of the LDS holds the twiddle tables), in two passes: pass p moves
+// the elements with bit 0 = p.  Group layout: register i = element E w + i (bit 0
+// = bit 0 of i); residue layout with the IL register order ridx(s, j) = RPW j + s:
+// element RPW w + s + E j, bit 0 = s (RPW = 2).  So in each pass a wave sends and
+// receives the SAME registers (even ones, then odd ones), and no register is
+// overwritten before it has been sent.  Buffer slot = element >> 1.
+template <int E, int R, bool TO_RESIDUE>
+__device__ __forceinline__ void xch_plane_half(uint32_t (&v)[E], uint32_t (*xch)[64], uint32_t w, uint32_t lane) {
+    constexpr int RPW = E / R;
+    static_assert(RPW == 2, "two residues per wave: element bit 0 = the residue's parity");
+    sfor<2>([&](auto Pc) {
+        constexpr int pp = decltype(Pc)::value;
+        auto grp_slot = [&](int i) { return (E * w + (uint32_t)i) >> 1; };
+        auto res_slot = [&](int j) { return (RPW * w + (uint32_t)pp + E * (uint32_t)j) >> 1; };
+        if constexpr (TO_RESIDUE) {
+            sfor<E / 2>([&](auto I) { constexpr int i = 2 * decltype(I)::value + pp; xch[grp_slot(i)][lane] = v[i]; });
+        } else {
+            sfor<R>([&](auto J) { constexpr int j = decltype(J)::value; xch[res_slot(j)][lane] = v[ridx<E, R, true>(pp, j)]; });
+        }
+        __syncthreads();
+        if constexpr (TO_RESIDUE) {
+            sfor<R>([&](auto J) { constexpr int j = decltype(J)::value; v[ridx<E, R, true>(pp, j)] = xch[res_slot(j)][lane]; });
+        } else {
+            sfor<E / 2>([&](auto I) { constexpr int i = 2 * decltype(I)::value + pp; v[i] = xch[grp_slot(i)][lane]; });
+        }
+        __syncthreads();
+    });
+}
+
 // Encoder: parity of codeword q, chunk c (512 bytes) = FFT(IFFT(data)).  The
 // encoder's IFFT uses SKEW[m - 1 + b + d] (data occupy the upper half of the
 // 2m-point domain), its FFT SKEW[b + d - 1]; every index is < 2m <= kSkewPermN.
@@ -469,12 +533,21 @@ __device__ __forceinline__ void xch_plane(uint32_t (&v)[E], uint32_t (*xch)[64],
 // E = 64 (m = 512 only, round 3q): 8 waves of 64 elements, 256 registers each (the
 // 16-wave form is held to 128 registers and spills 44 dwords per lane); the merged
 // middle pair is affordable there.
-template <int M, int E = 32>
+// HX (m = 512, 16 waves; production HX = 3 since round 4): persistent, the twiddle
+// tables staged in LDS beside HALF an exchange buffer (two passes per plane,
+// xch_plane_half, the IL residue register order); the top residue layer pair is not
+// merged (128 registers).  1.5-2.5 % faster than the round-3 form with scalar-loaded
+// tables (HX = 0, one workgroup per task) -- the tables were not what held it at ~5.8
+// cycles per VALU instruction.
+// HX bits: 1 half exchange buffer (persistent), 2 LDS tables, 4 just-in-time table reads
+template <int M, int E = 32, int HX = 0>
 __global__ __launch_bounds__(M * 64 / E, M == 256 ? 2 : (E == 32 ? 4 : 1)) void enc16_kernel(Enc16 p) {
     constexpr int WAVES = M / E, R = M / E;
-    constexpr bool LDS_TAB = M == 256;
+    constexpr bool LDS_TAB = M == 256 || (HX & 2);
+    constexpr bool JIT = (HX & 4) != 0;
+    static_assert(!HX || (M == 512 && E == 32), "HX: the 16-wave m = 512 form");
     constexpr int GT = WAVES * (E - 1) * kTabW;
-    __shared__ uint32_t xch[M][64];
+    __shared__ uint32_t xch[HX ? M / 2 : M][64];
     __shared__ uint32_t tabs[LDS_TAB ? 2 * GT + 2 * (R - 1) * kTabW : 1];
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
     uint32_t* gI = tabs;
@@ -501,6 +574,24 @@ __global__ __launch_bounds__(M * 64 / E, M == 256 ? 2 : (E == 32 ? 4 : 1)) void 
             l[i] = ld(in, ln.lo, so);
             h[i] = ld(in, ln.lo + 32, so);
         });
+        if constexpr (HX != 0) {
+            __syncthreads();  // tables staged (first task)
+            if constexpr (LDS_TAB) grp_xform<E, false, JIT>(l, h, gI + w * (E - 1) * kTabW);
+            else grp_xform_g<E, false>(l, h, p.tw, (int)(E * w), M - 1);
+            xch_plane_half<E, R, true>(l, xch, w, lane);
+            xch_plane_half<E, R, true>(h, xch, w, lane);
+            if constexpr (LDS_TAB) {
+                res_xform<E, R, false, false, JIT, true>(l, h, rtab);
+                res_xform<E, R, true, false, JIT, true>(l, h, rtab);
+            } else {
+                res_xform_g<E, R, false, false, true>(l, h, p.tw, M - 1);
+                res_xform_g<E, R, true, false, true>(l, h, p.tw, 0);
+            }
+            xch_plane_half<E, R, false>(l, xch, w, lane);
+            xch_plane_half<E, R, false>(h, xch, w, lane);
+            if constexpr (LDS_TAB) grp_xform<E, true, JIT>(l, h, gF + w * (E - 1) * kTabW);
+            else grp_xform_g<E, true>(l, h, p.tw, (int)(E * w), 0);
+        } else {
         if constexpr (LDS_TAB) {
             __syncthreads();  // tables staged (first task)
             grp_xform<E, false>(l, h, gI + w * (E - 1) * kTabW);
@@ -525,6 +616,7 @@ __global__ __launch_bounds__(M * 64 / E, M == 256 ? 2 : (E == 32 ? 4 : 1)) void 
         xch_plane<E, R, false>(h, xch, w, lane);
         if constexpr (LDS_TAB) grp_xform<E, true>(l, h, gF + w * (E - 1) * kTabW);
         else grp_xform_g<E, true>(l, h, p.tw, (int)(E * w), 0);
+        }
         const auto out = rsrc(p.cs.out_base + rel);
         sfor<E>([&](auto I) {
             constexpr int i = decltype(I)::value;
@@ -795,47 +887,69 @@ __global__ __launch_bounds__(256) void dec16_p5(Dec16 p) {  // group: FFT low + 
 //   group layout   FFT d = 16..1; reveal the missing shares (times exp(-err)).
 // The error locators come from errloc16_kernel (one workgroup per codeword).
 // ---------------------------------------------------------------------------
+// The formal derivative of one plane in the residue layout (see dec16f_kernel), in
+// two passes over the element halves (the L partners e + 2^t, t < 5, share e's half):
+// each pass publishes that half's pre-derivative values to LDS, then every wave
+// updates its registers of that half in ascending j.
 template <int E, int R>
 __device__ __forceinline__ void deriv_plane(uint32_t (&v)[E], uint32_t (*xch)[64], uint32_t w, uint32_t lane) {
-    constexpr int RPW = E / R;  // residues per wave; register s*R + j holds element RPW w + s + E j
-    sfor<E>([&](auto I) {
-        constexpr int i = decltype(I)::value;
-        xch[(RPW * w + i / R) + E * (i % R)][lane] = v[i];
-    });
-    __syncthreads();
-    sfor<RPW>([&](auto Sx) {
-        constexpr int sx = decltype(Sx)::value;
-        const uint32_t r = RPW * w + sx;  // residue = the element's low 5 bits
-        sfor<R>([&](auto J) {  // ascending j: v[s*R + j + 2^t] is still the pre-derivative value
-            constexpr int j = decltype(J)::value;
-            constexpr int i = sx * R + j;
-            uint32_t a = v[i];
-            sfor<12>([&](auto T) {  // H: the element's high bits (t >= 5) = bits of j
-                constexpr int t = decltype(T)::value;
-                if constexpr ((1 << t) < R && ((j >> t) & 1) == 0) a ^= v[i + (1 << t)];
+    // residues per wave; register ridx(s, j) = RPW j + s (IL) holds element RPW w + s + E j
+    constexpr int RPW = E / R, HJ = R / 2;
+    sfor<2>([&](auto Hc) {
+        constexpr int hf = decltype(Hc)::value;
+        sfor<RPW>([&](auto Sx) {
+            sfor<HJ>([&](auto J) {
+                constexpr int sx = decltype(Sx)::value, j = hf * HJ + decltype(J)::value;
+                xch[(RPW * w + sx) + E * (j - hf * HJ)][lane] = v[ridx<E, R, true>(sx, j)];
             });
-            sfor<5>([&](auto T) {  // L: bits of the residue, from the plane in LDS
-                constexpr uint32_t bit = 1u << decltype(T)::value;
-                if ((r & bit) == 0u) a ^= xch[(r + bit) + E * j][lane];
-            });
-            v[i] = a;
         });
+        __syncthreads();
+        sfor<RPW>([&](auto Sx) {
+            constexpr int sx = decltype(Sx)::value;
+            const uint32_t r = RPW * w + sx;  // residue = the element's low 5 bits
+            sfor<HJ>([&](auto J) {  // ascending j: register (sx, j + 2^t) still holds the pre-derivative value
+                constexpr int j = hf * HJ + decltype(J)::value;
+                constexpr int i = ridx<E, R, true>(sx, j);
+                uint32_t a = v[i];
+                sfor<12>([&](auto T) {  // H: the element's high bits (t >= 5) = bits of j
+                    constexpr int t = decltype(T)::value;
+                    if constexpr ((1 << t) < R && ((j >> t) & 1) == 0) a ^= v[ridx<E, R, true>(sx, j + (1 << t))];
+                });
+                sfor<5>([&](auto T) {  // L: bits of the residue, from this half's plane in LDS
+                    constexpr uint32_t bit = 1u << decltype(T)::value;
+                    if ((r & bit) == 0u) a ^= xch[(r + bit) + E * (j - hf * HJ)][lane];
+                });
+                v[i] = a;
+            });
+        });
+        __syncthreads();
     });
-    __syncthreads();
 }
 
+// Twiddle tables staged once per workgroup in LDS and read by uniform ds_read_b128
+// (enc16_kernel<256>'s scheme; a scalar table load from L2 per butterfly block left
+// the 16-wave kernels waiting, ~6.6 cycles per VALU instruction): the exchange
+// buffer is half the elements (two passes per plane) so the tables fit beside it.
 template <int M>
 __global__ __launch_bounds__(1024, 4) void dec16f_kernel(Dec16 p) {
     constexpr int N = 2 * M, E = 32, R = N / E, WAVES = N / E;
     static_assert(WAVES == 16 && R == 16, "n = 512: 16 waves of 32 elements, residues of 16");
-    __shared__ uint32_t xch[N][64];
+    constexpr int GT = WAVES * (E - 1) * kTabW;  // group tables of one direction (words)
+    __shared__ uint32_t xch[N / 2][64];
+    __shared__ uint32_t tabs[2 * GT + 2 * (R - 1) * kTabW];
+    uint32_t* gI = tabs;
+    uint32_t* gF = tabs + GT;
+    uint32_t* rtab = tabs + 2 * GT;
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    // decoder skews: IFFT SKEW[-1 + b + d] (off = -1), FFT SKEW[b + d - 1]
+    stage_grp<WAVES, E, false>(gI, p.tw, -1);
+    stage_grp<WAVES, E, true>(gF, p.tw, 0);
+    stage_res<R, E, WAVES * 64>(rtab, p.tw, -1);
     const uint32_t task = blockIdx.x;
     const uint32_t q = task / p.chunks, chunk = task - q * p.chunks;
     const Lane ln = lane_of(chunk, p.ds.S);
     const uint32_t k = p.ds.k, S = p.ds.S;
     const auto sq = rsrc(p.ds.base);
-    const PermTab16* tw = p.tw;
     // work slot e <- share: e < k parity k + e, M <= e < M + k data e - M, else zero
     auto share_of = [&](uint32_t e) -> uint32_t {
         return e < k ? k + e : (e >= (uint32_t)M && e < (uint32_t)M + k) ? e - (uint32_t)M : 0xFFFFFFFFu;
@@ -861,16 +975,17 @@ __global__ __launch_bounds__(1024, 4) void dec16f_kernel(Dec16 p) {
         constexpr int i = decltype(I)::value;
         if ((have >> i) & 1u) mul16(l[i], h[i], p.r.perm[err_of(p, q, E * w + i, N)]);
     });
-    grp_xform_g<E, false>(l, h, tw, (int)(E * w), -1);
-    xch_plane<E, R, true>(l, xch, w, lane);
-    xch_plane<E, R, true>(h, xch, w, lane);
-    res_xform_g<E, R, false>(l, h, tw, -1);
+    __syncthreads();  // tables staged
+    grp_xform<E, false, true>(l, h, gI + w * (E - 1) * kTabW);
+    xch_plane_half<E, R, true>(l, xch, w, lane);
+    xch_plane_half<E, R, true>(h, xch, w, lane);
+    res_xform<E, R, false, false, true, true>(l, h, rtab);
     deriv_plane<E, R>(l, xch, w, lane);
     deriv_plane<E, R>(h, xch, w, lane);
-    res_xform_g<E, R, true>(l, h, tw, 0);
-    xch_plane<E, R, false>(l, xch, w, lane);
-    xch_plane<E, R, false>(h, xch, w, lane);
-    grp_xform_g<E, true>(l, h, tw, (int)(E * w), 0);
+    res_xform<E, R, true, false, true, true>(l, h, rtab);
+    xch_plane_half<E, R, false>(l, xch, w, lane);
+    xch_plane_half<E, R, false>(h, xch, w, lane);
+    grp_xform<E, true, true>(l, h, gF + w * (E - 1) * kTabW);
     sfor<E>([&](auto I) {
         constexpr int i = decltype(I)::value;
         const uint32_t e = E * w + i;
@@ -1112,11 +1227,16 @@ __global__ __launch_bounds__(1024) void errloc16g_kernel(G16Pass p) {
 inline uint32_t blocks_for(uint64_t tasks) { return (uint32_t)((tasks + 3) / 4); }
 
 // m = 512 encoder form: 16 waves x 32 elements (production) or 8 x 64 (diagnostic A/B)
+// (diagnostic A/B: rsm_diag_set_enc16_e64 1 = 8 waves x 64 elements, 2 = the
+// round-3 16-wave form with scalar-loaded tables, one workgroup per task, 3 = that
+// form with the half exchange buffer, 5 = production with just-in-time table reads)
 #ifdef RSM_DIAG
-static std::atomic<bool> g_enc16_e64{false};
-static bool enc16_e64() { return g_enc16_e64.load(); }
+static std::atomic<int> g_enc16_e64{0};
+static bool enc16_e64() { return g_enc16_e64.load() == 1; }
+static int enc16_form() { return g_enc16_e64.load(); }
 #else
 static bool enc16_e64() { return false; }
+static int enc16_form() { return 0; }
 #endif
 
 template <int M>
@@ -1133,11 +1253,22 @@ hipError_t run_encode(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st) {
     // m = 256: persistent, one workgroup per CU (its twiddle tables stay in LDS);
     // m = 512: one workgroup per task (measured faster: the 16-wave form leaves no
     // registers for a persistent loop's state)
-    const uint32_t grid = M == 256 && tasks > g.cus ? g.cus : (uint32_t)tasks;
+    const uint32_t pgrid = tasks > g.cus ? g.cus : (uint32_t)tasks;  // persistent forms
+    const uint32_t grid = M == 256 ? pgrid : (uint32_t)tasks;
     if constexpr (M == 512) {
         if (enc16_e64()) {
             hipLaunchKernelGGL((enc16_kernel<512, 64>), dim3(grid), dim3(512), 0, st, p);
             return hipGetLastError();
+        }
+        // production (form 0): persistent, LDS tables beside a half exchange buffer,
+        // compiler-scheduled table reads -- c5 0.568-0.574 ms per square against
+        // 0.581-0.583 for the round-3 form (2) and 0.584 with just-in-time table reads
+        // (5), profiles/r04j_gf16_enc_ab.jsonl
+        switch (enc16_form()) {
+            case 0: hipLaunchKernelGGL((enc16_kernel<512, 32, 3>), dim3(pgrid), dim3(1024), 0, st, p); return hipGetLastError();
+            case 3: hipLaunchKernelGGL((enc16_kernel<512, 32, 1>), dim3(grid), dim3(1024), 0, st, p); return hipGetLastError();
+            case 5: hipLaunchKernelGGL((enc16_kernel<512, 32, 7>), dim3(pgrid), dim3(1024), 0, st, p); return hipGetLastError();
+            default: break;
         }
     }
     hipLaunchKernelGGL(enc16_kernel<M>, dim3(grid), dim3(M * 2), 0, st, p);
@@ -1342,7 +1473,7 @@ static hipError_t run_decode_generic(const DecodeSet& ds, const Gf16Dev& g, hipS
 }  // namespace
 
 #ifdef RSM_DIAG
-void set_enc16_diag_e64(bool on) { g_enc16_e64.store(on); }
+void set_enc16_diag_e64(int mode) { g_enc16_e64.store(mode); }
 void set_dec16_diag_five_pass(bool on) { g_dec16_five.store(on); }
 #endif
 

@@ -69,8 +69,8 @@ int rsm_diag_set_split_fused(int on) {
     return RSM_OK;
 }
 
-int rsm_diag_set_enc16_e64(int on) {
-    set_enc16_diag_e64(on != 0);
+int rsm_diag_set_enc16_e64(int mode) {
+    set_enc16_diag_e64(mode);
     return RSM_OK;
 }
 

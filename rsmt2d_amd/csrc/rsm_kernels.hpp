@@ -77,7 +77,7 @@ hipError_t launch_decode_gf8(const DecodeSet& ds, hipStream_t st);
 hipError_t launch_encode_gf8_split(const CodewordSet& a, const CodewordSet* b, hipStream_t st);
 void set_split_diag_waves(int first, int second);  // diagnostic builds only
 void set_split_diag_fused(bool on);                  // diagnostic builds only
-void set_enc16_diag_e64(bool on);                    // diagnostic builds only
+void set_enc16_diag_e64(int mode);                   // diagnostic builds only
 void set_dec16_diag_five_pass(bool on);              // diagnostic builds only
 bool bs128_diag_xcd_queues();                        // diagnostic builds only: XCD-affine queue mode set
 bool split_fused_enabled();                          // product: always

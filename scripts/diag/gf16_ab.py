@@ -1,7 +1,9 @@
 """GF(2^16) encoder A/B (diagnostic library): device time per c5 square (k = 512,
-S = 512) and per c4 square (k = 256, S = 2048) with the m = 512 encoder as 8 waves x
-64 elements or 16 x 32 (rsm_diag_set_enc16_e64); the c5 output is checked against
-the other form's.  One JSON line per configuration.
+S = 512) with the m = 512 encoder forms of rsm_diag_set_enc16_e64 (0 production:
+16 waves, persistent, LDS tables beside a half exchange buffer; 2 the round-3
+scalar-table form; 3 form 2 with the half buffer; 5 form 0 with just-in-time table
+reads); every output is checked against the round-3 form's.  One JSON line
+per configuration.
 usage: python3 scripts/diag/gf16_ab.py"""
 import ctypes
 import json
@@ -33,7 +35,7 @@ def main():
     chk(D.rsm_dev_alloc(ctx, n, ctypes.byref(p)))
     outs = {}
     for rep in range(2):
-        for e64 in (1, 0):
+        for e64 in (2, 0, 3, 5):
             chk(D.rsm_diag_set_enc16_e64(e64))
             chk(D.rsm_dev_fill_random(ctx, p.value, n, 7))
             chk(D.rsm_extend_squares_dev(ctx, p.value, k, S, 1, None))
@@ -49,9 +51,8 @@ def main():
             chk(D.rsm_sync(ctx))
             ms = ctypes.c_float()
             chk(D.rsm_event_elapsed_ms(e0, e1, ctypes.byref(ms)))
-            print(json.dumps({"e64": e64, "rep": rep, "c5_ms_per_square": round(ms.value / reps, 4),
-                              "same_output": bool(np.array_equal(outs[e64], outs[1 - e64])) if 1 - e64 in outs
-                              else None}), flush=True)
+            print(json.dumps({"form": e64, "rep": rep, "c5_ms_per_square": round(ms.value / reps, 4),
+                              "same_as_round3_form": bool(np.array_equal(outs[e64], outs[2]))}), flush=True)
     chk(D.rsm_diag_set_enc16_e64(0))
 
 
