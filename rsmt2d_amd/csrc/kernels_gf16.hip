@@ -541,7 +541,7 @@ __device__ __forceinline__ void xch_plane_half(uint32_t (&v)[E], uint32_t (*xch)
 // cycles per VALU instruction.
 // HX bits: 1 half exchange buffer (persistent), 2 LDS tables, 4 just-in-time table reads
 template <int M, int E = 32, int HX = 0>
-__global__ __launch_bounds__(M * 64 / E, M == 256 ? 2 : (E == 32 ? 4 : 1)) void enc16_kernel(Enc16 p) {
+__global__ __launch_bounds__(M * 64 / E, (M == 256 && E == 32) ? 2 : (E <= 32 ? 4 : 1)) void enc16_kernel(Enc16 p) {
     constexpr int WAVES = M / E, R = M / E;
     constexpr bool LDS_TAB = M == 256 || (HX & 2);
     constexpr bool JIT = (HX & 4) != 0;
@@ -1269,6 +1269,13 @@ hipError_t run_encode(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st) {
             case 3: hipLaunchKernelGGL((enc16_kernel<512, 32, 1>), dim3(grid), dim3(1024), 0, st, p); return hipGetLastError();
             case 5: hipLaunchKernelGGL((enc16_kernel<512, 32, 7>), dim3(pgrid), dim3(1024), 0, st, p); return hipGetLastError();
             default: break;
+        }
+    }
+    if constexpr (M == 256) {
+        // diagnostic form 6: 16 waves x 16 elements (4 waves per SIMD, 128 registers)
+        if (enc16_form() == 6) {
+            hipLaunchKernelGGL((enc16_kernel<256, 16>), dim3(grid), dim3(1024), 0, st, p);
+            return hipGetLastError();
         }
     }
     hipLaunchKernelGGL(enc16_kernel<M>, dim3(grid), dim3(M * 2), 0, st, p);
