@@ -38,7 +38,8 @@ int rsm_diag_set_split_fused(int on);
 /* GF(2^16) m = 512 encoder form: 0 = production (16 waves x 32 elements, persistent, LDS
  * tables, half exchange buffer), 1 = 8 waves x 64 elements, 2 = the round-3 16-wave form
  * (scalar tables), 3 = form 2 with the half exchange buffer, 5 = form 0 with just-in-time
- * table reads. */
+ * table reads.  m = 256: 7 = 8 waves x 32 elements (the form through round 3), any other
+ * value the production 16 waves x 16 elements. */
 int rsm_diag_set_enc16_e64(int mode);
 /* GF(2^16) m = 256 decoder: 1 = the five global passes (A/B), 0 = the single-pass kernel (production). */
 int rsm_diag_set_dec16_five_pass(int on);

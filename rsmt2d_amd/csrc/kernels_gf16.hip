@@ -1272,8 +1272,10 @@ hipError_t run_encode(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st) {
         }
     }
     if constexpr (M == 256) {
-        // diagnostic form 6: 16 waves x 16 elements (4 waves per SIMD, 128 registers)
-        if (enc16_form() == 6) {
+        // production since round 4: 16 waves x 16 elements (4 waves per SIMD, 128
+        // registers), c4 0.417-0.427 ms per square against 0.435-0.450 for 8 waves x 32
+        // elements (diagnostic form 7; profiles/r04k_gf16_enc_ab.jsonl)
+        if (enc16_form() != 7) {
             hipLaunchKernelGGL((enc16_kernel<256, 16>), dim3(grid), dim3(1024), 0, st, p);
             return hipGetLastError();
         }
