@@ -43,6 +43,9 @@ int rsm_diag_set_split_fused(int on);
 int rsm_diag_set_enc16_e64(int mode);
 /* GF(2^16) m = 256 decoder: 1 = the five global passes (A/B), 0 = the single-pass kernel (production). */
 int rsm_diag_set_dec16_five_pass(int on);
+/* GF(2^8) split decoder A/B: the upper half of the grid delays its point loads by
+ * `ticks` of the 100 MHz s_memrealtime clock (0 = off, production). */
+int rsm_diag_set_dec_delay(uint32_t ticks);
 /* Both passes of `count` in-place k = 128 squares in ONE persistent launch
  * (extend_gf8_bs128q_kernel: row and Q0-column sets from one queue, Q1-column sets
  * from a ready list; `delay` squares of row sets lead the Q0-column sets).

@@ -424,19 +424,40 @@ __device__ __forceinline__ void res_xform_g(uint32_t (&l)[E], uint32_t (&h)[E], 
     });
 }
 // The merged top pair of the residue layers (elements E R / 2 = m / 2 apart), see Enc16::mid.
-template <int E, int R>
+template <int E, int R, bool IL = false>
 __device__ __forceinline__ void res_mid(uint32_t (&l)[E], uint32_t (&h)[E], const PermTab16* mid) {
     constexpr int dj = R / 2;
     if (!mid) return;  // y ^= x twice: the identity
     const PermTab16& t = *mid;
     sfor<E / R>([&](auto Sx) {
         sfor<dj>([&](auto Q) {
-            constexpr int i = R * decltype(Sx)::value + decltype(Q)::value;
-            l[i + dj] ^= l[i];
-            h[i + dj] ^= h[i];
-            muladd16(l[i], h[i], l[i + dj], h[i + dj], t);
-            l[i + dj] ^= l[i];
-            h[i + dj] ^= h[i];
+            constexpr int i = ridx<E, R, IL>(decltype(Sx)::value, decltype(Q)::value);
+            constexpr int i2 = ridx<E, R, IL>(decltype(Sx)::value, decltype(Q)::value + dj);
+            l[i2] ^= l[i];
+            h[i2] ^= h[i];
+            muladd16(l[i], h[i], l[i2], h[i2], t);
+            l[i2] ^= l[i];
+            h[i2] ^= h[i];
+        });
+    });
+}
+// The same with the table read from LDS (mtab: kTabW words, staged from Enc16::mid).
+template <int E, int R, bool IL, bool JIT>
+__device__ __forceinline__ void res_mid_v(uint32_t (&l)[E], uint32_t (&h)[E], const uint32_t* mtab) {
+    constexpr int dj = R / 2;
+    uint32_t c[kTabW];
+    if constexpr (JIT) tab_load_jit(mtab, c);
+    else tab_load(mtab, c);
+    sfor<E / R>([&](auto Sx) {
+        sfor<dj>([&](auto Q) {
+            constexpr int i = ridx<E, R, IL>(decltype(Sx)::value, decltype(Q)::value);
+            constexpr int i2 = ridx<E, R, IL>(decltype(Sx)::value, decltype(Q)::value + dj);
+            l[i2] ^= l[i];
+            h[i2] ^= h[i];
+            muladd16v(l[i], h[i], l[i2], h[i2], c);
+            l[i2] ^= l[i];
+            h[i2] ^= h[i];
+            if constexpr (JIT) asm volatile("" : "+v"(l[i]), "+v"(h[i]), "+v"(l[i2]), "+v"(h[i2]));
         });
     });
 }
@@ -539,16 +560,18 @@ __device__ __forceinline__ void xch_plane_half(uint32_t (&v)[E], uint32_t (*xch)
 // merged (128 registers).  1.5-2.5 % faster than the round-3 form with scalar-loaded
 // tables (HX = 0, one workgroup per task) -- the tables were not what held it at ~5.8
 // cycles per VALU instruction.
-// HX bits: 1 half exchange buffer (persistent), 2 LDS tables, 4 just-in-time table reads
+// HX bits: 1 half exchange buffer (persistent), 2 LDS tables, 4 just-in-time table reads,
+// 8 the merged middle residue pair (res_mid)
 template <int M, int E = 32, int HX = 0>
 __global__ __launch_bounds__(M * 64 / E, (M == 256 && E == 32) ? 2 : (E <= 32 ? 4 : 1)) void enc16_kernel(Enc16 p) {
     constexpr int WAVES = M / E, R = M / E;
     constexpr bool LDS_TAB = M == 256 || (HX & 2);
     constexpr bool JIT = (HX & 4) != 0;
+    constexpr bool MID = (HX & 8) != 0;  // the merged middle pair (res_mid)
     static_assert(!HX || (M == 512 && E == 32), "HX: the 16-wave m = 512 form");
     constexpr int GT = WAVES * (E - 1) * kTabW;
     __shared__ uint32_t xch[HX ? M / 2 : M][64];
-    __shared__ uint32_t tabs[LDS_TAB ? 2 * GT + 2 * (R - 1) * kTabW : 1];
+    __shared__ uint32_t tabs[LDS_TAB ? 2 * GT + (2 * (R - 1) + (MID ? 1 : 0)) * kTabW : 1];
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
     uint32_t* gI = tabs;
     uint32_t* gF = tabs + GT;
@@ -557,6 +580,8 @@ __global__ __launch_bounds__(M * 64 / E, (M == 256 && E == 32) ? 2 : (E <= 32 ? 
         stage_grp<WAVES, E, false>(gI, p.tw, M - 1);
         stage_grp<WAVES, E, true>(gF, p.tw, 0);
         stage_res<R, E, WAVES * 64>(rtab, p.tw, M - 1);
+        if constexpr (MID)
+            if (p.mid && threadIdx.x < (uint32_t)kTabW) rtab[2 * (R - 1) * kTabW + threadIdx.x] = p.mid->w[tab_word((int)threadIdx.x)];
     }
     const uint32_t es = (uint32_t)p.cs.elem_stride, k = p.cs.k;
     const uint32_t oo = (uint32_t)p.cs.out_offset;
@@ -581,8 +606,10 @@ __global__ __launch_bounds__(M * 64 / E, (M == 256 && E == 32) ? 2 : (E <= 32 ? 
             xch_plane_half<E, R, true>(l, xch, w, lane);
             xch_plane_half<E, R, true>(h, xch, w, lane);
             if constexpr (LDS_TAB) {
-                res_xform<E, R, false, false, JIT, true>(l, h, rtab);
-                res_xform<E, R, true, false, JIT, true>(l, h, rtab);
+                res_xform<E, R, false, MID, JIT, true>(l, h, rtab);
+                if constexpr (MID)
+                    if (p.mid) res_mid_v<E, R, true, JIT>(l, h, rtab + 2 * (R - 1) * kTabW);
+                res_xform<E, R, true, MID, JIT, true>(l, h, rtab);
             } else {
                 res_xform_g<E, R, false, false, true>(l, h, p.tw, M - 1);
                 res_xform_g<E, R, true, false, true>(l, h, p.tw, 0);
@@ -1268,6 +1295,8 @@ hipError_t run_encode(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st) {
             case 0: hipLaunchKernelGGL((enc16_kernel<512, 32, 3>), dim3(pgrid), dim3(1024), 0, st, p); return hipGetLastError();
             case 3: hipLaunchKernelGGL((enc16_kernel<512, 32, 1>), dim3(grid), dim3(1024), 0, st, p); return hipGetLastError();
             case 5: hipLaunchKernelGGL((enc16_kernel<512, 32, 7>), dim3(pgrid), dim3(1024), 0, st, p); return hipGetLastError();
+            case 8: hipLaunchKernelGGL((enc16_kernel<512, 32, 11>), dim3(pgrid), dim3(1024), 0, st, p); return hipGetLastError();
+            case 9: hipLaunchKernelGGL((enc16_kernel<512, 32, 15>), dim3(pgrid), dim3(1024), 0, st, p); return hipGetLastError();
             default: break;
         }
     }

@@ -590,6 +590,14 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
         for (int i = 0; i < kTabWords; ++i) sv[i] = tw[i * 64 + lane];
     }
     asm volatile("" ::: "memory");
+#ifdef RSM_DIAG
+    if constexpr (!ZC) {
+        if (ds.delay && blockIdx.x >= gridDim.x / 2u) {  // A/B: stagger the two halves' loads
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            while (__builtin_amdgcn_s_memrealtime() - t0 < ds.delay) __builtin_amdgcn_s_sleep(2);
+        }
+    }
+#endif
     if constexpr (!ZC) load_points(valid);
     if (w == 0) {
         uint32_t* st = reinterpret_cast<uint32_t*>(&stab[0]);
@@ -1019,17 +1027,22 @@ static hipError_t launch_dec(const DecodeSet& ds, hipStream_t st) {
 
 #ifdef RSM_DIAG
 static std::atomic<uint32_t*> g_dec_trace{nullptr};
+static std::atomic<uint32_t> g_dec_delay{0};
 void set_dec_diag_trace(uint32_t* d) { g_dec_trace.store(d); }
+void set_dec_diag_delay(uint32_t ticks) { g_dec_delay.store(ticks); }
 #else
 void set_dec_diag_trace(uint32_t*) {}
+void set_dec_diag_delay(uint32_t) {}
 #endif
 
 hipError_t launch_decode_gf8(const DecodeSet& ds0, hipStream_t st) {
     DecodeSet ds = ds0;
 #ifdef RSM_DIAG
     ds.trace = g_dec_trace.load();
+    ds.delay = g_dec_delay.load();
 #else
     ds.trace = nullptr;
+    ds.delay = 0;
 #endif
     if (ceil_pow2(ds.k) == 128) {  // split form: kSplitWaves waves per (codeword, 256 B chunk)
         const uint64_t tasks = (uint64_t)ds.count * ds.chunks;

@@ -84,6 +84,11 @@ int rsm_diag_set_dec_trace(void* d_trace) {
     return RSM_OK;
 }
 
+int rsm_diag_set_dec_delay(uint32_t ticks) {
+    set_dec_diag_delay(ticks);
+    return RSM_OK;
+}
+
 int rsm_diag_set_bs_row_mode(int mode) {
     set_bs128_diag_row_mode(mode);
     return RSM_OK;

@@ -61,9 +61,13 @@ struct DecodeSet {
     // diagnostic builds only: per-workgroup phase stamps of the M = 128 split decoder
     // (kDecTraceWords s_memrealtime values per workgroup; nullptr = off)
     uint32_t* trace;
+    // diagnostic builds only: the upper half of the split decoder's grid issues its
+    // point loads `delay` s_memrealtime ticks (100 MHz) after it starts (0 = off)
+    uint32_t delay;
 };
 constexpr int kDecTraceWords = 8;
 void set_dec_diag_trace(uint32_t* d);
+void set_dec_diag_delay(uint32_t ticks);
 
 hipError_t launch_encode_gf8(const CodewordSet& cs, hipStream_t st);
 // bit-sliced M = 128 encode (kernels_gf8_bs.hip); launch_encode_gf8 picks it when applicable

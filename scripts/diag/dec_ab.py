@@ -1,8 +1,10 @@
 """Decode sweep A/B (diagnostic library): the c3 scheme (k of the 2k cells of every row
 erased, BenchmarkRepair), S = 512, decoded by rsm_decode_vectors_dev:
   k = 256, 200 (GF(2^16), m = 256): the single-pass decoder (dec16f_kernel,
-          production) or the five global passes (rsm_diag_set_dec16_five_pass).
-Every rebuilt square compared with the original EDS.  One JSON line per configuration.
+          production) or the five global passes (rsm_diag_set_dec16_five_pass);
+  k = 128 (GF(2^8) split decoder): the upper half of the grid delays its point loads by
+          DECAB_DELAYS ticks of the 100 MHz clock (rsm_diag_set_dec_delay; 0 = production).
+DECAB_KS picks the k values (default 256,200).  Every rebuilt square compared with the original EDS.  One JSON line per configuration.
 usage: python3 scripts/diag/dec_ab.py"""
 import ctypes
 import json
@@ -26,7 +28,7 @@ def chk(rc):
 def main():
     ctx = ctypes.c_void_p()
     chk(D.rsm_ctx_create(0, ctypes.byref(ctx)))
-    for k in (256, 200):
+    for k in [int(x) for x in os.environ.get("DECAB_KS", "256,200").split(",")]:
         S = 512
         W = 2 * k
         n = W * W * S
@@ -50,9 +52,10 @@ def main():
         chk(D.rsm_memcpy(ctx, pres.value, present.ctypes.data, W * W, 0))
         ids = np.arange(W, dtype=np.uint32)
         chk(D.rsm_memcpy(ctx, idx.value, ids.ctypes.data, 4 * W, 0))
-        setter = D.rsm_diag_set_dec16_five_pass
+        setter = D.rsm_diag_set_dec16_five_pass if k > 128 else D.rsm_diag_set_dec_delay
+        variants = (0, 1) if k > 128 else [int(x) for x in os.environ.get("DECAB_DELAYS", "0,150,300,450").split(",")]
         for rep in range(2):
-            for five in (0, 1):
+            for five in variants:
                 chk(setter(five))
                 chk(D.rsm_memcpy(ctx, buf.value, damaged.ctypes.data, n, 0))
                 chk(D.rsm_decode_vectors_dev(ctx, buf.value, pres.value, k, S, 0, idx.value, W, None))
@@ -65,7 +68,7 @@ def main():
                     chk(D.rsm_decode_vectors_dev(ctx, buf.value, pres.value, k, S, 0, idx.value, W, None))
                 chk(D.rsm_sync(ctx))
                 dt = (time.perf_counter() - t0) / reps
-                print(json.dumps({"k": k, "S": S, ("early_loads" if k <= 128 else "five_pass"): five, "rep": rep,
+                print(json.dumps({"k": k, "S": S, ("delay_ticks" if k <= 128 else "five_pass"): five, "rep": rep,
                                   "sweep_ms": round(dt * 1e3, 4),
                                   "frac": round(W * W * S / dt / 8e12, 4), "rebuilt_equal": bool(eq.value)}),
                       flush=True)

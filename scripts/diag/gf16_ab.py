@@ -3,7 +3,8 @@ S = 512) with the m = 512 encoder forms of rsm_diag_set_enc16_e64 (0 production:
 16 waves, persistent, LDS tables beside a half exchange buffer; 2 the round-3
 scalar-table form; 3 form 2 with the half buffer; 5 form 0 with just-in-time table
 reads); every output is checked against the round-3 form's.  One JSON line
-per configuration.
+per configuration.  GF16AB_FORMS (comma list) picks the m = 512 forms, GF16AB_REPS the
+repetitions, GF16AB_C4=0 skips the c4 part (single-form runs under rocprofv3 --pmc).
 usage: python3 scripts/diag/gf16_ab.py"""
 import ctypes
 import json
@@ -34,8 +35,10 @@ def main():
     p = ctypes.c_void_p()
     chk(D.rsm_dev_alloc(ctx, n, ctypes.byref(p)))
     outs = {}
-    for rep in range(2):
-        for e64 in (2, 0, 3, 5):
+    forms = [int(f) for f in os.environ.get("GF16AB_FORMS", "2,0,5,8,9").split(",")]
+    base = forms[0]
+    for rep in range(int(os.environ.get("GF16AB_REPS", "2"))):
+        for e64 in forms:
             chk(D.rsm_diag_set_enc16_e64(e64))
             chk(D.rsm_dev_fill_random(ctx, p.value, n, 7))
             chk(D.rsm_extend_squares_dev(ctx, p.value, k, S, 1, None))
@@ -52,8 +55,10 @@ def main():
             ms = ctypes.c_float()
             chk(D.rsm_event_elapsed_ms(e0, e1, ctypes.byref(ms)))
             print(json.dumps({"form": e64, "rep": rep, "c5_ms_per_square": round(ms.value / reps, 4),
-                              "same_as_round3_form": bool(np.array_equal(outs[e64], outs[2]))}), flush=True)
+                              f"same_as_form{base}": bool(np.array_equal(outs[e64], outs[base]))}), flush=True)
     chk(D.rsm_diag_set_enc16_e64(0))
+    if os.environ.get("GF16AB_C4", "1") == "0":
+        return
     # c4 (k = 256, S = 2048, 2 squares per step): m = 256 as 16 waves x 16 elements
     # (production since round 4, form 0) or 8 x 32 (form 7)
     k, S, B = 256, 2048, 2

@@ -1,8 +1,8 @@
 #!/bin/bash
-# r04 l: GF(2^16) parity with the 16-wave m=256 encoder in production + encoder form A/B
+# r04 l: GF(2^16) parity + encoder form A/B
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=gpurun_out/r04l; mkdir -p $OUT
+OUT=gpurun_out/${RUN:-r04l}; mkdir -p $OUT
 step() { local n=$1 t=$2; shift 2; echo "[$(date +%T)] $n" >> $OUT/steps.log; timeout -k 10 $t "$@" > $OUT/$n.log 2>&1; local rc=$?; echo "[$(date +%T)] $n rc=$rc" >> $OUT/steps.log; tail -n 14 $OUT/$n.log; return $rc; }
 step tests 300 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_gf16.py tests/test_gpu_gf16_large.py tests/test_gpu_runtime.py || exit 3
 step enc 240 python3 scripts/diag/gf16_ab.py || exit 3
