@@ -6,9 +6,10 @@
 // bytes, 4 hi bytes), so a wavefront spans 8 blocks = 512 bytes of share width
 // and every multiply-by-constant is 12 v_perm_b32 lookups (PermTab16).
 //
-// Encode (m = ceilPow2(k) in {256, 512}) is ONE pass per codeword: a workgroup of
-// m/32 waves owns a (codeword, 512-byte chunk) and keeps its m-point IFFT + FFT on
-// chip -- each wave holds E = 32 elements in registers, and one LDS exchange
+// Encode (m = ceilPow2(k) in {256, 512}) is ONE pass per codeword: a workgroup owns a
+// (codeword, chunk) and keeps its m-point IFFT + FFT on chip (m = 256: 256-byte chunks,
+// one element per lane-half, enc16h_kernel; m = 512 as follows) -- a workgroup of
+// m/32 waves, each holding E = 32 elements of a 512-byte chunk in registers; one LDS exchange
 // buffer ([element][lane] dwords, one plane at a time) switches between
 //   group layout   (wave w: elements 32 w .. 32 w + 31):  layers d < 32
 //   residue layout (wave w: residues r = (32/R) w + s, elements r + 32 j, j < R =
@@ -310,9 +311,9 @@ __device__ __forceinline__ int slot_layer(int slot, int n) {
 // Stage into LDS `tab` the group-layout tables of every wave (wave w: E - 1
 // slots, elements E w ..): IFFT SKEW[off + b + d] or FFT SKEW[b + d - 1].  Fixed
 // trip count, loads first: every thread's table words are in flight at once.
-template <int WAVES, int E, bool FFT>
+template <int WAVES, int E, bool FFT, int THREADS = WAVES * 64>
 __device__ __forceinline__ void stage_grp(uint32_t* tab, const PermTab16* tw, int off) {
-    constexpr int NT = WAVES * (E - 1), THREADS = WAVES * 64, PER = (NT * kTabW + THREADS - 1) / THREADS;
+    constexpr int NT = WAVES * (E - 1), PER = (NT * kTabW + THREADS - 1) / THREADS;
     uint32_t v[PER];
 #pragma unroll
     for (int r = 0; r < PER; ++r) {
@@ -517,19 +518,25 @@ __device__ __forceinline__ void xch_plane(uint32_t (&v)[E], uint32_t (*xch)[64],
 template <int E, int R, bool TO_RESIDUE>
 __device__ __forceinline__ void xch_plane_half(uint32_t (&v)[E], uint32_t (*xch)[64], uint32_t w, uint32_t lane) {
     constexpr int RPW = E / R;
-    static_assert(RPW == 2, "two residues per wave: element bit 0 = the residue's parity");
+    static_assert(RPW % 2 == 0, "an even number of residues per wave: element bit 0 = bit 0 of s");
     sfor<2>([&](auto Pc) {
         constexpr int pp = decltype(Pc)::value;
         auto grp_slot = [&](int i) { return (E * w + (uint32_t)i) >> 1; };
-        auto res_slot = [&](int j) { return (RPW * w + (uint32_t)pp + E * (uint32_t)j) >> 1; };
+        auto res_slot = [&](int s, int j) { return (RPW * w + (uint32_t)s + E * (uint32_t)j) >> 1; };
         if constexpr (TO_RESIDUE) {
             sfor<E / 2>([&](auto I) { constexpr int i = 2 * decltype(I)::value + pp; xch[grp_slot(i)][lane] = v[i]; });
         } else {
-            sfor<R>([&](auto J) { constexpr int j = decltype(J)::value; xch[res_slot(j)][lane] = v[ridx<E, R, true>(pp, j)]; });
+            sfor<RPW / 2>([&](auto Sx) {
+                constexpr int sr = 2 * decltype(Sx)::value + pp;
+                sfor<R>([&](auto J) { constexpr int j = decltype(J)::value; xch[res_slot(sr, j)][lane] = v[ridx<E, R, true>(sr, j)]; });
+            });
         }
         __syncthreads();
         if constexpr (TO_RESIDUE) {
-            sfor<R>([&](auto J) { constexpr int j = decltype(J)::value; v[ridx<E, R, true>(pp, j)] = xch[res_slot(j)][lane]; });
+            sfor<RPW / 2>([&](auto Sx) {
+                constexpr int sr = 2 * decltype(Sx)::value + pp;
+                sfor<R>([&](auto J) { constexpr int j = decltype(J)::value; v[ridx<E, R, true>(sr, j)] = xch[res_slot(sr, j)][lane]; });
+            });
         } else {
             sfor<E / 2>([&](auto I) { constexpr int i = 2 * decltype(I)::value + pp; v[i] = xch[grp_slot(i)][lane]; });
         }
@@ -563,12 +570,12 @@ __device__ __forceinline__ void xch_plane_half(uint32_t (&v)[E], uint32_t (*xch)
 // HX bits: 1 half exchange buffer (persistent), 2 LDS tables, 4 just-in-time table reads,
 // 8 the merged middle residue pair (res_mid)
 template <int M, int E = 32, int HX = 0>
-__global__ __launch_bounds__(M * 64 / E, (M == 256 && E == 32) ? 2 : (E <= 32 ? 4 : 1)) void enc16_kernel(Enc16 p) {
+__global__ __launch_bounds__(M * 64 / E, HX ? 4 : ((M == 256 && E == 32) ? 2 : (E <= 32 ? 4 : 1))) void enc16_kernel(Enc16 p) {
     constexpr int WAVES = M / E, R = M / E;
     constexpr bool LDS_TAB = M == 256 || (HX & 2);
     constexpr bool JIT = (HX & 4) != 0;
     constexpr bool MID = (HX & 8) != 0;  // the merged middle pair (res_mid)
-    static_assert(!HX || (M == 512 && E == 32), "HX: the 16-wave m = 512 form");
+    static_assert(!HX || E == 32, "HX: waves of 32 elements");
     constexpr int GT = WAVES * (E - 1) * kTabW;
     __shared__ uint32_t xch[HX ? M / 2 : M][64];
     __shared__ uint32_t tabs[LDS_TAB ? 2 * GT + (2 * (R - 1) + (MID ? 1 : 0)) * kTabW : 1];
@@ -657,6 +664,88 @@ __global__ __launch_bounds__(M * 64 / E, (M == 256 && E == 32) ? 2 : (E <= 32 ? 
         for (uint32_t task = blockIdx.x; task < tasks; task += gridDim.x) run(task);
     } else {
         run(blockIdx.x);  // grid = tasks
+    }
+}
+
+// Half-wave form of the m = 256 encoder (round 4): one task per (codeword, 256-byte
+// chunk), so each lane-half (32 lanes x 4 symbols = 256 bytes) holds ONE element's
+// chunk and every register two elements: half g = 2 w + (lane >> 5) of wave w.
+//   group layout   (half g: elements 16 g .. 16 g + 15):  layers d = 1..8, each half
+//                  reading its own twiddle tables (per-lane LDS address: one address
+//                  per 16-lane LDS group, a broadcast)
+//   residue layout (half g: elements g + 16 j, j < 16):  layers d = 16..128, tables
+//                  shared by all lanes
+// State is 32 registers per lane and the LDS 73 KiB (one plane of a [256][32]
+// exchange buffer + the tables), so TWO 8-wave workgroups share a CU: one's loads and
+// stores overlap the other's butterflies (the 512-byte-chunk forms hold 128 KiB of
+// state per task and run one workgroup per CU, their memory phases exposed).
+template <int E>
+__device__ __forceinline__ void xch_halfwave(uint32_t (&v)[E], uint32_t (*xch)[32], uint32_t g, uint32_t l32, bool to_res) {
+    sfor<E>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        xch[to_res ? E * g + i : g + E * i][l32] = v[i];
+    });
+    __syncthreads();
+    sfor<E>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        v[i] = xch[to_res ? g + E * i : E * g + i][l32];
+    });
+    __syncthreads();
+}
+
+template <bool JIT>
+__global__ __launch_bounds__(512, 4) void enc16h_kernel(Enc16 p) {
+    constexpr int M = 256, E = 16, G = 16, R = 16, THREADS = 512;
+    constexpr int GT = G * (E - 1) * kTabW;
+    __shared__ uint32_t xch[M][32];
+    __shared__ uint32_t tabs[2 * GT + 2 * (R - 1) * kTabW];
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    const uint32_t hh = lane >> 5, l32 = lane & 31u, g = 2u * w + hh;
+    uint32_t* gI = tabs;
+    uint32_t* gF = tabs + GT;
+    uint32_t* rtab = tabs + 2 * GT;
+    stage_grp<G, E, false, THREADS>(gI, p.tw, M - 1);
+    stage_grp<G, E, true, THREADS>(gF, p.tw, 0);
+    stage_res<R, E, THREADS>(rtab, p.tw, M - 1);
+    __syncthreads();
+    const uint32_t es = (uint32_t)p.cs.elem_stride, k = p.cs.k, S = p.cs.S;
+    const uint32_t oo = (uint32_t)p.cs.out_offset;
+    const uint32_t tasks = p.cs.count * p.chunks;
+    const uint32_t lim = k > E * g ? k - E * g : 0u;  // registers i < lim hold data / parity
+    const uint32_t hoff = hh * (uint32_t)E * es;     // the half's first element, beyond the wave's
+    const uint32_t* tI = gI + g * (E - 1) * kTabW;
+    const uint32_t* tF = gF + g * (E - 1) * kTabW;
+    for (uint32_t task = blockIdx.x; task < tasks; task += gridDim.x) {
+        const uint32_t q = task / p.chunks, chunk = task - q * p.chunks;
+        const uint32_t off = (chunk * 4u + (l32 >> 3)) * 64u + (l32 & 7u) * 4u;
+        const uint32_t lo = off < S ? off + hoff : kOob16;
+        const uint64_t rel = cw_rel(p.cs, q);
+        const auto in = rsrc(p.cs.base + rel);
+        uint32_t l[E], h[E];
+        sfor<E>([&](auto I) {
+            constexpr int i = decltype(I)::value;
+            const uint32_t v = (uint32_t)i < lim ? lo : kOob16;
+            const uint32_t so = (2u * E * w + i) * es;
+            l[i] = ld(in, v, so);
+            h[i] = ld(in, v + 32u, so);
+        });
+        grp_xform<E, false, JIT>(l, h, tI);
+        xch_halfwave<E>(l, xch, g, l32, true);
+        xch_halfwave<E>(h, xch, g, l32, true);
+        res_xform<E, R, false, true, JIT>(l, h, rtab);
+        res_mid<E, R>(l, h, p.mid);
+        res_xform<E, R, true, true, JIT>(l, h, rtab);
+        xch_halfwave<E>(l, xch, g, l32, false);
+        xch_halfwave<E>(h, xch, g, l32, false);
+        grp_xform<E, true, JIT>(l, h, tF);
+        const auto out = rsrc(p.cs.out_base + rel);
+        sfor<E>([&](auto I) {
+            constexpr int i = decltype(I)::value;
+            const uint32_t v = (uint32_t)i < lim ? lo : kOob16;
+            const uint32_t so = oo + (2u * E * w + i) * es;
+            st(out, l[i], v, so);
+            st(out, h[i], v + 32u, so);
+        });
     }
 }
 
@@ -1277,9 +1366,9 @@ hipError_t run_encode(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st) {
     auto elem = [&](uint32_t L) { return L == kMod16 ? 0u : (uint32_t)hst.exp[L]; };
     const uint32_t sum = elem(hst.skew[M - 1 + M / 2]) ^ elem(hst.skew[M / 2 - 1]);
     Enc16 p{cs, g.skewperm, chunks, sum ? g.perm + hst.log[sum] : nullptr};
-    // m = 256: persistent, one workgroup per CU (its twiddle tables stay in LDS);
-    // m = 512: one workgroup per task (measured faster: the 16-wave form leaves no
-    // registers for a persistent loop's state)
+    // persistent forms: one workgroup per CU (two for the m = 256 half-wave form), the
+    // twiddle tables staged once per workgroup; the non-persistent diagnostic forms run
+    // one workgroup per task
     const uint32_t pgrid = tasks > g.cus ? g.cus : (uint32_t)tasks;  // persistent forms
     const uint32_t grid = M == 256 ? pgrid : (uint32_t)tasks;
     if constexpr (M == 512) {
@@ -1301,11 +1390,25 @@ hipError_t run_encode(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st) {
         }
     }
     if constexpr (M == 256) {
-        // production since round 4: 16 waves x 16 elements (4 waves per SIMD, 128
-        // registers), c4 0.417-0.427 ms per square against 0.435-0.450 for 8 waves x 32
-        // elements (diagnostic form 7; profiles/r04k_gf16_enc_ab.jsonl)
-        if (enc16_form() != 7) {
+        // production since round 4: the half-wave form (enc16h_kernel<true>: 256-byte
+        // chunks, 32 state registers, two workgroups per CU, just-in-time tables), c4
+        // 0.415-0.419 ms per square against 0.427-0.431 for 16 waves x 16 elements over
+        // 512-byte chunks (diagnostic form 6) and 0.435-0.450 for 8 waves x 32 elements
+        // (form 7, through round 3); form 14: the half-wave form with compiler-scheduled
+        // table reads (0.436-0.440).  profiles/r04k_gf16_enc_ab.jsonl, r04q_gf16_enc_ab.jsonl
+        const int form = enc16_form();
+        if (form == 6) {
             hipLaunchKernelGGL((enc16_kernel<256, 16>), dim3(grid), dim3(1024), 0, st, p);
+            return hipGetLastError();
+        }
+        if (form != 7) {
+            Enc16 ph = p;
+            ph.chunks = (cs.S + 255) / 256;
+            const uint64_t th = (uint64_t)cs.count * ph.chunks;
+            if (th >= (1ull << 31)) return hipErrorInvalidValue;
+            const uint32_t gh = th > 2ull * g.cus ? 2u * g.cus : (uint32_t)th;
+            if (form == 14) hipLaunchKernelGGL(enc16h_kernel<false>, dim3(gh), dim3(512), 0, st, ph);
+            else hipLaunchKernelGGL(enc16h_kernel<true>, dim3(gh), dim3(512), 0, st, ph);
             return hipGetLastError();
         }
     }

@@ -4,7 +4,7 @@ S = 512) with the m = 512 encoder forms of rsm_diag_set_enc16_e64 (0 production:
 scalar-table form; 3 form 2 with the half buffer; 5 form 0 with just-in-time table
 reads); every output is checked against the round-3 form's.  One JSON line
 per configuration.  GF16AB_FORMS (comma list) picks the m = 512 forms, GF16AB_REPS the
-repetitions, GF16AB_C4=0 skips the c4 part (single-form runs under rocprofv3 --pmc).
+repetitions, GF16AB_C4=0 skips the c4 part, GF16AB_C4FORMS its forms (single-form runs under rocprofv3 --pmc).
 usage: python3 scripts/diag/gf16_ab.py"""
 import ctypes
 import json
@@ -66,8 +66,9 @@ def main():
     q = ctypes.c_void_p()
     chk(D.rsm_dev_alloc(ctx, n, ctypes.byref(q)))
     outs = {}
+    c4forms = [int(f) for f in os.environ.get("GF16AB_C4FORMS", "7,0").split(",")]
     for rep in range(2):
-        for form in (7, 0):
+        for form in c4forms:
             chk(D.rsm_diag_set_enc16_e64(form))
             chk(D.rsm_dev_fill_random(ctx, q.value, n, 11))
             chk(D.rsm_extend_squares_dev(ctx, q.value, k, S, B, None))
@@ -86,7 +87,7 @@ def main():
             t = ms.value / reps / B
             print(json.dumps({"c4_form": form, "rep": rep, "c4_ms_per_square": round(t, 4),
                               "frac": round(4 * k * k * S / (t / 1e3) / 8e12, 4),
-                              "same_as_form7": bool(np.array_equal(out, outs[7]))}), flush=True)
+                              f"same_as_form{c4forms[0]}": bool(np.array_equal(out, outs[c4forms[0]]))}), flush=True)
     chk(D.rsm_diag_set_enc16_e64(0))
     chk(D.rsm_dev_free(ctx, q))
 
