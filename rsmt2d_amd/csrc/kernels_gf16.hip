@@ -277,6 +277,30 @@ __device__ __forceinline__ void tab_load_jit(const uint32_t* lds, uint32_t (&c)[
     c[12] = f.x; c[13] = f.y; c[14] = f.z; c[15] = f.w;
     c[16] = g.x; c[17] = g.y; c[18] = g.z; c[19] = g.w;
 }
+// The same at a compile-time byte offset from `lds` (the instruction's offset field):
+// a per-lane base (the half-wave forms) then stays ONE address register instead of
+// one per table.
+template <int OFF>
+__device__ __forceinline__ void tab_load_jit_at(const uint32_t* lds, uint32_t (&c)[kTabW]) {
+    static_assert(OFF >= 0 && OFF + 64 < 65536, "ds_read offset field");
+    v4u16 a, b, e, f, g;
+    const uint32_t base = (uint32_t)(uintptr_t)lds;
+    asm volatile(
+        "ds_read_b128 %0, %5 offset:%6\n\t"
+        "ds_read_b128 %1, %5 offset:%7\n\t"
+        "ds_read_b128 %2, %5 offset:%8\n\t"
+        "ds_read_b128 %3, %5 offset:%9\n\t"
+        "ds_read_b128 %4, %5 offset:%10\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(a), "=&v"(b), "=&v"(e), "=&v"(f), "=&v"(g)
+        : "v"(base), "i"(OFF), "i"(OFF + 16), "i"(OFF + 32), "i"(OFF + 48), "i"(OFF + 64)
+        : "memory");
+    c[0] = a.x; c[1] = a.y; c[2] = a.z; c[3] = a.w;
+    c[4] = b.x; c[5] = b.y; c[6] = b.z; c[7] = b.w;
+    c[8] = e.x; c[9] = e.y; c[10] = e.z; c[11] = e.w;
+    c[12] = f.x; c[13] = f.y; c[14] = f.z; c[15] = f.w;
+    c[16] = g.x; c[17] = g.y; c[18] = g.z; c[19] = g.w;
+}
 // Butterflies with the twiddle table given directly (zero table = no multiply).
 __device__ __forceinline__ void ifft2t(uint32_t& xl, uint32_t& xh, uint32_t& yl, uint32_t& yh, const PermTab16& t) {
     yl ^= xl;
@@ -314,10 +338,14 @@ __device__ __forceinline__ int slot_layer(int slot, int n) {
 template <int WAVES, int E, bool FFT, int THREADS = WAVES * 64>
 __device__ __forceinline__ void stage_grp(uint32_t* tab, const PermTab16* tw, int off) {
     constexpr int NT = WAVES * (E - 1), PER = (NT * kTabW + THREADS - 1) / THREADS;
+    // opaque thread index: a second staging later in the kernel (dec16h_kernel) must not
+    // reuse this one's index arithmetic, kept alive (spilled) in between
+    uint32_t tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
     uint32_t v[PER];
 #pragma unroll
     for (int r = 0; r < PER; ++r) {
-        const int n = (int)threadIdx.x + r * THREADS;
+        const int n = (int)tid + r * THREADS;
         const int T = n / kTabW, j = n - T * kTabW;
         const int w = T / (E - 1), slot = T - w * (E - 1);
         const int L = slot_layer(slot, E);
@@ -327,7 +355,7 @@ __device__ __forceinline__ void stage_grp(uint32_t* tab, const PermTab16* tw, in
     }
 #pragma unroll
     for (int r = 0; r < PER; ++r) {
-        const int n = (int)threadIdx.x + r * THREADS;
+        const int n = (int)tid + r * THREADS;
         if (n < NT * kTabW) tab[n] = v[r];
     }
 }
@@ -365,7 +393,7 @@ __device__ __forceinline__ void grp_xform(uint32_t (&l)[E], uint32_t (&h)[E], co
         sfor<E / 2 / d>([&](auto Bk) {
             constexpr int block = decltype(Bk)::value;
             uint32_t c[kTabW];
-            if constexpr (JIT) tab_load_jit(wtab + (E - (E >> L) + block) * kTabW, c);
+            if constexpr (JIT) tab_load_jit_at<(E - (E >> L) + block) * kTabW * 4>(wtab, c);
             else tab_load(wtab + (E - (E >> L) + block) * kTabW, c);
             sfor<d>([&](auto Q) {
                 constexpr int i = block * 2 * d + decltype(Q)::value;
@@ -1116,6 +1144,175 @@ __global__ __launch_bounds__(1024, 4) void dec16f_kernel(Dec16 p) {
 }
 
 // ---------------------------------------------------------------------------
+// Half-wave single-pass decoder for m = 512 (n = 1024 points; 257 <= k <= 512), round
+// 4: one workgroup of 16 waves per (codeword, 256-byte chunk); lane-half g = 2 w +
+// (lane >> 5) of wave w holds ONE element's 256-byte chunk per register (32 lanes x 4
+// symbols), so the n-point state is 64 registers per lane, as in dec16f_kernel<256>:
+//   group layout   (half g: elements 32 g .. 32 g + 31): scale by exp(err), IFFT
+//                  d = 1..16 (twiddle tables per half: per-lane LDS addresses, one per
+//                  16-lane LDS group);
+//   residue layout (half g: elements g + 32 j, j < 32): IFFT d = 32..512, the formal
+//                  derivative (partners e + 2^t: t >= 5 in registers, t < 5 from the
+//                  other halves through LDS), FFT d = 512..32;
+//   group layout   FFT d = 16..1; reveal the missing shares (times exp(-err)).
+// No element bit is held by the registers in both layouts (group: bits 0-4, residue:
+// bits 5-9), so the exchange buffer -- one plane, [1024][16] -- moves half the LANES per
+// pass (lanes 0-15 of both halves, then 16-31).  The group tables of one direction
+// (32 halves x 31 slots, 79 KiB) are restaged between the phases; per-element scale /
+// reveal tables are selected per half from the two halves' scalar-loaded tables.
+// ---------------------------------------------------------------------------
+template <int E>
+__device__ __forceinline__ void xch_lanesplit(uint32_t (&v)[E], uint32_t (*xch)[16], uint32_t g, uint32_t l32,
+                                              bool to_res) {
+    const uint32_t ls = l32 & 15u, sub = l32 >> 4;
+    sfor<2>([&](auto Pc) {
+        constexpr uint32_t pp = decltype(Pc)::value;
+        if (sub == pp)
+            sfor<E>([&](auto I) {
+                constexpr int i = decltype(I)::value;
+                xch[to_res ? E * g + i : g + E * i][ls] = v[i];
+            });
+        __syncthreads();
+        if (sub == pp)
+            sfor<E>([&](auto I) {
+                constexpr int i = decltype(I)::value;
+                v[i] = xch[to_res ? g + E * i : E * g + i][ls];
+            });
+        __syncthreads();
+    });
+}
+// Formal derivative of one plane in the half-wave residue layout (element g + E j in
+// register j), lane halves as xch_lanesplit: out[e] = in[e] ^ XOR over the 0-bits t of
+// e of in[e + 2^t], every term pre-derivative (registers updated in ascending j).
+template <int E, int R>
+__device__ __forceinline__ void deriv_lanesplit(uint32_t (&v)[R], uint32_t (*xch)[16], uint32_t g, uint32_t l32) {
+    const uint32_t ls = l32 & 15u, sub = l32 >> 4;
+    sfor<2>([&](auto Pc) {
+        constexpr uint32_t pp = decltype(Pc)::value;
+        if (sub == pp)
+            sfor<R>([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                xch[g + E * j][ls] = v[j];
+            });
+        __syncthreads();
+        if (sub == pp)
+            sfor<R>([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                uint32_t a = v[j];
+                sfor<12>([&](auto T) {  // t >= log2(E): bits of j
+                    constexpr int t = decltype(T)::value;
+                    if constexpr ((1 << t) < R && ((j >> t) & 1) == 0) a ^= v[j + (1 << t)];
+                });
+                sfor<ilog2c(E)>([&](auto B) {  // t < log2(E): bits of g, partner g ^ bit when that bit is 0
+                    constexpr uint32_t bit = 1u << decltype(B)::value;
+                    const uint32_t x = xch[(g ^ bit) + E * j][ls];
+                    a ^= (g & bit) ? 0u : x;
+                });
+                v[j] = a;
+            });
+        __syncthreads();
+    });
+}
+// compact table of exp(L0) in lanes 0-31 and exp(L1) in lanes 32-63
+__device__ __forceinline__ void tab_sel(const PermTab16& t0, const PermTab16& t1, bool hi, uint32_t (&c)[kTabW]) {
+    sfor<kTabW>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        c[j] = hi ? t1.w[tab_word(j)] : t0.w[tab_word(j)];
+    });
+}
+
+template <int M>
+__global__ __launch_bounds__(1024, 4) void dec16h_kernel(Dec16 p) {
+    constexpr int N = 2 * M, E = 32, G = N / E, R = N / E;
+    static_assert(G == 32 && R == 32, "n = 1024: 32 halves of 32 elements, residues of 32");
+    constexpr int GT = G * (E - 1) * kTabW;  // group tables of one direction (words)
+    __shared__ uint32_t xch[N][16];
+    __shared__ uint32_t gtab[GT];
+    __shared__ uint32_t rtab[2 * (R - 1) * kTabW];
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    const uint32_t hh = lane >> 5, l32 = lane & 31u, g = 2u * w + hh;
+    const bool hi = hh != 0u;
+    // decoder skews: IFFT SKEW[-1 + b + d], FFT SKEW[b + d - 1]
+    stage_grp<G, E, false, 1024>(gtab, p.tw, -1);
+    stage_res<R, E, 1024>(rtab, p.tw, -1);
+    const uint32_t task = blockIdx.x;
+    const uint32_t q = task / p.chunks, chunk = task - q * p.chunks;
+    const uint32_t k = p.ds.k, S = p.ds.S;
+    const uint32_t off = (chunk * 4u + (l32 >> 3)) * 64u + (l32 & 7u) * 4u;
+    const bool lane_ok = off < S;
+    const auto sq = rsrc(p.ds.base);
+    auto share_of = [&](uint32_t e) -> uint32_t {
+        return e < k ? k + e : (e >= (uint32_t)M && e < (uint32_t)M + k) ? e - (uint32_t)M : 0xFFFFFFFFu;
+    };
+    // the two halves' elements of register i: E (2 w) + i and E (2 w + 1) + i (wave-uniform)
+    uint32_t have0 = 0, have1 = 0;
+    sfor<E>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        const uint32_t s0 = share_of(E * 2u * w + i), s1 = share_of(E * (2u * w + 1u) + i);
+        const uint32_t p0 = s0 != 0xFFFFFFFFu ? (uint32_t)p.ds.presence[cell_of(p.ds, p.q0 + q, s0)] : 0u;
+        const uint32_t p1 = s1 != 0xFFFFFFFFu ? (uint32_t)p.ds.presence[cell_of(p.ds, p.q0 + q, s1)] : 0u;
+        have0 |= (__builtin_amdgcn_readfirstlane(p0) != 0u ? 1u : 0u) << i;
+        have1 |= (__builtin_amdgcn_readfirstlane(p1) != 0u ? 1u : 0u) << i;
+    });
+    uint32_t l[E], h[E];
+    sfor<E>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        const uint32_t s0 = share_of(E * 2u * w + i), s1 = share_of(E * (2u * w + 1u) + i);
+        const uint32_t c0 = ((have0 >> i) & 1u) ? (uint32_t)(cell_of(p.ds, p.q0 + q, s0) * S) : kOob16;
+        const uint32_t c1 = ((have1 >> i) & 1u) ? (uint32_t)(cell_of(p.ds, p.q0 + q, s1) * S) : kOob16;
+        const uint32_t c = hi ? c1 : c0;
+        const uint32_t vo = (c == kOob16 || !lane_ok) ? kOob16 : c + off;
+        l[i] = ld(sq, vo, 0u);
+        h[i] = ld(sq, vo + 32u, 0u);
+    });
+    sfor<E>([&](auto I) {  // scale by exp(err) (absent points are zero)
+        constexpr int i = decltype(I)::value;
+        if (((have0 | have1) >> i) & 1u) {
+            uint32_t c[kTabW];
+            tab_sel(p.r.perm[err_of(p, q, E * 2u * w + i, N)], p.r.perm[err_of(p, q, E * (2u * w + 1u) + i, N)], hi, c);
+            const uint32_t yl = l[i], yh = h[i];
+            l[i] = 0u;
+            h[i] = 0u;
+            muladd16v(l[i], h[i], yl, yh, c);
+        }
+    });
+    __syncthreads();  // tables staged
+    grp_xform<E, false, true>(l, h, gtab + g * (E - 1) * kTabW);
+    xch_lanesplit<E>(l, xch, g, l32, true);
+    xch_lanesplit<E>(h, xch, g, l32, true);
+    stage_grp<G, E, true, 1024>(gtab, p.tw, 0);  // every wave is past its IFFT group tables
+    res_xform<E, R, false, false, true, false>(l, h, rtab);
+    deriv_lanesplit<E, R>(l, xch, g, l32);
+    deriv_lanesplit<E, R>(h, xch, g, l32);
+    res_xform<E, R, true, false, true, false>(l, h, rtab);
+    xch_lanesplit<E>(l, xch, g, l32, false);
+    xch_lanesplit<E>(h, xch, g, l32, false);  // (its barriers also publish the FFT tables)
+    grp_xform<E, true, true>(l, h, gtab + g * (E - 1) * kTabW);
+    // the reveal recomputes its cell offsets (opaque codeword index: the compiler would
+    // otherwise keep the load phase's 64 offsets alive across the transforms)
+    uint32_t qr = q, wr = w;
+    asm volatile("" : "+s"(qr), "+s"(wr));
+    sfor<E>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        const uint32_t e0 = E * 2u * wr + i, e1 = E * (2u * wr + 1u) + i;
+        const uint32_t d0 = share_of(e0), d1 = share_of(e1);
+        const bool m0 = d0 != 0xFFFFFFFFu && !((have0 >> i) & 1u), m1 = d1 != 0xFFFFFFFFu && !((have1 >> i) & 1u);
+        if (m0 || m1) {
+            uint32_t c[kTabW];
+            tab_sel(p.r.perm[kMod16 - err_of(p, qr, e0, N)], p.r.perm[kMod16 - err_of(p, qr, e1, N)], hi, c);
+            uint32_t xl = 0u, xh = 0u;
+            muladd16v(xl, xh, l[i], h[i], c);
+            const uint32_t c0 = m0 ? (uint32_t)(cell_of(p.ds, p.q0 + qr, d0) * S) : kOob16;
+            const uint32_t c1 = m1 ? (uint32_t)(cell_of(p.ds, p.q0 + qr, d1) * S) : kOob16;
+            const uint32_t cc = hi ? c1 : c0;
+            const uint32_t vo = (cc == kOob16 || !lane_ok) ? kOob16 : cc + off;
+            st(sq, xl, vo, 0u);
+            st(sq, xh, vo + 32u, 0u);
+        }
+    });
+}
+
+// ---------------------------------------------------------------------------
 // Generic multi-pass transforms for m = ceilPow2(k) >= 1024 (k up to 32768, the
 // reference's MaxChunks: leopard.go:76-84).  The m- (encode) or n = 2m- (decode)
 // point transforms no longer fit one workgroup, so they run as radix-2^b passes
@@ -1419,8 +1616,10 @@ hipError_t run_encode(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st) {
 #ifdef RSM_DIAG
 static std::atomic<bool> g_dec16_five{false};
 static bool dec16_five_pass() { return g_dec16_five.load(); }
+static bool dec16h_enabled() { return !g_dec16_five.load(); }
 #else
 static bool dec16_five_pass() { return false; }
+static bool dec16h_enabled() { return false; }  // not yet measured: the five passes stay
 #endif
 
 template <int M>
@@ -1436,6 +1635,16 @@ hipError_t run_decode(const DecodeSet& ds, const Gf16Dev& g, const uint16_t* log
         Dec16 p{ds, Res{g.perm, g.skew}, logwalsh, g.errs, g.scratch, q0,
                 ds.count - q0 < batch ? ds.count - q0 : batch, chunks, g.skewperm};
         hipLaunchKernelGGL(errloc16_kernel<M>, dim3(p.count), dim3(M), 0, st, p);
+        if constexpr (M == 512) {
+            if (dec16h_enabled()) {  // the half-wave single pass: 256-byte chunks
+                const uint32_t ch = (ds.S + 255) / 256;
+                Dec16 ph = p;
+                ph.chunks = ch;
+                hipLaunchKernelGGL(dec16h_kernel<M>, dim3(p.count * ch), dim3(1024), 0, st, ph);
+                if (hipError_t e = hipGetLastError()) return e;
+                continue;
+            }
+        }
         if constexpr (M == 256) {
             if (!dec16_five_pass()) {  // the single-pass form (diagnostic builds can A/B the five passes)
                 hipLaunchKernelGGL(dec16f_kernel<M>, dim3(p.count * chunks), dim3(1024), 0, st, p);
