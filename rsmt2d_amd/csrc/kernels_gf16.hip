@@ -1031,6 +1031,35 @@ __global__ __launch_bounds__(256) void dec16_p5(Dec16 p) {  // group: FFT low + 
 //   group layout   FFT d = 16..1; reveal the missing shares (times exp(-err)).
 // The error locators come from errloc16_kernel (one workgroup per codeword).
 // ---------------------------------------------------------------------------
+// Stage the codeword's per-element multiply tables -- exp(err[e]) (scale) or
+// exp(-err[e]) (reveal) -- into LDS dst[e][kTabW]: every thread loads its words at
+// once, so the err -> table chain costs one round of latency for the whole codeword
+// instead of one per element (a wave-uniform scalar chain per register left the
+// single-pass decoders waiting most of the time).
+template <int N, int THREADS>
+__device__ __forceinline__ void stage_elem_tabs(uint32_t* dst, const Dec16& p, uint32_t q, bool reveal) {
+    constexpr int W = N * kTabW, PER = (W + THREADS - 1) / THREADS;
+    uint32_t tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    uint32_t v[PER];
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+        const uint32_t n = tid + (uint32_t)r * THREADS;
+        const uint32_t e = n / kTabW, j = n - e * kTabW;
+        uint32_t x = 0u;
+        if (n < (uint32_t)W) {
+            const uint32_t L = p.errs[(uint64_t)q * N + e];
+            x = p.r.perm[reveal ? kMod16 - L : L].w[tab_word((int)j)];
+        }
+        v[r] = x;
+    }
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+        const uint32_t n = tid + (uint32_t)r * THREADS;
+        if (n < (uint32_t)W) dst[n] = v[r];
+    }
+}
+
 // The formal derivative of one plane in the residue layout (see dec16f_kernel), in
 // two passes over the element halves (the L partners e + 2^t, t < 5, share e's half):
 // each pass publishes that half's pre-derivative values to LDS, then every wave
@@ -1115,11 +1144,21 @@ __global__ __launch_bounds__(1024, 4) void dec16f_kernel(Dec16 p) {
         l[i] = ld(sq, ln.lo, so);
         h[i] = ld(sq, ln.lo + 32, so);
     });
+    uint32_t* etab = &xch[0][0];  // per-element tables while the exchange buffer is idle
+    stage_elem_tabs<N, 1024>(etab, p, q, false);
+    __syncthreads();  // twiddle and scale tables staged
     sfor<E>([&](auto I) {
         constexpr int i = decltype(I)::value;
-        if ((have >> i) & 1u) mul16(l[i], h[i], p.r.perm[err_of(p, q, E * w + i, N)]);
+        if ((have >> i) & 1u) {
+            uint32_t c[kTabW];
+            tab_load_jit_at<i * kTabW * 4>(etab + E * w * kTabW, c);
+            const uint32_t yl = l[i], yh = h[i];
+            l[i] = 0u;
+            h[i] = 0u;
+            muladd16v(l[i], h[i], yl, yh, c);
+        }
     });
-    __syncthreads();  // tables staged
+    __syncthreads();  // the exchange buffer is free again
     grp_xform<E, false, true>(l, h, gI + w * (E - 1) * kTabW);
     xch_plane_half<E, R, true>(l, xch, w, lane);
     xch_plane_half<E, R, true>(h, xch, w, lane);
@@ -1129,13 +1168,22 @@ __global__ __launch_bounds__(1024, 4) void dec16f_kernel(Dec16 p) {
     res_xform<E, R, true, false, true, true>(l, h, rtab);
     xch_plane_half<E, R, false>(l, xch, w, lane);
     xch_plane_half<E, R, false>(h, xch, w, lane);
+    uint32_t qr = q;
+    asm volatile("" : "+s"(qr));
+    stage_elem_tabs<N, 1024>(etab, p, qr, true);  // (the exchange's last barrier freed xch)
     grp_xform<E, true, true>(l, h, gF + w * (E - 1) * kTabW);
+    __syncthreads();  // reveal tables staged
     sfor<E>([&](auto I) {
         constexpr int i = decltype(I)::value;
         const uint32_t e = E * w + i;
         const uint32_t dst = share_of(e);
         if (dst != 0xFFFFFFFFu && !((have >> i) & 1u)) {
-            mul16(l[i], h[i], p.r.perm[kMod16 - err_of(p, q, e, N)]);
+            uint32_t c[kTabW];
+            tab_load_jit_at<i * kTabW * 4>(etab + E * w * kTabW, c);
+            const uint32_t yl = l[i], yh = h[i];
+            l[i] = 0u;
+            h[i] = 0u;
+            muladd16v(l[i], h[i], yl, yh, c);
             const uint32_t so = (uint32_t)(cell_of(p.ds, p.q0 + q, dst) * S);
             st(sq, l[i], ln.lo, so);
             st(sq, h[i], ln.lo + 32, so);
@@ -1157,9 +1205,10 @@ __global__ __launch_bounds__(1024, 4) void dec16f_kernel(Dec16 p) {
 //   group layout   FFT d = 16..1; reveal the missing shares (times exp(-err)).
 // No element bit is held by the registers in both layouts (group: bits 0-4, residue:
 // bits 5-9), so the exchange buffer -- one plane, [1024][16] -- moves half the LANES per
-// pass (lanes 0-15 of both halves, then 16-31).  The group tables of one direction
-// (32 halves x 31 slots, 79 KiB) are restaged between the phases; per-element scale /
-// reveal tables are selected per half from the two halves' scalar-loaded tables.
+// pass (lanes 0-15 of both halves, then 16-31).  One LDS pool holds in turn the
+// per-element scale tables (stage_elem_tabs), the twiddle tables (the group tables of
+// one direction, 32 halves x 31 slots = 79 KiB, restaged between the phases) and the
+// per-element reveal tables.
 // ---------------------------------------------------------------------------
 template <int E>
 __device__ __forceinline__ void xch_lanesplit(uint32_t (&v)[E], uint32_t (*xch)[16], uint32_t g, uint32_t l32,
@@ -1213,28 +1262,22 @@ __device__ __forceinline__ void deriv_lanesplit(uint32_t (&v)[R], uint32_t (*xch
         __syncthreads();
     });
 }
-// compact table of exp(L0) in lanes 0-31 and exp(L1) in lanes 32-63
-__device__ __forceinline__ void tab_sel(const PermTab16& t0, const PermTab16& t1, bool hi, uint32_t (&c)[kTabW]) {
-    sfor<kTabW>([&](auto J) {
-        constexpr int j = decltype(J)::value;
-        c[j] = hi ? t1.w[tab_word(j)] : t0.w[tab_word(j)];
-    });
-}
-
 template <int M>
 __global__ __launch_bounds__(1024, 4) void dec16h_kernel(Dec16 p) {
     constexpr int N = 2 * M, E = 32, G = N / E, R = N / E;
     static_assert(G == 32 && R == 32, "n = 1024: 32 halves of 32 elements, residues of 32");
     constexpr int GT = G * (E - 1) * kTabW;  // group tables of one direction (words)
+    constexpr int RT = 2 * (R - 1) * kTabW, ET = N * kTabW;
     __shared__ uint32_t xch[N][16];
-    __shared__ uint32_t gtab[GT];
-    __shared__ uint32_t rtab[2 * (R - 1) * kTabW];
+    // the pool holds the per-element scale tables, then the twiddle tables, then the
+    // per-element reveal tables
+    __shared__ uint32_t pool[GT + RT > ET ? GT + RT : ET];
+    uint32_t* gtab = pool;
+    uint32_t* rtab = pool + GT;
+    uint32_t* etab = pool;
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
     const uint32_t hh = lane >> 5, l32 = lane & 31u, g = 2u * w + hh;
     const bool hi = hh != 0u;
-    // decoder skews: IFFT SKEW[-1 + b + d], FFT SKEW[b + d - 1]
-    stage_grp<G, E, false, 1024>(gtab, p.tw, -1);
-    stage_res<R, E, 1024>(rtab, p.tw, -1);
     const uint32_t task = blockIdx.x;
     const uint32_t q = task / p.chunks, chunk = task - q * p.chunks;
     const uint32_t k = p.ds.k, S = p.ds.S;
@@ -1265,18 +1308,24 @@ __global__ __launch_bounds__(1024, 4) void dec16h_kernel(Dec16 p) {
         l[i] = ld(sq, vo, 0u);
         h[i] = ld(sq, vo + 32u, 0u);
     });
+    stage_elem_tabs<N, 1024>(etab, p, q, false);
+    __syncthreads();
     sfor<E>([&](auto I) {  // scale by exp(err) (absent points are zero)
         constexpr int i = decltype(I)::value;
         if (((have0 | have1) >> i) & 1u) {
             uint32_t c[kTabW];
-            tab_sel(p.r.perm[err_of(p, q, E * 2u * w + i, N)], p.r.perm[err_of(p, q, E * (2u * w + 1u) + i, N)], hi, c);
+            tab_load_jit_at<i * kTabW * 4>(etab + E * g * kTabW, c);
             const uint32_t yl = l[i], yh = h[i];
             l[i] = 0u;
             h[i] = 0u;
             muladd16v(l[i], h[i], yl, yh, c);
         }
     });
-    __syncthreads();  // tables staged
+    __syncthreads();  // every wave is past the scale tables
+    // decoder skews: IFFT SKEW[-1 + b + d], FFT SKEW[b + d - 1]
+    stage_grp<G, E, false, 1024>(gtab, p.tw, -1);
+    stage_res<R, E, 1024>(rtab, p.tw, -1);
+    __syncthreads();  // twiddle tables staged
     grp_xform<E, false, true>(l, h, gtab + g * (E - 1) * kTabW);
     xch_lanesplit<E>(l, xch, g, l32, true);
     xch_lanesplit<E>(h, xch, g, l32, true);
@@ -1288,10 +1337,13 @@ __global__ __launch_bounds__(1024, 4) void dec16h_kernel(Dec16 p) {
     xch_lanesplit<E>(l, xch, g, l32, false);
     xch_lanesplit<E>(h, xch, g, l32, false);  // (its barriers also publish the FFT tables)
     grp_xform<E, true, true>(l, h, gtab + g * (E - 1) * kTabW);
+    __syncthreads();  // every wave is past the twiddle tables
     // the reveal recomputes its cell offsets (opaque codeword index: the compiler would
     // otherwise keep the load phase's 64 offsets alive across the transforms)
     uint32_t qr = q, wr = w;
     asm volatile("" : "+s"(qr), "+s"(wr));
+    stage_elem_tabs<N, 1024>(etab, p, qr, true);
+    __syncthreads();  // reveal tables staged
     sfor<E>([&](auto I) {
         constexpr int i = decltype(I)::value;
         const uint32_t e0 = E * 2u * wr + i, e1 = E * (2u * wr + 1u) + i;
@@ -1299,7 +1351,7 @@ __global__ __launch_bounds__(1024, 4) void dec16h_kernel(Dec16 p) {
         const bool m0 = d0 != 0xFFFFFFFFu && !((have0 >> i) & 1u), m1 = d1 != 0xFFFFFFFFu && !((have1 >> i) & 1u);
         if (m0 || m1) {
             uint32_t c[kTabW];
-            tab_sel(p.r.perm[kMod16 - err_of(p, qr, e0, N)], p.r.perm[kMod16 - err_of(p, qr, e1, N)], hi, c);
+            tab_load_jit_at<i * kTabW * 4>(etab + E * g * kTabW, c);
             uint32_t xl = 0u, xh = 0u;
             muladd16v(xl, xh, l[i], h[i], c);
             const uint32_t c0 = m0 ? (uint32_t)(cell_of(p.ds, p.q0 + qr, d0) * S) : kOob16;
