@@ -41,7 +41,8 @@ int rsm_diag_set_split_fused(int on);
  * table reads.  m = 256: 7 = 8 waves x 32 elements (the form through round 3), any other
  * value the production 16 waves x 16 elements. */
 int rsm_diag_set_enc16_e64(int mode);
-/* GF(2^16) m = 256 decoder: 1 = the five global passes (A/B), 0 = the single-pass kernel (production). */
+/* GF(2^16) m = 256 / 512 decoders: 1 = the five global passes (A/B), 0 = the single-pass kernels
+ * (production: dec16f_kernel for m = 256, the half-wave dec16h_kernel for m = 512). */
 int rsm_diag_set_dec16_five_pass(int on);
 /* GF(2^8) split decoder A/B: the upper half of the grid delays its point loads by
  * `ticks` of the 100 MHz s_memrealtime clock (0 = off, production). */

@@ -1201,7 +1201,7 @@ __global__ __launch_bounds__(1024, 4) void dec16f_kernel(Dec16 p) {
 //                  16-lane LDS group);
 //   residue layout (half g: elements g + 32 j, j < 32): IFFT d = 32..512, the formal
 //                  derivative (partners e + 2^t: t >= 5 in registers, t < 5 from the
-//                  other halves through LDS), FFT d = 512..32;
+//                  other halves through LDS, deriv_halfwave), FFT d = 512..32;
 //   group layout   FFT d = 16..1; reveal the missing shares (times exp(-err)).
 // No element bit is held by the registers in both layouts (group: bits 0-4, residue:
 // bits 5-9), so the exchange buffer -- one plane, [1024][16] -- moves half the LANES per
@@ -1231,37 +1231,44 @@ __device__ __forceinline__ void xch_lanesplit(uint32_t (&v)[E], uint32_t (*xch)[
     });
 }
 // Formal derivative of one plane in the half-wave residue layout (element g + E j in
-// register j), lane halves as xch_lanesplit: out[e] = in[e] ^ XOR over the 0-bits t of
-// e of in[e + 2^t], every term pre-derivative (registers updated in ascending j).
+// register j of half g = 2 w + hh): out[e] = in[e] ^ XOR over the 0-bits t of e of
+// in[e + 2^t], every term pre-derivative.  Two passes over the register halves (element
+// bit 9): the partners across g (t < 5) share j, so a pass publishes only its R/2
+// registers of every half to LDS x2[N/2][32]; registers are updated in ascending j, so
+// the in-register partners (t >= 5, j + 2^t) are still pre-derivative.  Bits 1-4 of g
+// are bits of w (wave-uniform branches), bit 0 is the lane half.
 template <int E, int R>
-__device__ __forceinline__ void deriv_lanesplit(uint32_t (&v)[R], uint32_t (*xch)[16], uint32_t g, uint32_t l32) {
-    const uint32_t ls = l32 & 15u, sub = l32 >> 4;
-    sfor<2>([&](auto Pc) {
-        constexpr uint32_t pp = decltype(Pc)::value;
-        if (sub == pp)
-            sfor<R>([&](auto J) {
-                constexpr int j = decltype(J)::value;
-                xch[g + E * j][ls] = v[j];
-            });
+__device__ __forceinline__ void deriv_halfwave(uint32_t (&v)[R], uint32_t (*x2)[32], uint32_t w, uint32_t g, bool hi,
+                                               uint32_t l32) {
+    constexpr int HJ = R / 2;
+    sfor<2>([&](auto Hc) {
+        constexpr int hf = decltype(Hc)::value;
+        sfor<HJ>([&](auto J) {
+            constexpr int j = hf * HJ + decltype(J)::value;
+            x2[g + E * (j - hf * HJ)][l32] = v[j];
+        });
         __syncthreads();
-        if (sub == pp)
-            sfor<R>([&](auto J) {
-                constexpr int j = decltype(J)::value;
-                uint32_t a = v[j];
-                sfor<12>([&](auto T) {  // t >= log2(E): bits of j
-                    constexpr int t = decltype(T)::value;
-                    if constexpr ((1 << t) < R && ((j >> t) & 1) == 0) a ^= v[j + (1 << t)];
-                });
-                sfor<ilog2c(E)>([&](auto B) {  // t < log2(E): bits of g, partner g ^ bit when that bit is 0
-                    constexpr uint32_t bit = 1u << decltype(B)::value;
-                    const uint32_t x = xch[(g ^ bit) + E * j][ls];
-                    a ^= (g & bit) ? 0u : x;
-                });
-                v[j] = a;
+        sfor<HJ>([&](auto J) {
+            constexpr int j = hf * HJ + decltype(J)::value;
+            uint32_t a = v[j];
+            sfor<12>([&](auto T) {  // t >= log2(E): bits of j
+                constexpr int t = decltype(T)::value;
+                if constexpr ((1 << t) < R && ((j >> t) & 1) == 0) a ^= v[j + (1 << t)];
             });
+            {  // t = 0: the other lane half (g ^ 1), when this half's bit is 0
+                const uint32_t x = x2[(g ^ 1u) + E * (j - hf * HJ)][l32];
+                a ^= hi ? 0u : x;
+            }
+            sfor<ilog2c(E) - 1>([&](auto B) {  // t = 1..4: bit t - 1 of w
+                constexpr uint32_t bit = 2u << decltype(B)::value;
+                if ((w & (bit >> 1)) == 0u) a ^= x2[(g + bit) + E * (j - hf * HJ)][l32];
+            });
+            v[j] = a;
+        });
         __syncthreads();
     });
 }
+
 template <int M>
 __global__ __launch_bounds__(1024, 4) void dec16h_kernel(Dec16 p) {
     constexpr int N = 2 * M, E = 32, G = N / E, R = N / E;
@@ -1331,8 +1338,9 @@ __global__ __launch_bounds__(1024, 4) void dec16h_kernel(Dec16 p) {
     xch_lanesplit<E>(h, xch, g, l32, true);
     stage_grp<G, E, true, 1024>(gtab, p.tw, 0);  // every wave is past its IFFT group tables
     res_xform<E, R, false, false, true, false>(l, h, rtab);
-    deriv_lanesplit<E, R>(l, xch, g, l32);
-    deriv_lanesplit<E, R>(h, xch, g, l32);
+    uint32_t (*x2)[32] = reinterpret_cast<uint32_t (*)[32]>(&xch[0][0]);  // [N/2][32], the same 64 KiB
+    deriv_halfwave<E, R>(l, x2, w, g, hi, l32);
+    deriv_halfwave<E, R>(h, x2, w, g, hi, l32);
     res_xform<E, R, true, false, true, false>(l, h, rtab);
     xch_lanesplit<E>(l, xch, g, l32, false);
     xch_lanesplit<E>(h, xch, g, l32, false);  // (its barriers also publish the FFT tables)
@@ -1668,11 +1676,13 @@ hipError_t run_encode(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st) {
 #ifdef RSM_DIAG
 static std::atomic<bool> g_dec16_five{false};
 static bool dec16_five_pass() { return g_dec16_five.load(); }
-static bool dec16h_enabled() { return !g_dec16_five.load(); }
 #else
 static bool dec16_five_pass() { return false; }
-static bool dec16h_enabled() { return false; }  // not yet measured: the five passes stay
 #endif
+// m = 512: the half-wave single pass (dec16h_kernel) since round 4 -- decode sweep
+// k = 512 1.43-1.45 ms against 1.84-1.85 for the five passes (diagnostic A/B:
+// rsm_diag_set_dec16_five_pass; profiles/r04w_gf16_dec_ab.jsonl)
+static bool dec16h_enabled() { return !dec16_five_pass(); }
 
 template <int M>
 hipError_t run_decode(const DecodeSet& ds, const Gf16Dev& g, const uint16_t* logwalsh, hipStream_t st) {

@@ -39,12 +39,14 @@ def test_gf16_decode(lib, rng, k):
         assert R.NewLeoRSCodec().Decode(list(sh)) == full, (k, n_missing)
 
 
-def test_gf16_decode_byzantine_formula(lib, rng):
-    k, S = 200, 64
+@pytest.mark.parametrize("k,S", [(200, 64), (400, 320)])
+def test_gf16_decode_byzantine_formula(lib, rng, k, S):
+    """m = 256 (dec16f_kernel) and m = 512 (the half-wave dec16h_kernel, S = 320: a
+    partial 256-byte chunk): a corrupted present share decodes to the oracle's bytes."""
     data = rand_shares(rng, k, S)
     sh = data + oracle.encode(data)
     sh[5] = bytes([66]) * S
-    for i in (0, 250, 399):
+    for i in (0, (5 * k) // 4, 2 * k - 1):
         sh[i] = None
     assert R.NewLeoRSCodec().Decode(list(sh)) == oracle.decode(list(sh))
 
