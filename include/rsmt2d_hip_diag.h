@@ -44,6 +44,9 @@ int rsm_diag_set_enc16_e64(int mode);
 /* GF(2^16) m = 256 / 512 decoders: 1 = the five global passes (A/B), 0 = the single-pass kernels
  * (production: dec16f_kernel for m = 256, the half-wave dec16h_kernel for m = 512). */
 int rsm_diag_set_dec16_five_pass(int on);
+/* GF(2^16) m = 512 half-wave decoder A/B bits (wrong output by design): 1 = no scale /
+ * reveal table staging, 2 = no point loads; 0 = production. */
+int rsm_diag_set_dec16_mode(uint32_t mode);
 /* GF(2^8) split decoder A/B: the upper half of the grid delays its point loads by
  * `ticks` of the 100 MHz s_memrealtime clock (0 = off, production). */
 int rsm_diag_set_dec_delay(uint32_t ticks);

@@ -332,17 +332,15 @@ __device__ __forceinline__ int slot_layer(int slot, int n) {
     return L;
 }
 
-// Stage into LDS `tab` the group-layout tables of every wave (wave w: E - 1
-// slots, elements E w ..): IFFT SKEW[off + b + d] or FFT SKEW[b + d - 1].  Fixed
-// trip count, loads first: every thread's table words are in flight at once.
+template <int WAVES, int E, int THREADS>
+constexpr int grp_tab_per() { return (WAVES * (E - 1) * kTabW + THREADS - 1) / THREADS; }
 template <int WAVES, int E, bool FFT, int THREADS = WAVES * 64>
-__device__ __forceinline__ void stage_grp(uint32_t* tab, const PermTab16* tw, int off) {
-    constexpr int NT = WAVES * (E - 1), PER = (NT * kTabW + THREADS - 1) / THREADS;
+__device__ __forceinline__ void load_grp(const PermTab16* tw, int off, uint32_t (&v)[grp_tab_per<WAVES, E, THREADS>()]) {
+    constexpr int NT = WAVES * (E - 1), PER = grp_tab_per<WAVES, E, THREADS>();
     // opaque thread index: a second staging later in the kernel (dec16h_kernel) must not
     // reuse this one's index arithmetic, kept alive (spilled) in between
     uint32_t tid = threadIdx.x;
     asm volatile("" : "+v"(tid));
-    uint32_t v[PER];
 #pragma unroll
     for (int r = 0; r < PER; ++r) {
         const int n = (int)tid + r * THREADS;
@@ -353,11 +351,26 @@ __device__ __forceinline__ void stage_grp(uint32_t* tab, const PermTab16* tw, in
         const int idx = FFT ? E * w + bl + d - 1 : off + E * w + bl + d;
         v[r] = n < NT * kTabW ? tw[idx].w[tab_word(j)] : 0u;
     }
+}
+template <int WAVES, int E, int THREADS = WAVES * 64>
+__device__ __forceinline__ void store_grp(uint32_t* tab, const uint32_t (&v)[grp_tab_per<WAVES, E, THREADS>()]) {
+    constexpr int NT = WAVES * (E - 1), PER = grp_tab_per<WAVES, E, THREADS>();
+    uint32_t tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
 #pragma unroll
     for (int r = 0; r < PER; ++r) {
         const int n = (int)tid + r * THREADS;
         if (n < NT * kTabW) tab[n] = v[r];
     }
+}
+// Stage into LDS `tab` the group-layout tables of every wave (wave w: E - 1
+// slots, elements E w ..): IFFT SKEW[off + b + d] or FFT SKEW[b + d - 1].  Fixed
+// trip count, loads first: every thread's table words are in flight at once.
+template <int WAVES, int E, bool FFT, int THREADS = WAVES * 64>
+__device__ __forceinline__ void stage_grp(uint32_t* tab, const PermTab16* tw, int off) {
+    uint32_t v[grp_tab_per<WAVES, E, THREADS>()];
+    load_grp<WAVES, E, FFT, THREADS>(tw, off, v);
+    store_grp<WAVES, E, THREADS>(tab, v);
 }
 // Residue-layout tables (shared by all waves): slots 0..R-2 IFFT, R-1..2R-3 FFT.
 template <int R, int E, int THREADS>
@@ -788,6 +801,7 @@ struct Dec16 {
     uint8_t* scratch;   // [count][2][n][S] (the five-pass form)
     uint32_t q0, count, chunks;
     const PermTab16* tw;  // skewperm (the single-pass form)
+    uint32_t diag;        // diagnostic builds: dec16h_kernel A/B bits (rsm_diag_set_dec16_mode), else 0
 };
 
 __device__ __forceinline__ uint32_t addm(uint32_t a, uint32_t b) {
@@ -1037,11 +1051,13 @@ __global__ __launch_bounds__(256) void dec16_p5(Dec16 p) {  // group: FFT low + 
 // instead of one per element (a wave-uniform scalar chain per register left the
 // single-pass decoders waiting most of the time).
 template <int N, int THREADS>
-__device__ __forceinline__ void stage_elem_tabs(uint32_t* dst, const Dec16& p, uint32_t q, bool reveal) {
-    constexpr int W = N * kTabW, PER = (W + THREADS - 1) / THREADS;
+constexpr int elem_tab_per() { return (N * kTabW + THREADS - 1) / THREADS; }
+template <int N, int THREADS>
+__device__ __forceinline__ void load_elem_tabs(const Dec16& p, uint32_t q, bool reveal,
+                                               uint32_t (&v)[elem_tab_per<N, THREADS>()]) {
+    constexpr int W = N * kTabW, PER = elem_tab_per<N, THREADS>();
     uint32_t tid = threadIdx.x;
     asm volatile("" : "+v"(tid));
-    uint32_t v[PER];
 #pragma unroll
     for (int r = 0; r < PER; ++r) {
         const uint32_t n = tid + (uint32_t)r * THREADS;
@@ -1053,11 +1069,28 @@ __device__ __forceinline__ void stage_elem_tabs(uint32_t* dst, const Dec16& p, u
         }
         v[r] = x;
     }
+}
+template <int N, int THREADS>
+__device__ __forceinline__ void store_elem_tabs(uint32_t* dst, const uint32_t (&v)[elem_tab_per<N, THREADS>()]) {
+    constexpr int W = N * kTabW, PER = elem_tab_per<N, THREADS>();
+    uint32_t tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
 #pragma unroll
     for (int r = 0; r < PER; ++r) {
         const uint32_t n = tid + (uint32_t)r * THREADS;
         if (n < (uint32_t)W) dst[n] = v[r];
     }
+}
+// Stage the codeword's per-element multiply tables -- exp(err[e]) (scale) or
+// exp(-err[e]) (reveal) -- into LDS dst[e][kTabW]: every thread loads its words at
+// once, so the err -> table chain costs one round of latency for the whole codeword
+// instead of one per element (a wave-uniform scalar chain per register left the
+// single-pass decoders waiting most of the time).
+template <int N, int THREADS>
+__device__ __forceinline__ void stage_elem_tabs(uint32_t* dst, const Dec16& p, uint32_t q, bool reveal) {
+    uint32_t v[elem_tab_per<N, THREADS>()];
+    load_elem_tabs<N, THREADS>(p, q, reveal, v);
+    store_elem_tabs<N, THREADS>(dst, v);
 }
 
 // The formal derivative of one plane in the residue layout (see dec16f_kernel), in
@@ -1127,25 +1160,25 @@ __global__ __launch_bounds__(1024, 4) void dec16f_kernel(Dec16 p) {
     auto share_of = [&](uint32_t e) -> uint32_t {
         return e < k ? k + e : (e >= (uint32_t)M && e < (uint32_t)M + k) ? e - (uint32_t)M : 0xFFFFFFFFu;
     };
-    // presence of this wave's 32 slots first (uniform byte loads), then the present
-    // shares' loads all in flight together (an absent slot reads zeros)
-    uint32_t have = 0;
-    sfor<E>([&](auto I) {
-        constexpr int i = decltype(I)::value;
-        const uint32_t src = share_of(E * w + i);
-        const uint32_t pr = src != 0xFFFFFFFFu ? (uint32_t)p.ds.presence[cell_of(p.ds, p.q0 + q, src)] : 0u;
-        have |= (__builtin_amdgcn_readfirstlane(pr) != 0u ? 1u : 0u) << i;
-    });
+    uint32_t* etab = &xch[0][0];  // per-element tables while the exchange buffer is idle
+    uint32_t etv[elem_tab_per<N, 1024>()];  // the scale tables' err -> table chain first
+    load_elem_tabs<N, 1024>(p, q, false, etv);
+    // presence: lane j < 32 of wave w asks for slot 32 w + j (one load per lane, a ballot)
+    const uint32_t vec = __builtin_amdgcn_readfirstlane(p.ds.indices[p.q0 + q]);
+    const uint32_t Wd = 2u * k;
+    auto cell = [&](uint32_t s) -> uint32_t { return p.ds.axis == 0 ? vec * Wd + s : s * Wd + vec; };
+    const uint32_t my_s = lane < (uint32_t)E ? share_of(E * w + lane) : 0xFFFFFFFFu;
+    const uint32_t my_p = my_s != 0xFFFFFFFFu ? (uint32_t)p.ds.presence[cell(my_s)] : 0u;
+    const uint32_t have = __builtin_amdgcn_readfirstlane((uint32_t)__ballot(my_p != 0u));
     uint32_t l[E], h[E];
     sfor<E>([&](auto I) {
         constexpr int i = decltype(I)::value;
         const uint32_t src = share_of(E * w + i);
-        const uint32_t so = ((have >> i) & 1u) ? (uint32_t)(cell_of(p.ds, p.q0 + q, src) * S) : kOob16;
+        const uint32_t so = ((have >> i) & 1u) ? cell(src) * S : kOob16;
         l[i] = ld(sq, ln.lo, so);
         h[i] = ld(sq, ln.lo + 32, so);
     });
-    uint32_t* etab = &xch[0][0];  // per-element tables while the exchange buffer is idle
-    stage_elem_tabs<N, 1024>(etab, p, q, false);
+    store_elem_tabs<N, 1024>(etab, etv);
     __syncthreads();  // twiddle and scale tables staged
     sfor<E>([&](auto I) {
         constexpr int i = decltype(I)::value;
@@ -1184,7 +1217,7 @@ __global__ __launch_bounds__(1024, 4) void dec16f_kernel(Dec16 p) {
             l[i] = 0u;
             h[i] = 0u;
             muladd16v(l[i], h[i], yl, yh, c);
-            const uint32_t so = (uint32_t)(cell_of(p.ds, p.q0 + q, dst) * S);
+            const uint32_t so = cell(dst) * S;
             st(sq, l[i], ln.lo, so);
             st(sq, h[i], ln.lo + 32, so);
         }
@@ -1210,6 +1243,21 @@ __global__ __launch_bounds__(1024, 4) void dec16f_kernel(Dec16 p) {
 // one direction, 32 halves x 31 slots = 79 KiB, restaged between the phases) and the
 // per-element reveal tables.
 // ---------------------------------------------------------------------------
+// diagnostic phase stamp of the single-pass decoders (RSM_DIAG builds with a decode
+// trace set): thread 0, 100 MHz clock, kDec16TraceWords per workgroup
+__device__ __forceinline__ void d16_stamp(const Dec16& p, int i) {
+#ifdef RSM_DIAG
+    if (p.ds.trace && threadIdx.x == 0) {
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(p.ds.trace, (short)0, 0x7FFFFFFF, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)__builtin_amdgcn_s_memrealtime(), r,
+                                              (blockIdx.x * kDec16TraceWords + i) * 4u, 0, 0);
+    }
+#else
+    (void)p;
+    (void)i;
+#endif
+}
+
 template <int E>
 __device__ __forceinline__ void xch_lanesplit(uint32_t (&v)[E], uint32_t (*xch)[16], uint32_t g, uint32_t l32,
                                               bool to_res) {
@@ -1286,6 +1334,7 @@ __global__ __launch_bounds__(1024, 4) void dec16h_kernel(Dec16 p) {
     const uint32_t hh = lane >> 5, l32 = lane & 31u, g = 2u * w + hh;
     const bool hi = hh != 0u;
     const uint32_t task = blockIdx.x;
+    d16_stamp(p, 0);
     const uint32_t q = task / p.chunks, chunk = task - q * p.chunks;
     const uint32_t k = p.ds.k, S = p.ds.S;
     const uint32_t off = (chunk * 4u + (l32 >> 3)) * 64u + (l32 & 7u) * 4u;
@@ -1294,29 +1343,42 @@ __global__ __launch_bounds__(1024, 4) void dec16h_kernel(Dec16 p) {
     auto share_of = [&](uint32_t e) -> uint32_t {
         return e < k ? k + e : (e >= (uint32_t)M && e < (uint32_t)M + k) ? e - (uint32_t)M : 0xFFFFFFFFu;
     };
-    // the two halves' elements of register i: E (2 w) + i and E (2 w + 1) + i (wave-uniform)
-    uint32_t have0 = 0, have1 = 0;
-    sfor<E>([&](auto I) {
-        constexpr int i = decltype(I)::value;
-        const uint32_t s0 = share_of(E * 2u * w + i), s1 = share_of(E * (2u * w + 1u) + i);
-        const uint32_t p0 = s0 != 0xFFFFFFFFu ? (uint32_t)p.ds.presence[cell_of(p.ds, p.q0 + q, s0)] : 0u;
-        const uint32_t p1 = s1 != 0xFFFFFFFFu ? (uint32_t)p.ds.presence[cell_of(p.ds, p.q0 + q, s1)] : 0u;
-        have0 |= (__builtin_amdgcn_readfirstlane(p0) != 0u ? 1u : 0u) << i;
-        have1 |= (__builtin_amdgcn_readfirstlane(p1) != 0u ? 1u : 0u) << i;
-    });
+    // the scale tables' err -> table chain first (it depends on nothing else)
+    uint32_t etv[elem_tab_per<N, 1024>()];
+#ifdef RSM_DIAG
+    if (!(p.diag & 1u))  // A/B bit 0: no scale / reveal table staging (wrong output)
+#endif
+    load_elem_tabs<N, 1024>(p, q, false, etv);
+    // presence: lane j of wave w asks for element 64 w + j = register j & 31 of half j >> 5
+    const uint32_t vec = __builtin_amdgcn_readfirstlane(p.ds.indices[p.q0 + q]);
+    const uint32_t Wd = 2u * k;
+    auto cell = [&](uint32_t s) -> uint32_t { return p.ds.axis == 0 ? vec * Wd + s : s * Wd + vec; };
+    const uint32_t my_s = share_of(64u * w + lane);
+    const uint32_t my_p = my_s != 0xFFFFFFFFu ? (uint32_t)p.ds.presence[cell(my_s)] : 0u;
+    const uint64_t hv = __ballot(my_p != 0u);
+    const uint32_t have0 = __builtin_amdgcn_readfirstlane((uint32_t)hv);
+    const uint32_t have1 = __builtin_amdgcn_readfirstlane((uint32_t)(hv >> 32));
+    d16_stamp(p, 1);
     uint32_t l[E], h[E];
-    sfor<E>([&](auto I) {
+    sfor<E>([&](auto I) {  // the two halves' elements of register i: E (2 w) + i, E (2 w + 1) + i
         constexpr int i = decltype(I)::value;
         const uint32_t s0 = share_of(E * 2u * w + i), s1 = share_of(E * (2u * w + 1u) + i);
-        const uint32_t c0 = ((have0 >> i) & 1u) ? (uint32_t)(cell_of(p.ds, p.q0 + q, s0) * S) : kOob16;
-        const uint32_t c1 = ((have1 >> i) & 1u) ? (uint32_t)(cell_of(p.ds, p.q0 + q, s1) * S) : kOob16;
+        const uint32_t c0 = ((have0 >> i) & 1u) ? cell(s0) * S : kOob16;
+        const uint32_t c1 = ((have1 >> i) & 1u) ? cell(s1) * S : kOob16;
         const uint32_t c = hi ? c1 : c0;
-        const uint32_t vo = (c == kOob16 || !lane_ok) ? kOob16 : c + off;
+        uint32_t vo = (c == kOob16 || !lane_ok) ? kOob16 : c + off;
+#ifdef RSM_DIAG
+        if (p.diag & 2u) vo = kOob16;  // A/B bit 1: no point loads (wrong output)
+#endif
         l[i] = ld(sq, vo, 0u);
         h[i] = ld(sq, vo + 32u, 0u);
     });
-    stage_elem_tabs<N, 1024>(etab, p, q, false);
+#ifdef RSM_DIAG
+    if (!(p.diag & 1u))
+#endif
+    store_elem_tabs<N, 1024>(etab, etv);
     __syncthreads();
+    d16_stamp(p, 2);
     sfor<E>([&](auto I) {  // scale by exp(err) (absent points are zero)
         constexpr int i = decltype(I)::value;
         if (((have0 | have1) >> i) & 1u) {
@@ -1333,25 +1395,39 @@ __global__ __launch_bounds__(1024, 4) void dec16h_kernel(Dec16 p) {
     stage_grp<G, E, false, 1024>(gtab, p.tw, -1);
     stage_res<R, E, 1024>(rtab, p.tw, -1);
     __syncthreads();  // twiddle tables staged
+    d16_stamp(p, 3);
     grp_xform<E, false, true>(l, h, gtab + g * (E - 1) * kTabW);
+    d16_stamp(p, 4);
+    uint32_t gfv[grp_tab_per<G, E, 1024>()];  // the FFT group tables, loaded ahead of the exchange
+    load_grp<G, E, true, 1024>(p.tw, 0, gfv);
     xch_lanesplit<E>(l, xch, g, l32, true);
     xch_lanesplit<E>(h, xch, g, l32, true);
-    stage_grp<G, E, true, 1024>(gtab, p.tw, 0);  // every wave is past its IFFT group tables
+    store_grp<G, E, 1024>(gtab, gfv);  // every wave is past its IFFT group tables
+    d16_stamp(p, 5);
     res_xform<E, R, false, false, true, false>(l, h, rtab);
+    d16_stamp(p, 6);
     uint32_t (*x2)[32] = reinterpret_cast<uint32_t (*)[32]>(&xch[0][0]);  // [N/2][32], the same 64 KiB
     deriv_halfwave<E, R>(l, x2, w, g, hi, l32);
     deriv_halfwave<E, R>(h, x2, w, g, hi, l32);
+    d16_stamp(p, 7);
     res_xform<E, R, true, false, true, false>(l, h, rtab);
+    d16_stamp(p, 8);
     xch_lanesplit<E>(l, xch, g, l32, false);
     xch_lanesplit<E>(h, xch, g, l32, false);  // (its barriers also publish the FFT tables)
+    d16_stamp(p, 9);
     grp_xform<E, true, true>(l, h, gtab + g * (E - 1) * kTabW);
     __syncthreads();  // every wave is past the twiddle tables
+    d16_stamp(p, 10);
     // the reveal recomputes its cell offsets (opaque codeword index: the compiler would
     // otherwise keep the load phase's 64 offsets alive across the transforms)
     uint32_t qr = q, wr = w;
     asm volatile("" : "+s"(qr), "+s"(wr));
+#ifdef RSM_DIAG
+    if (!(p.diag & 1u))
+#endif
     stage_elem_tabs<N, 1024>(etab, p, qr, true);
     __syncthreads();  // reveal tables staged
+    d16_stamp(p, 11);
     sfor<E>([&](auto I) {
         constexpr int i = decltype(I)::value;
         const uint32_t e0 = E * 2u * wr + i, e1 = E * (2u * wr + 1u) + i;
@@ -1362,14 +1438,15 @@ __global__ __launch_bounds__(1024, 4) void dec16h_kernel(Dec16 p) {
             tab_load_jit_at<i * kTabW * 4>(etab + E * g * kTabW, c);
             uint32_t xl = 0u, xh = 0u;
             muladd16v(xl, xh, l[i], h[i], c);
-            const uint32_t c0 = m0 ? (uint32_t)(cell_of(p.ds, p.q0 + qr, d0) * S) : kOob16;
-            const uint32_t c1 = m1 ? (uint32_t)(cell_of(p.ds, p.q0 + qr, d1) * S) : kOob16;
+            const uint32_t c0 = m0 ? cell(d0) * S : kOob16;
+            const uint32_t c1 = m1 ? cell(d1) * S : kOob16;
             const uint32_t cc = hi ? c1 : c0;
             const uint32_t vo = (cc == kOob16 || !lane_ok) ? kOob16 : cc + off;
             st(sq, xl, vo, 0u);
             st(sq, xh, vo + 32u, 0u);
         }
     });
+    d16_stamp(p, 12);
 }
 
 // ---------------------------------------------------------------------------
@@ -1676,8 +1753,11 @@ hipError_t run_encode(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st) {
 #ifdef RSM_DIAG
 static std::atomic<bool> g_dec16_five{false};
 static bool dec16_five_pass() { return g_dec16_five.load(); }
+static std::atomic<uint32_t> g_dec16_mode{0};
+static uint32_t dec16_diag_mode() { return g_dec16_mode.load(); }
 #else
 static bool dec16_five_pass() { return false; }
+static uint32_t dec16_diag_mode() { return 0u; }
 #endif
 // m = 512: the half-wave single pass (dec16h_kernel) since round 4 -- decode sweep
 // k = 512 1.43-1.45 ms against 1.84-1.85 for the five passes (diagnostic A/B:
@@ -1696,6 +1776,8 @@ hipError_t run_decode(const DecodeSet& ds, const Gf16Dev& g, const uint16_t* log
     for (uint32_t q0 = 0; q0 < ds.count; q0 += batch) {
         Dec16 p{ds, Res{g.perm, g.skew}, logwalsh, g.errs, g.scratch, q0,
                 ds.count - q0 < batch ? ds.count - q0 : batch, chunks, g.skewperm};
+        p.ds.trace = dec_diag_trace_ptr();
+        p.diag = dec16_diag_mode();
         hipLaunchKernelGGL(errloc16_kernel<M>, dim3(p.count), dim3(M), 0, st, p);
         if constexpr (M == 512) {
             if (dec16h_enabled()) {  // the half-wave single pass: 256-byte chunks
@@ -1887,6 +1969,7 @@ static hipError_t run_decode_generic(const DecodeSet& ds, const Gf16Dev& g, hipS
 #ifdef RSM_DIAG
 void set_enc16_diag_e64(int mode) { g_enc16_e64.store(mode); }
 void set_dec16_diag_five_pass(bool on) { g_dec16_five.store(on); }
+void set_dec16_diag_mode(uint32_t m) { g_dec16_mode.store(m); }
 #endif
 
 hipError_t launch_encode_gf16(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st) {

@@ -1029,9 +1029,11 @@ static hipError_t launch_dec(const DecodeSet& ds, hipStream_t st) {
 static std::atomic<uint32_t*> g_dec_trace{nullptr};
 static std::atomic<uint32_t> g_dec_delay{0};
 void set_dec_diag_trace(uint32_t* d) { g_dec_trace.store(d); }
+uint32_t* dec_diag_trace_ptr() { return g_dec_trace.load(); }
 void set_dec_diag_delay(uint32_t ticks) { g_dec_delay.store(ticks); }
 #else
 void set_dec_diag_trace(uint32_t*) {}
+uint32_t* dec_diag_trace_ptr() { return nullptr; }
 void set_dec_diag_delay(uint32_t) {}
 #endif
 

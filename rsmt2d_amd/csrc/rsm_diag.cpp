@@ -84,6 +84,11 @@ int rsm_diag_set_dec_trace(void* d_trace) {
     return RSM_OK;
 }
 
+int rsm_diag_set_dec16_mode(uint32_t mode) {
+    set_dec16_diag_mode(mode);
+    return RSM_OK;
+}
+
 int rsm_diag_set_dec_delay(uint32_t ticks) {
     set_dec_diag_delay(ticks);
     return RSM_OK;

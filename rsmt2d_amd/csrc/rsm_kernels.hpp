@@ -67,6 +67,8 @@ struct DecodeSet {
 };
 constexpr int kDecTraceWords = 8;
 void set_dec_diag_trace(uint32_t* d);
+uint32_t* dec_diag_trace_ptr();  // (diagnostic builds; the GF(2^16) single-pass decoders stamp kDec16TraceWords)
+constexpr int kDec16TraceWords = 16;
 void set_dec_diag_delay(uint32_t ticks);
 
 hipError_t launch_encode_gf8(const CodewordSet& cs, hipStream_t st);
@@ -83,6 +85,7 @@ void set_split_diag_waves(int first, int second);  // diagnostic builds only
 void set_split_diag_fused(bool on);                  // diagnostic builds only
 void set_enc16_diag_e64(int mode);                   // diagnostic builds only
 void set_dec16_diag_five_pass(bool on);              // diagnostic builds only
+void set_dec16_diag_mode(uint32_t mode);            // diagnostic builds only: dec16h_kernel A/B bits
 bool bs128_diag_xcd_queues();                        // diagnostic builds only: XCD-affine queue mode set
 bool split_fused_enabled();                          // product: always
 // One square in ONE launch of the split encoder (rows -> Q1, Q0 columns -> Q2, then
