@@ -711,7 +711,7 @@ def bench_single_square(local, L, R, k=128, S=512, reps=200):
 
 
 def bench_c4(local, L, R, steps, B=2, k=256, S=2048):
-    """Config 4: 256x256 -> 512x512 squares of 2048 B shares (GF(2^16), enc16_kernel<256>),
+    """Config 4: 256x256 -> 512x512 squares of 2048 B shares (GF(2^16), enc16h_kernel: m = 256),
     device-resident, B squares (1 GiB of EDS) per step, steps alternating over two
     buffers so no step finds its squares in the 256 MiB Infinity Cache.  With S = 512
     the same code times BenchmarkExtensionEncoding's own k = 256 shape
@@ -752,7 +752,8 @@ def bench_c4(local, L, R, steps, B=2, k=256, S=2048):
                          "GF(2^16)"), "squares_per_step": B,
             "ms_per_square": round(dt / B * 1e3, 4), "ods_GiB_s": round(k * k * S * B / dt / 2**30, 3),
             "frac": round(algo / dt / 1e9 / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_square": 4 * k * k * S,
-            "kernel": f"enc16_kernel<{1 << (k - 1).bit_length()}> (row pass, column pass)"}
+            "kernel": ("enc16h_kernel (m = 256, half-wave form)" if (1 << (k - 1).bit_length()) == 256
+                       else f"enc16_kernel<{1 << (k - 1).bit_length()}>") + " (row pass, column pass)"}
 
 
 def bench_nmt_roots(local, L, R, k, S, squares=32, reps=5, ns=29):
