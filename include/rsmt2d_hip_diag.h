@@ -35,11 +35,14 @@ int rsm_diag_set_split_waves(int first, int second);
 /* One square in the latency form: 1 = one launch with a device-side wait (A/B only:
  * slower), 0 = two launches (production). */
 int rsm_diag_set_split_fused(int on);
-/* GF(2^16) m = 512 encoder form: 0 = production (16 waves x 32 elements, persistent, LDS
- * tables, half exchange buffer), 1 = 8 waves x 64 elements, 2 = the round-3 16-wave form
- * (scalar tables), 3 = form 2 with the half exchange buffer, 5 = form 0 with just-in-time
- * table reads.  m = 256: 7 = 8 waves x 32 elements (the form through round 3), any other
- * value the production 16 waves x 16 elements. */
+/* GF(2^16) encoder form (m = 512): 0 = production (the half-wave form, enc16h512_kernel,
+ * just-in-time tables), 1 = 8 waves x 64 elements, 2 = the round-3 16-wave form (scalar
+ * tables), 3 = form 2 with the half exchange buffer, 4 = 16 waves x 32 elements,
+ * persistent, LDS tables beside a half exchange buffer, 5 = form 4 with just-in-time
+ * table reads, 8 / 9 = forms 4 / 5 with the merged middle pair, 16 = the half-wave form
+ * with compiler-scheduled table reads.  m = 256: 6 = 16 waves x 16 elements, 7 = 8 waves
+ * x 32 elements, 14 = the half-wave form with compiler-scheduled reads, any other value
+ * the production half-wave form. */
 int rsm_diag_set_enc16_e64(int mode);
 /* GF(2^16) m = 256 / 512 decoders: 1 = the five global passes (A/B), 0 = the single-pass kernels
  * (production: dec16f_kernel for m = 256, the half-wave dec16h_kernel for m = 512). */

@@ -790,6 +790,145 @@ __global__ __launch_bounds__(512, 4) void enc16h_kernel(Enc16 p) {
     }
 }
 
+// Half-wave form of the m = 512 encoder (round 4): one task per (codeword, 256-byte
+// chunk), 16 waves, half g = 2 w + (lane >> 5) holding elements 16 g .. 16 g + 15 in
+// its registers (32 state registers, against 64 for 512-byte chunks):
+//   layers d = 1..8   in registers, per-half tables (as enc16h_kernel);
+//   layer  d = 16     joins the two halves of a wave: v_permlane32_swap of the register
+//                     pairs (i, i + 1) puts elements 32 w + i + hh and 32 w + 16 + i + hh
+//                     in one lane each, and the wave's one table serves both halves;
+//   layers d = 32..256 in the residue layout (half g: elements g + 32 j, j < 16),
+//                     through a [512][32] exchange buffer (one plane at a time).
+__device__ __forceinline__ void swap_halves(uint32_t& a, uint32_t& b) {
+    const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+    a = r[0];
+    b = r[1];
+}
+// element of register r in the swapped group arrangement (after the d = 16 swap)
+__device__ __forceinline__ uint32_t swapped_elem(uint32_t w, int r, uint32_t hh) {
+    return 32u * w + ((r & 1) ? 16u : 0u) + (uint32_t)(r & ~1) + hh;
+}
+
+template <bool JIT>
+__global__ __launch_bounds__(1024, 4) void enc16h512_kernel(Enc16 p) {
+    constexpr int M = 512, E = 16, G = 32, R = 16, THREADS = 1024;
+    constexpr int GT = G * (E - 1) * kTabW, WT = 16 * kTabW, RT = 2 * (R - 1) * kTabW;
+    __shared__ uint32_t xch[M][32];
+    __shared__ uint32_t tabs[2 * GT + 2 * WT + RT];
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    const uint32_t hh = lane >> 5, l32 = lane & 31u, g = 2u * w + hh;
+    uint32_t* gI = tabs;
+    uint32_t* gF = tabs + GT;
+    uint32_t* wI = tabs + 2 * GT;
+    uint32_t* wF = wI + WT;
+    uint32_t* rtab = wF + WT;
+    stage_grp<G, E, false, THREADS>(gI, p.tw, M - 1);
+    stage_grp<G, E, true, THREADS>(gF, p.tw, 0);
+    {  // the d = 16 layer's table of every wave: IFFT SKEW[m - 1 + 32 w + 16], FFT SKEW[32 w + 15]
+        uint32_t tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        if (tid < 2u * WT) {
+            const bool fft = tid >= (uint32_t)WT;
+            const uint32_t n = fft ? tid - WT : tid, ww = n / kTabW, j = n - ww * kTabW;
+            const uint32_t idx = fft ? 32u * ww + 15u : M - 1 + 32u * ww + 16u;
+            (fft ? wF : wI)[n] = p.tw[idx].w[tab_word((int)j)];
+        }
+    }
+    stage_res<R, 32, THREADS>(rtab, p.tw, M - 1);
+    __syncthreads();
+    const uint32_t es = (uint32_t)p.cs.elem_stride, k = p.cs.k, S = p.cs.S;
+    const uint32_t oo = (uint32_t)p.cs.out_offset;
+    const uint32_t tasks = p.cs.count * p.chunks;
+    const uint32_t lim = k > E * g ? k - E * g : 0u;  // registers i < lim hold data / parity
+    const uint32_t hoff = hh * (uint32_t)E * es;
+    const uint32_t* tI = gI + g * (E - 1) * kTabW;
+    const uint32_t* tF = gF + g * (E - 1) * kTabW;
+    for (uint32_t task = blockIdx.x; task < tasks; task += gridDim.x) {
+        const uint32_t q = task / p.chunks, chunk = task - q * p.chunks;
+        const uint32_t off = (chunk * 4u + (l32 >> 3)) * 64u + (l32 & 7u) * 4u;
+        const uint32_t lo = off < S ? off + hoff : kOob16;
+        const uint64_t rel = cw_rel(p.cs, q);
+        const auto in = rsrc(p.cs.base + rel);
+        uint32_t l[E], h[E];
+        sfor<E>([&](auto I) {
+            constexpr int i = decltype(I)::value;
+            const uint32_t v = (uint32_t)i < lim ? lo : kOob16;
+            const uint32_t so = (2u * E * w + i) * es;
+            l[i] = ld(in, v, so);
+            h[i] = ld(in, v + 32u, so);
+        });
+        grp_xform<E, false, JIT>(l, h, tI);
+        {  // d = 16
+            sfor<E / 2>([&](auto P) {
+                constexpr int i = 2 * decltype(P)::value;
+                swap_halves(l[i], l[i + 1]);
+                swap_halves(h[i], h[i + 1]);
+            });
+            uint32_t c[kTabW];
+            if constexpr (JIT) tab_load_jit(wI + w * kTabW, c);
+            else tab_load(wI + w * kTabW, c);
+            sfor<E / 2>([&](auto P) {
+                constexpr int i = 2 * decltype(P)::value;
+                ifft2v(l[i], h[i], l[i + 1], h[i + 1], c);
+            });
+        }
+        auto to_res = [&](uint32_t (&v)[E]) {
+            sfor<E>([&](auto I) {
+                constexpr int r = decltype(I)::value;
+                xch[swapped_elem(w, r, hh)][l32] = v[r];
+            });
+            __syncthreads();
+            sfor<R>([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                v[j] = xch[g + 32u * j][l32];
+            });
+            __syncthreads();
+        };
+        auto to_grp = [&](uint32_t (&v)[E]) {
+            sfor<R>([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                xch[g + 32u * j][l32] = v[j];
+            });
+            __syncthreads();
+            sfor<E>([&](auto I) {
+                constexpr int r = decltype(I)::value;
+                v[r] = xch[swapped_elem(w, r, hh)][l32];
+            });
+            __syncthreads();
+        };
+        to_res(l);
+        to_res(h);
+        res_xform<R, R, false, true, JIT>(l, h, rtab);
+        res_mid<R, R>(l, h, p.mid);
+        res_xform<R, R, true, true, JIT>(l, h, rtab);
+        to_grp(l);
+        to_grp(h);
+        {  // d = 16, then back to the plain group arrangement
+            uint32_t c[kTabW];
+            if constexpr (JIT) tab_load_jit(wF + w * kTabW, c);
+            else tab_load(wF + w * kTabW, c);
+            sfor<E / 2>([&](auto P) {
+                constexpr int i = 2 * decltype(P)::value;
+                fft2v(l[i], h[i], l[i + 1], h[i + 1], c);
+            });
+            sfor<E / 2>([&](auto P) {
+                constexpr int i = 2 * decltype(P)::value;
+                swap_halves(l[i], l[i + 1]);
+                swap_halves(h[i], h[i + 1]);
+            });
+        }
+        grp_xform<E, true, JIT>(l, h, tF);
+        const auto out = rsrc(p.cs.out_base + rel);
+        sfor<E>([&](auto I) {
+            constexpr int i = decltype(I)::value;
+            const uint32_t v = (uint32_t)i < lim ? lo : kOob16;
+            const uint32_t so = oo + (2u * E * w + i) * es;
+            st(out, l[i], v, so);
+            st(out, h[i], v + 32u, so);
+        });
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Decoder
 // ---------------------------------------------------------------------------
@@ -1710,16 +1849,39 @@ hipError_t run_encode(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st) {
             hipLaunchKernelGGL((enc16_kernel<512, 64>), dim3(grid), dim3(512), 0, st, p);
             return hipGetLastError();
         }
-        // production (form 0): persistent, LDS tables beside a half exchange buffer,
-        // compiler-scheduled table reads -- c5 0.568-0.574 ms per square against
-        // 0.581-0.583 for the round-3 form (2) and 0.584 with just-in-time table reads
-        // (5), profiles/r04j_gf16_enc_ab.jsonl
+        // production since round 4 (form 0): the half-wave form with just-in-time tables
+        // (enc16h512_kernel<true>), c5 0.472-0.474 ms per square against 0.587-0.590 for
+        // 512-byte chunks (form 4 below; profiles/r04aa_gf16_enc_ab.jsonl).  Diagnostic
+        // forms: 1 8 waves x 64 elements (above), 4 persistent 16 waves x 32 elements, LDS
+        // tables beside a half exchange buffer (0.568-0.574, production through the
+        // round's middle), 2 the round-3 form (0.581-0.583), 3 form 2 with the half
+        // buffer, 5 form 4 with just-in-time table reads (0.584), 8 / 9 forms 4 / 5 with
+        // the merged middle pair, 16 the half-wave form with compiler-scheduled table
+        // reads (0.505-0.510)
         switch (enc16_form()) {
-            case 0: hipLaunchKernelGGL((enc16_kernel<512, 32, 3>), dim3(pgrid), dim3(1024), 0, st, p); return hipGetLastError();
+            case 0: {
+                Enc16 ph = p;
+                ph.chunks = (cs.S + 255) / 256;
+                const uint64_t th = (uint64_t)cs.count * ph.chunks;
+                if (th >= (1ull << 31)) return hipErrorInvalidValue;
+                const uint32_t gh = th > g.cus ? g.cus : (uint32_t)th;
+                hipLaunchKernelGGL(enc16h512_kernel<true>, dim3(gh), dim3(1024), 0, st, ph);
+                return hipGetLastError();
+            }
+            case 4: hipLaunchKernelGGL((enc16_kernel<512, 32, 3>), dim3(pgrid), dim3(1024), 0, st, p); return hipGetLastError();
             case 3: hipLaunchKernelGGL((enc16_kernel<512, 32, 1>), dim3(grid), dim3(1024), 0, st, p); return hipGetLastError();
             case 5: hipLaunchKernelGGL((enc16_kernel<512, 32, 7>), dim3(pgrid), dim3(1024), 0, st, p); return hipGetLastError();
             case 8: hipLaunchKernelGGL((enc16_kernel<512, 32, 11>), dim3(pgrid), dim3(1024), 0, st, p); return hipGetLastError();
             case 9: hipLaunchKernelGGL((enc16_kernel<512, 32, 15>), dim3(pgrid), dim3(1024), 0, st, p); return hipGetLastError();
+            case 16: {
+                Enc16 ph = p;
+                ph.chunks = (cs.S + 255) / 256;
+                const uint64_t th = (uint64_t)cs.count * ph.chunks;
+                if (th >= (1ull << 31)) return hipErrorInvalidValue;
+                const uint32_t gh = th > g.cus ? g.cus : (uint32_t)th;
+                hipLaunchKernelGGL(enc16h512_kernel<false>, dim3(gh), dim3(1024), 0, st, ph);
+                return hipGetLastError();
+            }
             default: break;
         }
     }

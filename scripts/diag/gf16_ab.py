@@ -1,8 +1,6 @@
 """GF(2^16) encoder A/B (diagnostic library): device time per c5 square (k = 512,
-S = 512) with the m = 512 encoder forms of rsm_diag_set_enc16_e64 (0 production:
-16 waves, persistent, LDS tables beside a half exchange buffer; 2 the round-3
-scalar-table form; 3 form 2 with the half buffer; 5 form 0 with just-in-time table
-reads); every output is checked against the round-3 form's.  One JSON line
+S = 512) with the m = 512 encoder forms of rsm_diag_set_enc16_e64 (the list is in
+include/rsmt2d_hip_diag.h); every output is checked against the first form's.  One JSON line
 per configuration.  GF16AB_FORMS (comma list) picks the m = 512 forms, GF16AB_REPS the
 repetitions, GF16AB_C4=0 skips the c4 part, GF16AB_C4FORMS its forms (single-form runs under rocprofv3 --pmc).
 usage: python3 scripts/diag/gf16_ab.py"""
@@ -35,7 +33,7 @@ def main():
     p = ctypes.c_void_p()
     chk(D.rsm_dev_alloc(ctx, n, ctypes.byref(p)))
     outs = {}
-    forms = [int(f) for f in os.environ.get("GF16AB_FORMS", "2,0,5,8,9").split(",")]
+    forms = [int(f) for f in os.environ.get("GF16AB_FORMS", "2,4,0").split(",")]
     base = forms[0]
     for rep in range(int(os.environ.get("GF16AB_REPS", "2"))):
         for e64 in forms:
