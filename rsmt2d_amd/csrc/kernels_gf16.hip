@@ -734,7 +734,8 @@ __device__ __forceinline__ void xch_halfwave(uint32_t (&v)[E], uint32_t (*xch)[3
     __syncthreads();
 }
 
-template <bool JIT>
+// PF: the next task's points are loaded while the current one transforms
+template <bool JIT, bool PF = false>
 __global__ __launch_bounds__(512, 4) void enc16h_kernel(Enc16 p) {
     constexpr int M = 256, E = 16, G = 16, R = 16, THREADS = 512;
     constexpr int GT = G * (E - 1) * kTabW;
@@ -756,13 +757,14 @@ __global__ __launch_bounds__(512, 4) void enc16h_kernel(Enc16 p) {
     const uint32_t hoff = hh * (uint32_t)E * es;     // the half's first element, beyond the wave's
     const uint32_t* tI = gI + g * (E - 1) * kTabW;
     const uint32_t* tF = gF + g * (E - 1) * kTabW;
-    for (uint32_t task = blockIdx.x; task < tasks; task += gridDim.x) {
-        const uint32_t q = task / p.chunks, chunk = task - q * p.chunks;
+    auto lane_off = [&](uint32_t task) -> uint32_t {
+        const uint32_t chunk = task - (task / p.chunks) * p.chunks;
         const uint32_t off = (chunk * 4u + (l32 >> 3)) * 64u + (l32 & 7u) * 4u;
-        const uint32_t lo = off < S ? off + hoff : kOob16;
-        const uint64_t rel = cw_rel(p.cs, q);
-        const auto in = rsrc(p.cs.base + rel);
-        uint32_t l[E], h[E];
+        return off < S ? off + hoff : kOob16;
+    };
+    auto load_task = [&](uint32_t task, uint32_t (&l)[E], uint32_t (&h)[E]) {
+        const uint32_t lo = lane_off(task);
+        const auto in = rsrc(p.cs.base + cw_rel(p.cs, task / p.chunks));
         sfor<E>([&](auto I) {
             constexpr int i = decltype(I)::value;
             const uint32_t v = (uint32_t)i < lim ? lo : kOob16;
@@ -770,6 +772,24 @@ __global__ __launch_bounds__(512, 4) void enc16h_kernel(Enc16 p) {
             l[i] = ld(in, v, so);
             h[i] = ld(in, v + 32u, so);
         });
+    };
+    uint32_t nl[E], nh[E];
+    if constexpr (PF)
+        if (blockIdx.x < tasks) load_task(blockIdx.x, nl, nh);
+    for (uint32_t task = blockIdx.x; task < tasks; task += gridDim.x) {
+        const uint32_t q = task / p.chunks;
+        const uint32_t lo = lane_off(task);
+        const uint64_t rel = cw_rel(p.cs, q);
+        uint32_t l[E], h[E];
+        if constexpr (PF) {
+            sfor<E>([&](auto I) {
+                l[decltype(I)::value] = nl[decltype(I)::value];
+                h[decltype(I)::value] = nh[decltype(I)::value];
+            });
+            if (task + gridDim.x < tasks) load_task(task + gridDim.x, nl, nh);
+        } else {
+            load_task(task, l, h);
+        }
         grp_xform<E, false, JIT>(l, h, tI);
         xch_halfwave<E>(l, xch, g, l32, true);
         xch_halfwave<E>(h, xch, g, l32, true);
@@ -809,7 +829,8 @@ __device__ __forceinline__ uint32_t swapped_elem(uint32_t w, int r, uint32_t hh)
     return 32u * w + ((r & 1) ? 16u : 0u) + (uint32_t)(r & ~1) + hh;
 }
 
-template <bool JIT>
+// PF: the next task's points are loaded while the current one transforms (32 more registers)
+template <bool JIT, bool PF = false>
 __global__ __launch_bounds__(1024, 4) void enc16h512_kernel(Enc16 p) {
     constexpr int M = 512, E = 16, G = 32, R = 16, THREADS = 1024;
     constexpr int GT = G * (E - 1) * kTabW, WT = 16 * kTabW, RT = 2 * (R - 1) * kTabW;
@@ -843,13 +864,14 @@ __global__ __launch_bounds__(1024, 4) void enc16h512_kernel(Enc16 p) {
     const uint32_t hoff = hh * (uint32_t)E * es;
     const uint32_t* tI = gI + g * (E - 1) * kTabW;
     const uint32_t* tF = gF + g * (E - 1) * kTabW;
-    for (uint32_t task = blockIdx.x; task < tasks; task += gridDim.x) {
-        const uint32_t q = task / p.chunks, chunk = task - q * p.chunks;
+    auto lane_off = [&](uint32_t task) -> uint32_t {
+        const uint32_t chunk = task - (task / p.chunks) * p.chunks;
         const uint32_t off = (chunk * 4u + (l32 >> 3)) * 64u + (l32 & 7u) * 4u;
-        const uint32_t lo = off < S ? off + hoff : kOob16;
-        const uint64_t rel = cw_rel(p.cs, q);
-        const auto in = rsrc(p.cs.base + rel);
-        uint32_t l[E], h[E];
+        return off < S ? off + hoff : kOob16;
+    };
+    auto load_task = [&](uint32_t task, uint32_t (&l)[E], uint32_t (&h)[E]) {
+        const uint32_t lo = lane_off(task);
+        const auto in = rsrc(p.cs.base + cw_rel(p.cs, task / p.chunks));
         sfor<E>([&](auto I) {
             constexpr int i = decltype(I)::value;
             const uint32_t v = (uint32_t)i < lim ? lo : kOob16;
@@ -857,6 +879,24 @@ __global__ __launch_bounds__(1024, 4) void enc16h512_kernel(Enc16 p) {
             l[i] = ld(in, v, so);
             h[i] = ld(in, v + 32u, so);
         });
+    };
+    uint32_t nl[E], nh[E];
+    if constexpr (PF)
+        if (blockIdx.x < tasks) load_task(blockIdx.x, nl, nh);
+    for (uint32_t task = blockIdx.x; task < tasks; task += gridDim.x) {
+        const uint32_t q = task / p.chunks;
+        const uint32_t lo = lane_off(task);
+        const uint64_t rel = cw_rel(p.cs, q);
+        uint32_t l[E], h[E];
+        if constexpr (PF) {
+            sfor<E>([&](auto I) {
+                l[decltype(I)::value] = nl[decltype(I)::value];
+                h[decltype(I)::value] = nh[decltype(I)::value];
+            });
+            if (task + gridDim.x < tasks) load_task(task + gridDim.x, nl, nh);
+        } else {
+            load_task(task, l, h);
+        }
         grp_xform<E, false, JIT>(l, h, tI);
         {  // d = 16
             sfor<E / 2>([&](auto P) {
@@ -1873,6 +1913,15 @@ hipError_t run_encode(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st) {
             case 5: hipLaunchKernelGGL((enc16_kernel<512, 32, 7>), dim3(pgrid), dim3(1024), 0, st, p); return hipGetLastError();
             case 8: hipLaunchKernelGGL((enc16_kernel<512, 32, 11>), dim3(pgrid), dim3(1024), 0, st, p); return hipGetLastError();
             case 9: hipLaunchKernelGGL((enc16_kernel<512, 32, 15>), dim3(pgrid), dim3(1024), 0, st, p); return hipGetLastError();
+            case 18: {  // the production form with the next task's points prefetched
+                Enc16 ph = p;
+                ph.chunks = (cs.S + 255) / 256;
+                const uint64_t th = (uint64_t)cs.count * ph.chunks;
+                if (th >= (1ull << 31)) return hipErrorInvalidValue;
+                const uint32_t gh = th > g.cus ? g.cus : (uint32_t)th;
+                hipLaunchKernelGGL((enc16h512_kernel<true, true>), dim3(gh), dim3(1024), 0, st, ph);
+                return hipGetLastError();
+            }
             case 16: {
                 Enc16 ph = p;
                 ph.chunks = (cs.S + 255) / 256;
@@ -1903,7 +1952,8 @@ hipError_t run_encode(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st) {
             const uint64_t th = (uint64_t)cs.count * ph.chunks;
             if (th >= (1ull << 31)) return hipErrorInvalidValue;
             const uint32_t gh = th > 2ull * g.cus ? 2u * g.cus : (uint32_t)th;
-            if (form == 14) hipLaunchKernelGGL(enc16h_kernel<false>, dim3(gh), dim3(512), 0, st, ph);
+            if (form == 19) hipLaunchKernelGGL((enc16h_kernel<true, true>), dim3(gh), dim3(512), 0, st, ph);
+            else if (form == 14) hipLaunchKernelGGL(enc16h_kernel<false>, dim3(gh), dim3(512), 0, st, ph);
             else hipLaunchKernelGGL(enc16h_kernel<true>, dim3(gh), dim3(512), 0, st, ph);
             return hipGetLastError();
         }
