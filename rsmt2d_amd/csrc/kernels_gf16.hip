@@ -1418,8 +1418,8 @@ __global__ __launch_bounds__(1024, 4) void dec16f_kernel(Dec16 p) {
 // No element bit is held by the registers in both layouts (group: bits 0-4, residue:
 // bits 5-9), so the exchange buffer -- one plane, [1024][16] -- moves half the LANES per
 // pass (lanes 0-15 of both halves, then 16-31).  One LDS pool holds in turn the
-// per-element scale tables (stage_elem_tabs), the twiddle tables (the group tables of
-// one direction, 32 halves x 31 slots = 79 KiB, restaged between the phases) and the
+// per-element scale tables (stage_elem_tabs), the twiddle tables (the group tables, 32
+// halves x 31 slots = 79 KiB: the decoder's IFFT and FFT twiddles coincide) and the
 // per-element reveal tables.
 // ---------------------------------------------------------------------------
 // diagnostic phase stamp of the single-pass decoders (RSM_DIAG builds with a decode
@@ -1577,11 +1577,10 @@ __global__ __launch_bounds__(1024, 4) void dec16h_kernel(Dec16 p) {
     d16_stamp(p, 3);
     grp_xform<E, false, true>(l, h, gtab + g * (E - 1) * kTabW);
     d16_stamp(p, 4);
-    uint32_t gfv[grp_tab_per<G, E, 1024>()];  // the FFT group tables, loaded ahead of the exchange
-    load_grp<G, E, true, 1024>(p.tw, 0, gfv);
     xch_lanesplit<E>(l, xch, g, l32, true);
     xch_lanesplit<E>(h, xch, g, l32, true);
-    store_grp<G, E, 1024>(gtab, gfv);  // every wave is past its IFFT group tables
+    // (the decoder's FFT twiddles SKEW[b + d - 1] are its IFFT ones SKEW[-1 + b + d]: the
+    // group tables stay)
     d16_stamp(p, 5);
     res_xform<E, R, false, false, true, false>(l, h, rtab);
     d16_stamp(p, 6);
@@ -1592,7 +1591,7 @@ __global__ __launch_bounds__(1024, 4) void dec16h_kernel(Dec16 p) {
     res_xform<E, R, true, false, true, false>(l, h, rtab);
     d16_stamp(p, 8);
     xch_lanesplit<E>(l, xch, g, l32, false);
-    xch_lanesplit<E>(h, xch, g, l32, false);  // (its barriers also publish the FFT tables)
+    xch_lanesplit<E>(h, xch, g, l32, false);
     d16_stamp(p, 9);
     grp_xform<E, true, true>(l, h, gtab + g * (E - 1) * kTabW);
     __syncthreads();  // every wave is past the twiddle tables
@@ -1975,6 +1974,7 @@ static uint32_t dec16_diag_mode() { return 0u; }
 // k = 512 1.43-1.45 ms against 1.84-1.85 for the five passes (diagnostic A/B:
 // rsm_diag_set_dec16_five_pass; profiles/r04w_gf16_dec_ab.jsonl)
 static bool dec16h_enabled() { return !dec16_five_pass(); }
+
 
 template <int M>
 hipError_t run_decode(const DecodeSet& ds, const Gf16Dev& g, const uint16_t* logwalsh, hipStream_t st) {

@@ -4,7 +4,8 @@ erased, BenchmarkRepair), S = 512, decoded by rsm_decode_vectors_dev:
           production) or the five global passes (rsm_diag_set_dec16_five_pass);
   k = 128 (GF(2^8) split decoder): the upper half of the grid delays its point loads by
           DECAB_DELAYS ticks of the 100 MHz clock (rsm_diag_set_dec_delay; 0 = production).
-DECAB_KS picks the k values (default 256,200).  Every rebuilt square compared with the original EDS.  One JSON line per configuration.
+DECAB_KS picks the k values (default 256,200); DECAB_V16 the GF(2^16) variants (0 production,
+1 the five passes, other values rsm_diag_set_dec16_mode bits).  Every rebuilt square compared with the original EDS.  One JSON line per configuration.
 usage: python3 scripts/diag/dec_ab.py"""
 import ctypes
 import json
@@ -52,8 +53,13 @@ def main():
         chk(D.rsm_memcpy(ctx, pres.value, present.ctypes.data, W * W, 0))
         ids = np.arange(W, dtype=np.uint32)
         chk(D.rsm_memcpy(ctx, idx.value, ids.ctypes.data, 4 * W, 0))
-        setter = D.rsm_diag_set_dec16_five_pass if k > 128 else D.rsm_diag_set_dec_delay
-        variants = (0, 1) if k > 128 else [int(x) for x in os.environ.get("DECAB_DELAYS", "0,150,300,450").split(",")]
+        def set16(v):  # 0 production, 1 the five passes, other values rsm_diag_set_dec16_mode bits
+            chk(D.rsm_diag_set_dec16_five_pass(1 if v == 1 else 0))
+            chk(D.rsm_diag_set_dec16_mode(0 if v == 1 else v))
+            return 0
+        setter = set16 if k > 128 else D.rsm_diag_set_dec_delay
+        variants = ([int(x) for x in os.environ.get("DECAB_V16", "0,1").split(",")] if k > 128
+                    else [int(x) for x in os.environ.get("DECAB_DELAYS", "0,150,300,450").split(",")])
         for rep in range(2):
             for five in variants:
                 chk(setter(five))
