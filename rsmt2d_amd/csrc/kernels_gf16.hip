@@ -1319,18 +1319,19 @@ template <int M>
 __global__ __launch_bounds__(1024, 4) void dec16f_kernel(Dec16 p) {
     constexpr int N = 2 * M, E = 32, R = N / E, WAVES = N / E;
     static_assert(WAVES == 16 && R == 16, "n = 512: 16 waves of 32 elements, residues of 16");
-    constexpr int GT = WAVES * (E - 1) * kTabW;  // group tables of one direction (words)
+    constexpr int GT = WAVES * (E - 1) * kTabW;  // group tables (words)
     __shared__ uint32_t xch[N / 2][64];
-    __shared__ uint32_t tabs[2 * GT + 2 * (R - 1) * kTabW];
+    __shared__ uint32_t tabs[GT + 2 * (R - 1) * kTabW];
+    // decoder skews: IFFT SKEW[-1 + b + d], FFT SKEW[b + d - 1] -- the same tables, so
+    // one set serves both directions; staged once per workgroup of the persistent grid
     uint32_t* gI = tabs;
-    uint32_t* gF = tabs + GT;
-    uint32_t* rtab = tabs + 2 * GT;
+    uint32_t* gF = tabs;
+    uint32_t* rtab = tabs + GT;
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
-    // decoder skews: IFFT SKEW[-1 + b + d] (off = -1), FFT SKEW[b + d - 1]
     stage_grp<WAVES, E, false>(gI, p.tw, -1);
-    stage_grp<WAVES, E, true>(gF, p.tw, 0);
     stage_res<R, E, WAVES * 64>(rtab, p.tw, -1);
-    const uint32_t task = blockIdx.x;
+    const uint32_t tasks = p.count * p.chunks;
+    for (uint32_t task = blockIdx.x; task < tasks; task += gridDim.x) {
     const uint32_t q = task / p.chunks, chunk = task - q * p.chunks;
     const Lane ln = lane_of(chunk, p.ds.S);
     const uint32_t k = p.ds.k, S = p.ds.S;
@@ -1401,6 +1402,8 @@ __global__ __launch_bounds__(1024, 4) void dec16f_kernel(Dec16 p) {
             st(sq, h[i], ln.lo + 32, so);
         }
     });
+    __syncthreads();  // the next task's scale tables reuse the exchange buffer
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -2003,7 +2006,8 @@ hipError_t run_decode(const DecodeSet& ds, const Gf16Dev& g, const uint16_t* log
         }
         if constexpr (M == 256) {
             if (!dec16_five_pass()) {  // the single-pass form (diagnostic builds can A/B the five passes)
-                hipLaunchKernelGGL(dec16f_kernel<M>, dim3(p.count * chunks), dim3(1024), 0, st, p);
+                const uint32_t tk = p.count * chunks;
+                hipLaunchKernelGGL(dec16f_kernel<M>, dim3(tk > g.cus ? g.cus : tk), dim3(1024), 0, st, p);
                 if (hipError_t e = hipGetLastError()) return e;
                 continue;
             }
