@@ -3,7 +3,7 @@
 # headline kernel trace/stats.  PART=A|B picks the half (one gpurun call each).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=gpurun_out/r04final; mkdir -p $OUT
+OUT=gpurun_out/${RUN:-r04final}; mkdir -p $OUT
 export TMPDIR=/tmp
 step() { local n=$1 t=$2; shift 2; echo "[$(date +%T)] $n" >> $OUT/steps.log; timeout -k 10 $t "$@" > $OUT/$n.log 2>&1; local rc=$?; echo "[$(date +%T)] $n rc=$rc" >> $OUT/steps.log; tail -n 3 $OUT/$n.log; return $rc; }
 if [ "${PART:-A}" = A ]; then
