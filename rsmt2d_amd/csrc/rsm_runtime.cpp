@@ -222,6 +222,11 @@ int launch_encode(rsm_ctx* ctx, const CodewordSet& cs0, hipStream_t st) {
     CodewordSet cs = cs0;
     if (cs.out_base == nullptr) cs.out_base = cs.base;
     hipError_t e;
+    // the single-pass kernels address a codeword's cells with 32-bit buffer offsets from
+    // its first cell (the multi-pass m >= 1024 path folds them into 64-bit bases)
+    if ((field_bits(cs.k) == 8 || !gf16_generic(cs.k)) &&
+        cs.out_offset + (uint64_t)cs.k * cs.elem_stride + cs.S >= (1ull << 31))
+        return fail(RSM_EUNSUPPORTED, "encode: k=%u with %u-byte shares spans over 2 GiB per codeword", cs.k, cs.S);
     if (field_bits(cs.k) == 8) {
         cs.chunks = (cs.S + 255) / 256;
         const uint32_t cap = ctx->pass_grid[cs.pass == 0 ? 0 : 1].load(std::memory_order_relaxed);
@@ -254,6 +259,9 @@ int launch_encode(rsm_ctx* ctx, const CodewordSet& cs0, hipStream_t st) {
 int launch_decode(rsm_ctx* ctx, const DecodeSet& ds0, hipStream_t st) {
     DecodeSet ds = ds0;
     hipError_t e;
+    // the single-pass decoders address the square's cells with 32-bit buffer offsets
+    if ((field_bits(ds.k) == 8 || !gf16_generic(ds.k)) && 4ull * ds.k * ds.k * ds.S >= (1ull << 31))
+        return fail(RSM_EUNSUPPORTED, "decode: a %ux%u square of %u-byte shares is over 2 GiB", 2 * ds.k, 2 * ds.k, ds.S);
     if (field_bits(ds.k) == 8) {
         ds.chunks = (ds.S + 255) / 256;
         e = launch_decode_gf8(ds, st);
