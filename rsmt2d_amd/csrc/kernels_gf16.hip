@@ -1341,14 +1341,15 @@ __global__ __launch_bounds__(1024, 4) void dec16f_kernel(Dec16 p) {
         return e < k ? k + e : (e >= (uint32_t)M && e < (uint32_t)M + k) ? e - (uint32_t)M : 0xFFFFFFFFu;
     };
     uint32_t* etab = &xch[0][0];  // per-element tables while the exchange buffer is idle
-    uint32_t etv[elem_tab_per<N, 1024>()];  // the scale tables' err -> table chain first
-    load_elem_tabs<N, 1024>(p, q, false, etv);
-    // presence: lane j < 32 of wave w asks for slot 32 w + j (one load per lane, a ballot)
+    // presence: lane j < 32 of wave w asks for slot 32 w + j (one load per lane, a ballot);
+    // issued first, the scale tables' err -> table chain beside it
     const uint32_t vec = __builtin_amdgcn_readfirstlane(p.ds.indices[p.q0 + q]);
     const uint32_t Wd = 2u * k;
     auto cell = [&](uint32_t s) -> uint32_t { return p.ds.axis == 0 ? vec * Wd + s : s * Wd + vec; };
     const uint32_t my_s = lane < (uint32_t)E ? share_of(E * w + lane) : 0xFFFFFFFFu;
     const uint32_t my_p = my_s != 0xFFFFFFFFu ? (uint32_t)p.ds.presence[cell(my_s)] : 0u;
+    uint32_t etv[elem_tab_per<N, 1024>()];
+    load_elem_tabs<N, 1024>(p, q, false, etv);
     const uint32_t have = __builtin_amdgcn_readfirstlane((uint32_t)__ballot(my_p != 0u));
     uint32_t l[E], h[E];
     sfor<E>([&](auto I) {
@@ -1525,18 +1526,19 @@ __global__ __launch_bounds__(1024, 4) void dec16h_kernel(Dec16 p) {
     auto share_of = [&](uint32_t e) -> uint32_t {
         return e < k ? k + e : (e >= (uint32_t)M && e < (uint32_t)M + k) ? e - (uint32_t)M : 0xFFFFFFFFu;
     };
-    // the scale tables' err -> table chain first (it depends on nothing else)
-    uint32_t etv[elem_tab_per<N, 1024>()];
-#ifdef RSM_DIAG
-    if (!(p.diag & 1u))  // A/B bit 0: no scale / reveal table staging (wrong output)
-#endif
-    load_elem_tabs<N, 1024>(p, q, false, etv);
     // presence: lane j of wave w asks for element 64 w + j = register j & 31 of half j >> 5
+    // (issued first: the point loads wait for it; the scale tables' err -> table chain
+    // runs beside it)
     const uint32_t vec = __builtin_amdgcn_readfirstlane(p.ds.indices[p.q0 + q]);
     const uint32_t Wd = 2u * k;
     auto cell = [&](uint32_t s) -> uint32_t { return p.ds.axis == 0 ? vec * Wd + s : s * Wd + vec; };
     const uint32_t my_s = share_of(64u * w + lane);
     const uint32_t my_p = my_s != 0xFFFFFFFFu ? (uint32_t)p.ds.presence[cell(my_s)] : 0u;
+    uint32_t etv[elem_tab_per<N, 1024>()];
+#ifdef RSM_DIAG
+    if (!(p.diag & 1u))  // A/B bit 0: no scale / reveal table staging (wrong output)
+#endif
+    load_elem_tabs<N, 1024>(p, q, false, etv);
     const uint64_t hv = __ballot(my_p != 0u);
     const uint32_t have0 = __builtin_amdgcn_readfirstlane((uint32_t)hv);
     const uint32_t have1 = __builtin_amdgcn_readfirstlane((uint32_t)(hv >> 32));
