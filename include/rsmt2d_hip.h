@@ -27,7 +27,9 @@ extern "C" {
 #define RSM_ESHAPE (-4)        /* non-square count, uneven shares, odd EDS width, > MaxChunks */
 #define RSM_EDEVICE (-5)       /* HIP runtime failure / no GPU: never a silent CPU fallback */
 #define RSM_ENOMEM (-6)
-#define RSM_EUNSUPPORTED (-7)  /* configuration this build does not implement */
+#define RSM_EUNSUPPORTED (-7)  /* configuration this build does not implement -- among them
+                                   squares of 2 GiB or more with k <= 512 (the single-pass
+                                   kernels address cells with 32-bit buffer offsets) */
 #define RSM_EUNREPAIRABLE (-8) /* ErrUnrepairableDataSquare (extendeddatacrossword.go:37) */
 #define RSM_EBYZANTINE (-9)    /* ErrByzantineData (extendeddatacrossword.go:42-58) */
 #define RSM_ECELL (-10)        /* SetCell on a non-nil cell or wrong size (datasquare.go:341-353) */
