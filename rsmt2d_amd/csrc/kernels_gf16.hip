@@ -1486,9 +1486,10 @@ __device__ __forceinline__ void deriv_halfwave(uint32_t (&v)[R], uint32_t (*x2)[
                 constexpr int t = decltype(T)::value;
                 if constexpr ((1 << t) < R && ((j >> t) & 1) == 0) a ^= v[j + (1 << t)];
             });
-            {  // t = 0: the other lane half (g ^ 1), when this half's bit is 0
-                const uint32_t x = x2[(g ^ 1u) + E * (j - hf * HJ)][l32];
-                a ^= hi ? 0u : x;
+            {  // t = 0: the other lane half (g ^ 1) of this wave's register j, when this
+               // half's bit is 0 -- a lane swap instead of an LDS read
+                const auto sw = __builtin_amdgcn_permlane32_swap(v[j], v[j], false, false);
+                a ^= hi ? 0u : sw[1];
             }
             sfor<ilog2c(E) - 1>([&](auto B) {  // t = 1..4: bit t - 1 of w
                 constexpr uint32_t bit = 2u << decltype(B)::value;
