@@ -710,6 +710,58 @@ def bench_single_square(local, L, R, k=128, S=512, reps=200):
                     "launch (rsm_ctx_set_split_max 0)"}
 
 
+def bench_small_squares(local, L, R, S=512, ks=(4, 8, 16, 32, 64)):
+    """BenchmarkExtensionEncoding's small squares (extendeddatasquare_test.go:279-302:
+    k = 4 .. 64 at shareSize 512, GF(2^8) byte-table kernels): per k, one square per
+    call (what a cgo ComputeExtendedDataSquare gets, device-resident: back-to-back calls
+    on one stream, device time per call) and a batch of squares per call (1 GiB of EDS)
+    as throughput.  Every k is oracle-checked first."""
+    import ctypes
+    import numpy as np
+    import oracle
+    ctx = R.device_context(local)
+    e0, e1 = ctypes.c_void_p(), ctypes.c_void_p()
+    R._check(L.rsm_event_create(ctx, ctypes.byref(e0)))
+    R._check(L.rsm_event_create(ctx, ctypes.byref(e1)))
+
+    def dev_ms(ptr, k, count, n):
+        R._check(L.rsm_extend_squares_dev(ctx, ptr, k, S, count, None))  # warm
+        R._check(L.rsm_event_record(ctx, e0, None))
+        for _ in range(n):
+            R._check(L.rsm_extend_squares_dev(ctx, ptr, k, S, count, None))
+        R._check(L.rsm_event_record(ctx, e1, None))
+        ms = ctypes.c_float()
+        R._check(L.rsm_event_elapsed_ms(e0, e1, ctypes.byref(ms)))
+        return ms.value / n
+
+    out = {}
+    for k in ks:
+        W = 2 * k
+        sq = W * W * S
+        B = max(1, (1 << 30) // sq)
+        buf = R.DeviceBuffer(B * sq, local)
+        buf.fill_random(0x5A + k)
+        R._check(L.rsm_extend_squares_dev(ctx, buf.ptr, k, S, B, None))
+        R._check(L.rsm_sync(ctx))
+        for i in (0, B - 1):
+            got = buf.download(sq, i * sq).reshape(W, W, S)
+            if not np.array_equal(got, oracle.extend_square(got[:k, :k].copy(), nthreads=8)):
+                raise SystemExit(f"bench small squares: GPU EDS (k={k}) differs from the oracle")
+        one = dev_ms(buf.ptr, k, 1, 200)
+        batch = dev_ms(buf.ptr, k, B, 10)
+        buf.free()
+        out[str(k)] = {"single_square_us": round(one * 1e3, 2), "batch_squares": B,
+                       "batch_us_per_square": round(batch * 1e3 / B, 3),
+                       "batch_ods_GiB_s": round(k * k * S * B / (batch / 1e3) / 2**30, 2),
+                       "batch_frac": round(4 * k * k * S * B / (batch / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
+    for e in (e0, e1):
+        L.rsm_event_destroy(e)
+    return {"workload": f"BenchmarkExtensionEncoding k = {', '.join(map(str, ks))} at S = {S} (GF(2^8))",
+            "kernel": "encode_gf8_kernel<M> (byte tables), row pass then column pass", "by_k": out,
+            "note": "single = one square per rsm_extend_squares_dev (device time of back-to-back calls on one "
+                    "stream); batch = 1 GiB of EDS per call; frac = 4 k^2 S per square / time / 8 TB/s"}
+
+
 def bench_c4(local, L, R, steps, B=2, k=256, S=2048):
     """Config 4: 256x256 -> 512x512 squares of 2048 B shares (GF(2^16), enc16h_kernel: m = 256),
     device-resident, B squares (1 GiB of EDS) per step, steps alternating over two
@@ -1118,9 +1170,12 @@ def main():
         out["cpu_baseline"] = None if a.no_cpu_baseline else cpu_baseline(k, S, a.cpu_seconds)
         cb = out["cpu_baseline"]
         if cb:
-            # GPU / CPU against the measured affinity-wide run and against the linear
+            # GPU / CPU against the measured run capped to the job's CPU share (cb["value"]),
+            # against the run on every CPU of the affinity mask, and against the linear
             # all-host-CPUs extrapolation of the single-thread rate
             cb["gpu_over_cpu"] = round(value / cb["value"], 2)
+            if cb.get("affinity_threads_GiB_s"):
+                cb["gpu_over_cpu_affinity_threads"] = round(value / cb["affinity_threads_GiB_s"], 2)
             cb["gpu_over_cpu_all_cores_estimate"] = round(value / cb["all_cores_estimate_GiB_s"], 2)
     if rank == 0 and world == 1 and not a.no_roots:
         out["with_roots"] = bench_roots(local, L, R, buf, k, S, B, a.steps)
@@ -1131,6 +1186,7 @@ def main():
         R._check(L.rsm_stream_destroy(ctx, st))
     if rank == 0 and world == 1 and k == 128 and not a.no_single:
         out["single_square"] = bench_single_square(local, L, R)
+        out["small_squares"] = bench_small_squares(local, L, R)
         if not a.no_c4:
             out["c4"] = bench_c4(local, L, R, a.steps)
             # BenchmarkExtensionEncoding's k = 256 square at its shareSize 512 (GF(2^16))

@@ -27,9 +27,8 @@ extern "C" {
 #define RSM_ESHAPE (-4)        /* non-square count, uneven shares, odd EDS width, > MaxChunks */
 #define RSM_EDEVICE (-5)       /* HIP runtime failure / no GPU: never a silent CPU fallback */
 #define RSM_ENOMEM (-6)
-#define RSM_EUNSUPPORTED (-7)  /* configuration this build does not implement -- among them
-                                   squares of 2 GiB or more with k <= 512 (the single-pass
-                                   kernels address cells with 32-bit buffer offsets) */
+#define RSM_EUNSUPPORTED (-7)  /* configuration this build does not implement (2k > 65536,
+                                   as klauspost rejects it; device roots beyond their widths) */
 #define RSM_EUNREPAIRABLE (-8) /* ErrUnrepairableDataSquare (extendeddatacrossword.go:37) */
 #define RSM_EBYZANTINE (-9)    /* ErrByzantineData (extendeddatacrossword.go:42-58) */
 #define RSM_ECELL (-10)        /* SetCell on a non-nil cell or wrong size (datasquare.go:341-353) */
@@ -63,6 +62,14 @@ int rsm_ctx_set_pass_grid(rsm_ctx* ctx, int pass, int cus, int* previous);
  * queue launch.  Default 12.  *previous (may be NULL) receives the old value.  Results
  * never depend on it. */
 int rsm_ctx_set_split_max(rsm_ctx* ctx, int squares, int* previous);
+/* Test hook: the single-pass kernels address each half of a codeword with 32-bit
+ * offsets, so codewords whose halves span more than offset_limit bytes (default 2^31:
+ * columns of squares over 4 GiB) run on the wide forms (64-bit per-symbol bases), and
+ * GF(2^16) work arrays get at most work_budget bytes per stream (default 1 GiB; wider
+ * shares run as byte slabs).  Lowering them sends small shapes down those paths so
+ * their parity can be tested without 4 GiB squares; 0 restores a default.  Results
+ * never depend on them. */
+int rsm_ctx_set_limits(rsm_ctx* ctx, uint64_t offset_limit, uint64_t work_budget);
 const char* rsm_last_error(void);
 const char* rsm_version(void);
 int rsm_device_count(void);

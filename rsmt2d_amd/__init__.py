@@ -117,6 +117,7 @@ SIGNATURES = {
     "rsm_ctx_device": (_I32, [_VP]),
     "rsm_ctx_set_pass_grid": (_I32, [_VP, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     "rsm_ctx_set_split_max": (_I32, [_VP, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
+    "rsm_ctx_set_limits": (_I32, [_VP, _U64, _U64]),
     "rsm_last_error": (ctypes.c_char_p, []),
     "rsm_version": (ctypes.c_char_p, []),
     "rsm_device_count": (_I32, []),

@@ -768,7 +768,8 @@ __global__ __launch_bounds__(512, 4) void enc16h_kernel(Enc16 p) {
         sfor<E>([&](auto I) {
             constexpr int i = decltype(I)::value;
             const uint32_t v = (uint32_t)i < lim ? lo : kOob16;
-            const uint32_t so = (2u * E * w + i) * es;
+            // (0 for padding: an offset past the half would wrap kOob16 + so)
+            const uint32_t so = 2u * E * w + i < k ? (2u * E * w + i) * es : 0u;
             l[i] = ld(in, v, so);
             h[i] = ld(in, v + 32u, so);
         });
@@ -803,7 +804,7 @@ __global__ __launch_bounds__(512, 4) void enc16h_kernel(Enc16 p) {
         sfor<E>([&](auto I) {
             constexpr int i = decltype(I)::value;
             const uint32_t v = (uint32_t)i < lim ? lo : kOob16;
-            const uint32_t so = oo + (2u * E * w + i) * es;
+            const uint32_t so = oo + (2u * E * w + i < k ? (2u * E * w + i) * es : 0u);
             st(out, l[i], v, so);
             st(out, h[i], v + 32u, so);
         });
@@ -875,7 +876,8 @@ __global__ __launch_bounds__(1024, 4) void enc16h512_kernel(Enc16 p) {
         sfor<E>([&](auto I) {
             constexpr int i = decltype(I)::value;
             const uint32_t v = (uint32_t)i < lim ? lo : kOob16;
-            const uint32_t so = (2u * E * w + i) * es;
+            // (0 for padding: an offset past the half would wrap kOob16 + so)
+            const uint32_t so = 2u * E * w + i < k ? (2u * E * w + i) * es : 0u;
             l[i] = ld(in, v, so);
             h[i] = ld(in, v + 32u, so);
         });
@@ -962,7 +964,7 @@ __global__ __launch_bounds__(1024, 4) void enc16h512_kernel(Enc16 p) {
         sfor<E>([&](auto I) {
             constexpr int i = decltype(I)::value;
             const uint32_t v = (uint32_t)i < lim ? lo : kOob16;
-            const uint32_t so = oo + (2u * E * w + i) * es;
+            const uint32_t so = oo + (2u * E * w + i < k ? (2u * E * w + i) * es : 0u);
             st(out, l[i], v, so);
             st(out, h[i], v + 32u, so);
         });
@@ -1335,7 +1337,6 @@ __global__ __launch_bounds__(1024, 4) void dec16f_kernel(Dec16 p) {
     const uint32_t q = task / p.chunks, chunk = task - q * p.chunks;
     const Lane ln = lane_of(chunk, p.ds.S);
     const uint32_t k = p.ds.k, S = p.ds.S;
-    const auto sq = rsrc(p.ds.base);
     // work slot e <- share: e < k parity k + e, M <= e < M + k data e - M, else zero
     auto share_of = [&](uint32_t e) -> uint32_t {
         return e < k ? k + e : (e >= (uint32_t)M && e < (uint32_t)M + k) ? e - (uint32_t)M : 0xFFFFFFFFu;
@@ -1346,6 +1347,11 @@ __global__ __launch_bounds__(1024, 4) void dec16f_kernel(Dec16 p) {
     const uint32_t vec = __builtin_amdgcn_readfirstlane(p.ds.indices[p.q0 + q]);
     const uint32_t Wd = 2u * k;
     auto cell = [&](uint32_t s) -> uint32_t { return p.ds.axis == 0 ? vec * Wd + s : s * Wd + vec; };
+    // this wave's half of the codeword (slots e < M: parity shares, waves w < 8; else
+    // data) from its own 64-bit base, 32-bit offsets within it (narrow_fits)
+    const uint32_t hfirst = w < (uint32_t)WAVES / 2 ? k : 0u, cstep = p.ds.axis == 0 ? 1u : Wd;
+    const auto sq = rsrc(p.ds.base + ((uint64_t)cell(0) + (uint64_t)hfirst * cstep) * S);
+    auto hoff = [&](uint32_t s) -> uint32_t { return (s - hfirst) * cstep * S; };
     const uint32_t my_s = lane < (uint32_t)E ? share_of(E * w + lane) : 0xFFFFFFFFu;
     const uint32_t my_p = my_s != 0xFFFFFFFFu ? (uint32_t)p.ds.presence[cell(my_s)] : 0u;
     uint32_t etv[elem_tab_per<N, 1024>()];
@@ -1355,7 +1361,7 @@ __global__ __launch_bounds__(1024, 4) void dec16f_kernel(Dec16 p) {
     sfor<E>([&](auto I) {
         constexpr int i = decltype(I)::value;
         const uint32_t src = share_of(E * w + i);
-        const uint32_t so = ((have >> i) & 1u) ? cell(src) * S : kOob16;
+        const uint32_t so = ((have >> i) & 1u) ? hoff(src) : kOob16;
         l[i] = ld(sq, ln.lo, so);
         h[i] = ld(sq, ln.lo + 32, so);
     });
@@ -1398,7 +1404,7 @@ __global__ __launch_bounds__(1024, 4) void dec16f_kernel(Dec16 p) {
             l[i] = 0u;
             h[i] = 0u;
             muladd16v(l[i], h[i], yl, yh, c);
-            const uint32_t so = cell(dst) * S;
+            const uint32_t so = hoff(dst);
             st(sq, l[i], ln.lo, so);
             st(sq, h[i], ln.lo + 32, so);
         }
@@ -1523,7 +1529,6 @@ __global__ __launch_bounds__(1024, 4) void dec16h_kernel(Dec16 p) {
     const uint32_t k = p.ds.k, S = p.ds.S;
     const uint32_t off = (chunk * 4u + (l32 >> 3)) * 64u + (l32 & 7u) * 4u;
     const bool lane_ok = off < S;
-    const auto sq = rsrc(p.ds.base);
     auto share_of = [&](uint32_t e) -> uint32_t {
         return e < k ? k + e : (e >= (uint32_t)M && e < (uint32_t)M + k) ? e - (uint32_t)M : 0xFFFFFFFFu;
     };
@@ -1533,6 +1538,11 @@ __global__ __launch_bounds__(1024, 4) void dec16h_kernel(Dec16 p) {
     const uint32_t vec = __builtin_amdgcn_readfirstlane(p.ds.indices[p.q0 + q]);
     const uint32_t Wd = 2u * k;
     auto cell = [&](uint32_t s) -> uint32_t { return p.ds.axis == 0 ? vec * Wd + s : s * Wd + vec; };
+    // this wave's half of the codeword (elements < M: parity shares, waves w < 8; else
+    // data) from its own 64-bit base, 32-bit offsets within it (narrow_fits)
+    const uint32_t hfirst = w < 8u ? k : 0u, cstep = p.ds.axis == 0 ? 1u : Wd;
+    const auto sq = rsrc(p.ds.base + ((uint64_t)cell(0) + (uint64_t)hfirst * cstep) * S);
+    auto hoff = [&](uint32_t s) -> uint32_t { return (s - hfirst) * cstep * S; };
     const uint32_t my_s = share_of(64u * w + lane);
     const uint32_t my_p = my_s != 0xFFFFFFFFu ? (uint32_t)p.ds.presence[cell(my_s)] : 0u;
     uint32_t etv[elem_tab_per<N, 1024>()];
@@ -1548,8 +1558,8 @@ __global__ __launch_bounds__(1024, 4) void dec16h_kernel(Dec16 p) {
     sfor<E>([&](auto I) {  // the two halves' elements of register i: E (2 w) + i, E (2 w + 1) + i
         constexpr int i = decltype(I)::value;
         const uint32_t s0 = share_of(E * 2u * w + i), s1 = share_of(E * (2u * w + 1u) + i);
-        const uint32_t c0 = ((have0 >> i) & 1u) ? cell(s0) * S : kOob16;
-        const uint32_t c1 = ((have1 >> i) & 1u) ? cell(s1) * S : kOob16;
+        const uint32_t c0 = ((have0 >> i) & 1u) ? hoff(s0) : kOob16;
+        const uint32_t c1 = ((have1 >> i) & 1u) ? hoff(s1) : kOob16;
         const uint32_t c = hi ? c1 : c0;
         uint32_t vo = (c == kOob16 || !lane_ok) ? kOob16 : c + off;
 #ifdef RSM_DIAG
@@ -1622,8 +1632,8 @@ __global__ __launch_bounds__(1024, 4) void dec16h_kernel(Dec16 p) {
             tab_load_jit_at<i * kTabW * 4>(etab + E * g * kTabW, c);
             uint32_t xl = 0u, xh = 0u;
             muladd16v(xl, xh, l[i], h[i], c);
-            const uint32_t c0 = m0 ? cell(d0) * S : kOob16;
-            const uint32_t c1 = m1 ? cell(d1) * S : kOob16;
+            const uint32_t c0 = m0 ? hoff(d0) : kOob16;
+            const uint32_t c1 = m1 ? hoff(d1) : kOob16;
             const uint32_t cc = hi ? c1 : c0;
             const uint32_t vo = (cc == kOob16 || !lane_ok) ? kOob16 : cc + off;
             st(sq, xl, vo, 0u);
@@ -1661,6 +1671,7 @@ struct G16Pass {
     const uint16_t* logwalsh;
     uint8_t* work;         // [count][2][npts][S] (decode) or [count][npts][S] (encode)
     uint64_t cw_bytes;     // bytes of one codeword's work (all arrays)
+    uint64_t pitch;        // decode: bytes between consecutive cells (the share size)
     uint32_t npts, m, k, S, chunks;
     uint32_t q0, count;    // codewords [q0, q0 + count) of the set, work slot q - q0
     uint32_t D, bits;      // group stride and size (G = 2^bits <= 16)
@@ -1715,7 +1726,7 @@ __global__ __launch_bounds__(256) void g16_pass_kernel(G16Pass p) {
                 const uint64_t cell = cell_of(p.ds, q, srcs);
                 const bool have = __builtin_amdgcn_readfirstlane(p.ds.presence[cell] ? 1u : 0u) != 0;
                 if (have) {
-                    const auto rs = rsrc(p.ds.base + cell * p.S);
+                    const auto rs = rsrc(p.ds.base + cell * p.pitch);
                     l[j] = ld(rs, ln.lo, 0u);
                     h[j] = ld(rs, ln.lo + 32, 0u);
                     const uint32_t L = __builtin_amdgcn_readfirstlane((uint32_t)p.errs[(uint64_t)qi * p.npts + e]);
@@ -1769,7 +1780,7 @@ __global__ __launch_bounds__(256) void g16_pass_kernel(G16Pass p) {
                 if (missing) {
                     const uint32_t L = kMod16 - __builtin_amdgcn_readfirstlane((uint32_t)p.errs[(uint64_t)qi * p.npts + e]);
                     mul16(l[j], h[j], p.r.perm[L]);
-                    const auto rs = rsrc(p.ds.base + cell * p.S);
+                    const auto rs = rsrc(p.ds.base + cell * p.pitch);
                     st(rs, l[j], ln.lo, 0u);
                     st(rs, h[j], ln.lo + 32, 0u);
                 }
@@ -1980,16 +1991,22 @@ static uint32_t dec16_diag_mode() { return 0u; }
 // k = 512 1.43-1.45 ms against 1.84-1.85 for the five passes (diagnostic A/B:
 // rsm_diag_set_dec16_five_pass; profiles/r04w_gf16_dec_ab.jsonl)
 static bool dec16h_enabled() { return !dec16_five_pass(); }
+}  // namespace
+bool dec16_needs_work() { return dec16_five_pass(); }
+namespace {
 
 
 template <int M>
 hipError_t run_decode(const DecodeSet& ds, const Gf16Dev& g, const uint16_t* logwalsh, hipStream_t st) {
     constexpr int N = 2 * M;
     const uint32_t chunks = (ds.S + 511) / 512;
-    const uint64_t per_cw = 2ull * N * ds.S;
-    uint32_t batch = (uint32_t)(g.scratch_bytes / per_cw);
-    const uint32_t ebatch = (uint32_t)(g.errs_bytes / (N * sizeof(uint16_t)));
-    if (ebatch < batch) batch = ebatch;
+    // batches: the error locators of a batch (the host sizes them for the whole set);
+    // only the five-pass diagnostic form also needs per-codeword work arrays
+    uint32_t batch = (uint32_t)(g.errs_bytes / (N * sizeof(uint16_t)));
+    if (dec16_needs_work()) {
+        const uint32_t wbatch = (uint32_t)(g.scratch_bytes / (2ull * N * ds.S));
+        if (wbatch < batch) batch = wbatch;
+    }
     if (batch == 0) return hipErrorOutOfMemory;
     for (uint32_t q0 = 0; q0 < ds.count; q0 += batch) {
         Dec16 p{ds, Res{g.perm, g.skew}, logwalsh, g.errs, g.scratch, q0,
@@ -2089,13 +2106,29 @@ static uint32_t ilog2u(uint32_t x) {
     return r;
 }
 
-static hipError_t run_encode_generic(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st) {
-    const uint32_t m = ceil_pow2(cs.k);
+// Byte slabs of the shares: a codeword's work arrays (`per_point` bytes per point and
+// byte of share width) must fit the stream's scratch, so wide shares run as slabs of
+// whole 64-byte blocks (the GF(2^16) symbol layout never crosses one) -- each slab a
+// launch sequence of its own over base + first byte, the strides unchanged.
+static uint32_t g16_slab(uint64_t per_point, uint32_t S, uint64_t scratch) {
+    if (per_point * S <= scratch) return S;
+    return (uint32_t)(scratch / per_point / 64u * 64u);
+}
+
+static hipError_t run_encode_generic(const CodewordSet& cs0, const Gf16Dev& g, hipStream_t st) {
+    const uint32_t m = ceil_pow2(cs0.k);
+    const uint32_t slab = g16_slab(m, cs0.S, g.scratch_bytes);
+    if (slab == 0) return hipErrorOutOfMemory;
+    const G16Groups gr = g16_groups(ilog2u(m));
+    for (uint64_t c0 = 0; c0 < cs0.S; c0 += slab) {
+    CodewordSet cs = cs0;
+    cs.base = cs0.base + c0;
+    cs.out_base = (cs0.out_base ? cs0.out_base : cs0.base) + c0;
+    cs.S = (uint32_t)(cs0.S - c0 < slab ? cs0.S - c0 : slab);
     const uint32_t chunks = (cs.S + 511) / 512;
     const uint64_t per_cw = (uint64_t)m * cs.S;
     const uint32_t batch = (uint32_t)(g.scratch_bytes / per_cw);
     if (batch == 0) return hipErrorOutOfMemory;
-    const G16Groups gr = g16_groups(ilog2u(m));
     for (uint32_t q0 = 0; q0 < cs.count; q0 += batch) {
         G16Pass p{};
         p.cs = cs;
@@ -2129,19 +2162,26 @@ static hipError_t run_encode_generic(const CodewordSet& cs, const Gf16Dev& g, hi
             if ((e = g16_pass(p, 4, 0, 4, st)) != hipSuccess) return e;
         }
     }
+    }
     return hipSuccess;
 }
 
-static hipError_t run_decode_generic(const DecodeSet& ds, const Gf16Dev& g, hipStream_t st) {
-    const uint32_t m = ceil_pow2(ds.k), n = 2 * m;
+static hipError_t run_decode_generic(const DecodeSet& ds0, const Gf16Dev& g, hipStream_t st) {
+    const uint32_t m = ceil_pow2(ds0.k), n = 2 * m;
+    const uint32_t slab = g16_slab(2ull * n, ds0.S, g.scratch_bytes);
+    if (slab == 0) return hipErrorOutOfMemory;
+    const G16Groups gr = g16_groups(ilog2u(n));
+    const uint32_t top = gr.n - 1;
+    for (uint64_t c0 = 0; c0 < ds0.S; c0 += slab) {
+    DecodeSet ds = ds0;
+    ds.base = ds0.base + c0;
+    ds.S = (uint32_t)(ds0.S - c0 < slab ? ds0.S - c0 : slab);
     const uint32_t chunks = (ds.S + 511) / 512;
     const uint64_t per_cw = 2ull * n * ds.S;
     uint32_t batch = (uint32_t)(g.scratch_bytes / per_cw);
     const uint32_t ebatch = (uint32_t)(g.errs_bytes / (n * sizeof(uint16_t)));
     if (ebatch < batch) batch = ebatch;
     if (batch == 0) return hipErrorOutOfMemory;
-    const G16Groups gr = g16_groups(ilog2u(n));
-    const uint32_t top = gr.n - 1;
     for (uint32_t q0 = 0; q0 < ds.count; q0 += batch) {
         G16Pass p{};
         p.ds = ds;
@@ -2151,6 +2191,7 @@ static hipError_t run_decode_generic(const DecodeSet& ds, const Gf16Dev& g, hipS
         p.logwalsh = g.logwalsh;
         p.work = g.scratch;
         p.cw_bytes = per_cw;
+        p.pitch = ds0.pitch ? ds0.pitch : ds0.S;
         p.npts = n;
         p.m = m;
         p.k = ds.k;
@@ -2181,6 +2222,7 @@ static hipError_t run_decode_generic(const DecodeSet& ds, const Gf16Dev& g, hipS
             if ((e = g16_pass(p, gr.bits[i], 0, gr.bits[i], st)) != hipSuccess) return e;
         }
     }
+    }
     return hipSuccess;
 }
 }  // namespace
@@ -2192,6 +2234,7 @@ void set_dec16_diag_mode(uint32_t m) { g_dec16_mode.store(m); }
 #endif
 
 hipError_t launch_encode_gf16(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st) {
+    if (cs.wide) return cs.k <= 32768u ? run_encode_generic(cs, g, st) : hipErrorNotSupported;
     switch (ceil_pow2(cs.k)) {
         case 256: return run_encode<256>(cs, g, st);
         case 512: return run_encode<512>(cs, g, st);
@@ -2200,6 +2243,7 @@ hipError_t launch_encode_gf16(const CodewordSet& cs, const Gf16Dev& g, hipStream
 }
 
 hipError_t launch_decode_gf16(const DecodeSet& ds, const Gf16Dev& g, hipStream_t st) {
+    if (ds.wide) return ds.k <= 32768u ? run_decode_generic(ds, g, st) : hipErrorNotSupported;
     switch (ceil_pow2(ds.k)) {
         case 256: return run_decode<256>(ds, g, g.logwalsh, st);
         case 512: return run_decode<512>(ds, g, g.logwalsh, st);

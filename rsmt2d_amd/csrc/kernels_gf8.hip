@@ -241,6 +241,41 @@ __global__ __launch_bounds__(256, 3) void encode_gf8_kernel(CodewordSet cs) {
     });
 }
 
+// Wide form (codewords whose halves span more than kOffsetLimit: columns of squares
+// over 4 GiB): a 64-bit base per symbol, the same butterflies; a capped grid of
+// one-wave workgroups loops over the tasks (M registers of state per lane).
+template <int M>
+__global__ __launch_bounds__(64) void encode_gf8_wide_kernel(CodewordSet cs) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t chunks = cs.chunks, k = cs.k;
+    const uint32_t tasks = cs.count * chunks;
+    for (uint32_t t = blockIdx.x; t < tasks; t += gridDim.x) {
+        const uint32_t task = __builtin_amdgcn_readfirstlane(t);
+        const uint32_t q = task / chunks;
+        const uint32_t chunk = task - q * chunks;
+        const uint32_t off0 = chunk * 256u + lane * 4u;
+        const uint32_t off = off0 < cs.S ? off0 : kOob;
+        const uint64_t rel = cw_rel(cs, q);
+        uint32_t w[M];
+        static_for<M>([&](auto E) {
+            constexpr int e = decltype(E)::value;
+            w[e] = (uint32_t)e < k ? __builtin_amdgcn_raw_buffer_load_b32(
+                                         make_rsrc(cs.base + rel + (uint64_t)e * cs.elem_stride), off, 0, 0)
+                                   : 0u;
+        });
+        if constexpr (M > 1) {
+            ifft_layers<M, M - 1>(w);
+            fft_layers<M>(w);
+        }
+        static_for<M>([&](auto E) {
+            constexpr int e = decltype(E)::value;
+            if ((uint32_t)e < k)
+                __builtin_amdgcn_raw_buffer_store_b32(
+                    w[e], make_rsrc(cs.out_base + rel + cs.out_offset + (uint64_t)e * cs.elem_stride), off, 0, 0);
+        });
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Decode (reconstruct, recoverAll): fills every missing symbol of the listed
 // codewords in place.  Element e of codeword q: e < k data, k <= e < 2k parity.
@@ -315,13 +350,13 @@ __device__ __forceinline__ void derivative_half(uint32_t (&w)[H]) {
 // transform is run as two m-point halves: layers below m stay inside a half, so
 // only one half lives in registers at a time and the other is parked in LDS
 // (m x 64 dwords, lane-major: conflict-free).
-template <int M>
-__global__ __launch_bounds__(64) void decode_gf8_kernel(DecodeSet ds) {
-    __shared__ uint32_t park[M][64];
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x);
+// Cells: narrow form -- one buffer resource per half of the codeword (data cells
+// e < k, parity cells k + i), 32-bit offsets i * cell_step * S within the half
+// (narrow_fits); WIDE -- a 64-bit base per cell, cells `pitch` bytes apart.
+template <int M, bool WIDE>
+__device__ __forceinline__ void decode_gf8_task(const DecodeSet& ds, uint32_t wave, uint32_t (&park)[M][64]) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t chunks = ds.chunks;
-    if (wave >= ds.count * chunks) return;
     const uint32_t qi = wave / chunks;
     const uint32_t chunk = wave - qi * chunks;
     const uint32_t k = ds.k;
@@ -365,9 +400,22 @@ __global__ __launch_bounds__(64) void decode_gf8_kernel(DecodeSet ds) {
 
     const uint32_t off0 = chunk * 256u + lane * 4u;
     const uint32_t off = off0 < ds.S ? off0 : kOob;
-    const __amdgpu_buffer_rsrc_t rs = make_rsrc(ds.base);
-    auto soff = [&](uint32_t e) -> uint32_t { return pin_sgpr((uint32_t)((cell0 + (uint64_t)e * cell_step) * ds.S)); };
-    auto st = [&](uint32_t e, uint32_t v) { __builtin_amdgcn_raw_buffer_store_b32(v, rs, off, soff(e), 0); };
+    const uint64_t pitch = WIDE && ds.pitch ? ds.pitch : ds.S;
+    const __amdgpu_buffer_rsrc_t rd = make_rsrc(ds.base + cell0 * pitch);                            // data half
+    const __amdgpu_buffer_rsrc_t rp = make_rsrc(ds.base + (cell0 + (uint64_t)k * cell_step) * pitch);  // parity half
+    auto soff = [&](uint32_t i) -> uint32_t { return pin_sgpr((uint32_t)((uint64_t)i * cell_step * ds.S)); };
+    // symbol i of a half (par: parity cell k + i, else data cell i)
+    auto cell_rsrc = [&](uint32_t i, bool par) {
+        return make_rsrc(ds.base + (cell0 + ((par ? (uint64_t)k : 0ull) + i) * cell_step) * pitch);
+    };
+    auto ld = [&](uint32_t i, bool par, bool ok) -> uint32_t {
+        if constexpr (WIDE) return ok ? __builtin_amdgcn_raw_buffer_load_b32(cell_rsrc(i, par), off, 0, 0) : 0u;
+        else return __builtin_amdgcn_raw_buffer_load_b32(par ? rp : rd, off, ok ? soff(i) : kOob, 0);
+    };
+    auto st = [&](uint32_t i, bool par, uint32_t v) {
+        if constexpr (WIDE) __builtin_amdgcn_raw_buffer_store_b32(v, cell_rsrc(i, par), off, 0, 0);
+        else __builtin_amdgcn_raw_buffer_store_b32(v, par ? rp : rd, off, soff(i), 0);
+    };
 
     constexpr unsigned LM = kGf8.skew[M - 1];  // twiddle of the layer joining the halves
     uint32_t w[M];
@@ -375,7 +423,7 @@ __global__ __launch_bounds__(64) void decode_gf8_kernel(DecodeSet ds) {
     // 1. upper half: original data, scaled by the error locator; IFFT layers < M
     static_for<M>([&](auto E) {
         constexpr int e = decltype(E)::value;
-        w[e] = __builtin_amdgcn_raw_buffer_load_b32(rs, off, ((uint32_t)e < k && present(e)) ? soff(e) : kOob, 0);
+        w[e] = ld(e, false, (uint32_t)e < k && present(e));
     });
     static_for<M>([&](auto E) {
         constexpr int e = decltype(E)::value;
@@ -387,7 +435,7 @@ __global__ __launch_bounds__(64) void decode_gf8_kernel(DecodeSet ds) {
     // 2. lower half: recovery (parity) data; IFFT layers < M
     static_for<M>([&](auto E) {
         constexpr int e = decltype(E)::value;
-        w[e] = __builtin_amdgcn_raw_buffer_load_b32(rs, off, ((uint32_t)e < k && present(k + e)) ? soff(k + e) : kOob, 0);
+        w[e] = ld(e, true, (uint32_t)e < k && present(k + e));
     });
     static_for<M>([&](auto E) {
         constexpr int e = decltype(E)::value;
@@ -423,7 +471,7 @@ __global__ __launch_bounds__(64) void decode_gf8_kernel(DecodeSet ds) {
     fft_layers<M, M - 1>(w);
     static_for<M>([&](auto E) {
         constexpr int e = decltype(E)::value;
-        if ((uint32_t)e < k && !present(e)) st(e, gf8_mul_rt(w[e], 255u - err_at(M + e)));
+        if ((uint32_t)e < k && !present(e)) st(e, false, gf8_mul_rt(w[e], 255u - err_at(M + e)));
     });
 
     // 5. lower half: FFT layers < M, reveal missing parity
@@ -431,8 +479,26 @@ __global__ __launch_bounds__(64) void decode_gf8_kernel(DecodeSet ds) {
     fft_layers<M, -1>(w);
     static_for<M>([&](auto E) {
         constexpr int e = decltype(E)::value;
-        if ((uint32_t)e < k && !present(k + e)) st(k + e, gf8_mul_rt(w[e], 255u - err_at(e)));
+        if ((uint32_t)e < k && !present(k + e)) st(e, true, gf8_mul_rt(w[e], 255u - err_at(e)));
     });
+}
+
+template <int M>
+__global__ __launch_bounds__(64) void decode_gf8_kernel(DecodeSet ds) {
+    __shared__ uint32_t park[M][64];
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x);
+    if (wave >= ds.count * ds.chunks) return;
+    decode_gf8_task<M, false>(ds, wave, park);
+}
+
+// wide form: a capped grid of one-wave workgroups loops over the tasks (one wave
+// per workgroup: the LDS park is reused in program order, no barrier needed)
+template <int M>
+__global__ __launch_bounds__(64) void decode_gf8_wide_kernel(DecodeSet ds) {
+    __shared__ uint32_t park[M][64];
+    const uint32_t tasks = ds.count * ds.chunks;
+    for (uint32_t t = blockIdx.x; t < tasks; t += gridDim.x)
+        decode_gf8_task<M, true>(ds, __builtin_amdgcn_readfirstlane(t), park);
 }
 
 // ---------------------------------------------------------------------------
@@ -549,14 +615,16 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
     // first, and the PCIe bytes halve.
     const uint32_t off0 = chunk * 256u + lane * 4u;
     const uint32_t off = off0 < ds.S ? off0 : kOob;
-    const __amdgpu_buffer_rsrc_t rs = make_rsrc(ds.base);
+    // this wave's half of the codeword (parity cells k + i for w < NW/2, data cells i
+    // otherwise) has its own 64-bit base; offsets within it are 32-bit (narrow_fits)
+    const uint64_t hcell = (cell0 + (w < HALF ? (uint64_t)k * cell_step : 0ull)) * ds.S;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(ds.base + hcell);
     const bool mirror = ds.mirror != nullptr;  // rebuilt cells also written there
-    const __amdgpu_buffer_rsrc_t ri = make_rsrc(ZC ? ds.in_base : ds.base);
+    const __amdgpu_buffer_rsrc_t ri = make_rsrc((ZC ? ds.in_base : ds.base) + hcell);
     const uint32_t ib = (w % HALF) * PW;
-    const uint32_t p0 = (w < HALF ? k : 0u) + ib;
     const uint32_t nvalid = ib >= k ? 0u : (k - ib >= (uint32_t)PW ? (uint32_t)PW : k - ib);
-    const uint32_t pbase = (uint32_t)((cell0 + (uint64_t)p0 * cell_step) * ds.S);
     const uint32_t pstep = (uint32_t)(cell_step * ds.S);
+    const uint32_t pbase = ib * pstep;
     const uint64_t valid = nvalid == 64u ? ~0ull : ((1ull << nvalid) - 1ull);
     uint32_t v[PW];
     auto load_points = [&](uint64_t mask) {
@@ -696,7 +764,7 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
     split_low<NW, PW, true>(v, w);
     if constexpr (!ZC) dec_stamp(ds, 6);
     const uint64_t reveal = valid & ~have;
-    const __amdgpu_buffer_rsrc_t rm = make_rsrc(mirror ? ds.mirror : ds.base);
+    const __amdgpu_buffer_rsrc_t rm = make_rsrc((mirror ? ds.mirror : ds.base) + hcell);
     uint32_t sbase = pbase, sstep = pstep;
     asm volatile("" : "+s"(sbase), "+s"(sstep));
     static_for<PW>([&](auto J) {
@@ -945,7 +1013,7 @@ static int split_waves(int launch) {
 #endif
 }
 static void split_set(SplitEncPlan& p, int i, const CodewordSet& c, uint32_t& n) {
-    p.cs[i] = c;
+    p.cs[i] = rebased(c);  // parity from its own base: offsets span one half (narrow_fits)
     p.cs[i].chunks = (c.S + 255) / 256;
     n = p.cs[i].count * p.cs[i].chunks;
 }
@@ -1015,6 +1083,79 @@ hipError_t launch_encode_gf8(const CodewordSet& cs, hipStream_t st) {
         case 128: return launch_enc<128>(cs, st);
         default: return hipErrorInvalidValue;
     }
+}
+
+// Wide forms: one launch per byte slab of the shares (base advanced to the slab's
+// first byte, S = its width; at most 1 GiB, and few enough 256-byte chunks that
+// count * chunks stays a 32-bit task index); a capped grid loops over the tasks.
+constexpr uint32_t kWideGrid = 2048;
+static uint32_t wide_slab(uint32_t count) {
+    uint64_t chunks = (1ull << 31) / (count ? count : 1u);
+    if (chunks > (1u << 22)) chunks = 1u << 22;  // 1 GiB
+    return (uint32_t)(chunks ? chunks : 1u) * 256u;
+}
+template <int M>
+static hipError_t go_enc_wide(const CodewordSet& cs, hipStream_t st) {
+    const uint32_t tasks = cs.count * cs.chunks;
+    hipLaunchKernelGGL(encode_gf8_wide_kernel<M>, dim3(tasks < kWideGrid ? tasks : kWideGrid), dim3(64), 0, st, cs);
+    return hipGetLastError();
+}
+template <int M>
+static hipError_t go_dec_wide(const DecodeSet& ds, hipStream_t st) {
+    const uint32_t tasks = ds.count * ds.chunks;
+    hipLaunchKernelGGL(decode_gf8_wide_kernel<M>, dim3(tasks < kWideGrid ? tasks : kWideGrid), dim3(64), 0, st, ds);
+    return hipGetLastError();
+}
+
+hipError_t launch_encode_gf8_wide(const CodewordSet& cs0, hipStream_t st) {
+    if (cs0.k == 0 || ceil_pow2(cs0.k) > 128 || cs0.count >= (1u << 31)) return hipErrorInvalidValue;
+    const uint32_t slab = wide_slab(cs0.count);
+    for (uint64_t c0 = 0; c0 < cs0.S; c0 += slab) {
+        CodewordSet cs = cs0;
+        cs.base = cs0.base + c0;
+        cs.out_base = (cs0.out_base ? cs0.out_base : cs0.base) + c0;
+        cs.S = (uint32_t)(cs0.S - c0 < slab ? cs0.S - c0 : slab);
+        cs.chunks = (cs.S + 255) / 256;
+        hipError_t e;
+        switch (ceil_pow2(cs.k)) {
+            case 1: e = go_enc_wide<1>(cs, st); break;
+            case 2: e = go_enc_wide<2>(cs, st); break;
+            case 4: e = go_enc_wide<4>(cs, st); break;
+            case 8: e = go_enc_wide<8>(cs, st); break;
+            case 16: e = go_enc_wide<16>(cs, st); break;
+            case 32: e = go_enc_wide<32>(cs, st); break;
+            case 64: e = go_enc_wide<64>(cs, st); break;
+            default: e = go_enc_wide<128>(cs, st); break;
+        }
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+hipError_t launch_decode_gf8_wide(const DecodeSet& ds0, hipStream_t st) {
+    if (ds0.k == 0 || ceil_pow2(ds0.k) > 128 || ds0.in_base || ds0.mirror) return hipErrorInvalidValue;
+    const uint32_t slab = wide_slab(ds0.count);
+    for (uint64_t c0 = 0; c0 < ds0.S; c0 += slab) {
+        DecodeSet ds = ds0;
+        ds.trace = nullptr;
+        ds.base = ds0.base + c0;
+        ds.pitch = ds0.pitch ? ds0.pitch : ds0.S;
+        ds.S = (uint32_t)(ds0.S - c0 < slab ? ds0.S - c0 : slab);
+        ds.chunks = (ds.S + 255) / 256;
+        hipError_t e;
+        switch (ceil_pow2(ds.k)) {
+            case 1: e = go_dec_wide<1>(ds, st); break;
+            case 2: e = go_dec_wide<2>(ds, st); break;
+            case 4: e = go_dec_wide<4>(ds, st); break;
+            case 8: e = go_dec_wide<8>(ds, st); break;
+            case 16: e = go_dec_wide<16>(ds, st); break;
+            case 32: e = go_dec_wide<32>(ds, st); break;
+            case 64: e = go_dec_wide<64>(ds, st); break;
+            default: e = go_dec_wide<128>(ds, st); break;
+        }
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 template <int M>

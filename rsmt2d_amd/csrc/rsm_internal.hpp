@@ -88,6 +88,11 @@ struct rsm_ctx {
     hipStream_t stream = nullptr;
     std::atomic<uint32_t> pass_grid[2] = {0, 0};  // rsm_ctx_set_pass_grid (0 = all CUs)
     std::atomic<uint32_t> split_max{12};           // rsm_ctx_set_split_max
+    // rsm_ctx_set_limits (test hooks; defaults: the kernels' own limits): codeword halves
+    // spanning more than offset_limit bytes take the wide forms, and GF(2^16) work
+    // arrays get at most work_budget bytes per stream (wider shares run as byte slabs)
+    std::atomic<uint64_t> offset_limit{rsm::kOffsetLimit};
+    std::atomic<uint64_t> work_budget{1ull << 30};
 
     // lane pool (Codec calls, host-memory extension)
     static constexpr size_t kMaxLanes = 32;
@@ -139,6 +144,9 @@ int ensure_gf16_tables(rsm_ctx* ctx);
 // between OS threads; the HIP current device is per thread).
 int use_device(rsm_ctx* ctx);
 
+// Whether the single-pass kernels address codewords of k symbols es bytes apart
+// (narrow_fits under the context's offset limit); otherwise the wide forms run.
+bool narrow_ok(const rsm_ctx* ctx, uint64_t k, uint64_t es, uint64_t S);
 int launch_encode(rsm_ctx* ctx, const CodewordSet& cs, hipStream_t st);
 int launch_decode(rsm_ctx* ctx, const DecodeSet& ds, hipStream_t st);
 int extend_squares(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, uint32_t count, hipStream_t st,

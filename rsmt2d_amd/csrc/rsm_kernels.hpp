@@ -34,7 +34,30 @@ struct CodewordSet {
     uint32_t pass;    // 0 = row pass of a square, 1 = column pass / anything else (launch shape)
     uint32_t grid;    // persistent-grid size (workgroups) of the bit-sliced launch: the
                       // context's CU count or its per-pass cap (rsm_ctx_set_pass_grid)
+    uint32_t wide;    // non-zero: symbols addressed with 64-bit per-symbol bases (the
+                      // wide forms; the host sets it when narrow_fits() fails)
 };
+
+// The single-pass kernels address a codeword's symbols with 32-bit buffer offsets
+// from one 64-bit base per codeword half (encoders: the data symbols from the
+// codeword's first cell, the parity from out_base + out_offset; decoders: each half
+// of the 2k cells from its own first cell).  A half of k symbols e * es + byte must
+// stay below kOffsetLimit -- the buffer resources' num_records, also the kernels'
+// out-of-range marker -- so a half may span up to 2 GiB and a square up to 4 GiB;
+// beyond that the wide forms (64-bit per-symbol bases) run instead.
+constexpr uint64_t kOffsetLimit = 1ull << 31;
+__host__ __device__ constexpr bool narrow_fits(uint64_t k, uint64_t es, uint64_t S, uint64_t limit = kOffsetLimit) {
+    return (k + 1) * es + S <= limit;
+}
+
+// Parity addressed from its own base: out_base + out_offset with out_offset = 0
+// (same bytes; the symbol offsets then span one half instead of out_offset + k es).
+__host__ __device__ inline CodewordSet rebased(CodewordSet cs) {
+    if (cs.out_base == nullptr) cs.out_base = cs.base;
+    cs.out_base += cs.out_offset;
+    cs.out_offset = 0;
+    return cs;
+}
 
 // A list of row (axis 0) or column (axis 1) vectors of ONE [W][W][S] square to
 // reconstruct in place; presence is one byte per cell (non-zero = present).
@@ -64,6 +87,12 @@ struct DecodeSet {
     // diagnostic builds only: the upper half of the split decoder's grid issues its
     // point loads `delay` s_memrealtime ticks (100 MHz) after it starts (0 = off)
     uint32_t delay;
+    // wide forms only (64-bit per-cell bases; the host sets `wide` when narrow_fits()
+    // fails): bytes between consecutive cells, 0 = S.  The host runs a share wider
+    // than one launch handles as byte slabs: base advanced by the slab's first byte,
+    // S = the slab's width, pitch = the share size.
+    uint32_t wide;
+    uint64_t pitch;
 };
 constexpr int kDecTraceWords = 8;
 void set_dec_diag_trace(uint32_t* d);
@@ -72,6 +101,13 @@ constexpr int kDec16TraceWords = 16;
 void set_dec_diag_delay(uint32_t ticks);
 
 hipError_t launch_encode_gf8(const CodewordSet& cs, hipStream_t st);
+// wide forms of the byte-table GF(2^8) kernels (any k <= 128): 64-bit per-symbol
+// bases, a capped grid looping over the (codeword, 256-byte chunk) tasks
+hipError_t launch_encode_gf8_wide(const CodewordSet& cs, hipStream_t st);
+hipError_t launch_decode_gf8_wide(const DecodeSet& ds, hipStream_t st);
+// whether the GF(2^16) m <= 512 decoder in use needs per-stream work arrays (only the
+// five-pass diagnostic form does; the single-pass forms keep everything on chip)
+bool dec16_needs_work();
 // bit-sliced M = 128 encode (kernels_gf8_bs.hip); launch_encode_gf8 picks it when applicable
 bool bs128_applicable(const CodewordSet& cs);
 hipError_t launch_encode_gf8_bs128(const CodewordSet& cs, hipStream_t st);

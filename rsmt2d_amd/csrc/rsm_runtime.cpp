@@ -210,48 +210,58 @@ static int gf16_for_stream(rsm_ctx* ctx, StreamScratch& ss, hipStream_t st, uint
     return RSM_OK;
 }
 
-// Work arrays for GF(2^16): all codewords of a launch when that fits in 1 GiB,
-// else 1 GiB worth per batch (the launcher loops).
-static uint64_t gf16_budget(uint64_t per_cw, uint64_t count) {
-    const uint64_t cap = 1ull << 30;
+// Work arrays for GF(2^16): all codewords of a launch when that fits the budget,
+// else a whole number of codewords of the budget per batch (the launcher loops), and
+// at least one codeword's worth -- or, for shares too wide for that, one byte slab's
+// (the launcher slabs the shares: kernels_gf16.hip g16_slab).
+static uint64_t gf16_budget(uint64_t per_cw, uint64_t count, uint64_t cap) {
     const uint64_t want = per_cw * count;
-    return want < cap ? want : (cap / per_cw) * per_cw;
+    if (want <= cap) return want;
+    return per_cw <= cap ? (cap / per_cw) * per_cw : cap;
+}
+
+bool narrow_ok(const rsm_ctx* ctx, uint64_t k, uint64_t es, uint64_t S) {
+    return narrow_fits(k, es, S, ctx->offset_limit.load(std::memory_order_relaxed));
 }
 
 int launch_encode(rsm_ctx* ctx, const CodewordSet& cs0, hipStream_t st) {
-    CodewordSet cs = cs0;
-    if (cs.out_base == nullptr) cs.out_base = cs.base;
+    // parity from its own base (out_base + out_offset): every kernel's symbol offsets
+    // then span one half of the codeword, k symbols es bytes apart (narrow_fits)
+    CodewordSet cs = rebased(cs0);
+    cs.wide = narrow_ok(ctx, cs.k, cs.elem_stride, cs.S) ? 0u : 1u;
     hipError_t e;
-    // the single-pass kernels address a codeword's cells with 32-bit buffer offsets from
-    // its first cell (the multi-pass m >= 1024 path folds them into 64-bit bases)
-    if ((field_bits(cs.k) == 8 || !gf16_generic(cs.k)) &&
-        cs.out_offset + (uint64_t)cs.k * cs.elem_stride + cs.S >= (1ull << 31))
-        return fail(RSM_EUNSUPPORTED, "encode: k=%u with %u-byte shares spans over 2 GiB per codeword", cs.k, cs.S);
     if (field_bits(cs.k) == 8) {
-        cs.chunks = (cs.S + 255) / 256;
-        const uint32_t cap = ctx->pass_grid[cs.pass == 0 ? 0 : 1].load(std::memory_order_relaxed);
-        cs.grid = (cap > 0 && cap < ctx->cus) ? cap : ctx->cus;
-        e = launch_encode_gf8(cs, st);
+        if (cs.wide) {
+            e = launch_encode_gf8_wide(cs, st);
+        } else {
+            cs.chunks = (cs.S + 255) / 256;
+            const uint32_t cap = ctx->pass_grid[cs.pass == 0 ? 0 : 1].load(std::memory_order_relaxed);
+            cs.grid = (cap > 0 && cap < ctx->cus) ? cap : ctx->cus;
+            e = launch_encode_gf8(cs, st);
+        }
     } else {
         if (!gf16_supported(cs.k)) return fail(RSM_EUNSUPPORTED, "encode: k=%u exceeds 32768", cs.k);
-        if ((uint64_t)ceil_pow2(cs.k) * 2 * cs.S >= (1ull << 31))
-            return fail(RSM_EUNSUPPORTED, "encode: k=%u with %u-byte shares exceeds the 2 GiB work-array offsets", cs.k, cs.S);
-        if (!gf16_generic(cs.k)) {
+        if (!gf16_generic(cs.k) && !cs.wide) {
             // single pass per codeword: the tables only, no work arrays
             if (int rc = ensure_gf16_tables(ctx)) return rc;
             Gf16Dev g = ctx->gf16;
             g.cus = ctx->cus;
             e = launch_encode_gf16(cs, g, st);
         } else {
+            // multi-pass through per-stream work arrays, 64-bit per-symbol bases (the
+            // wide form of k <= 512 as well)
+            cs.wide = 1u;
             const uint64_t per_cw = (uint64_t)ceil_pow2(cs.k) * cs.S;
             StreamScratch& ss = stream_scratch(ctx, st);
             std::lock_guard<std::mutex> lk(ss.mu);
             Gf16Dev g;
-            if (int rc = gf16_for_stream(ctx, ss, st, gf16_budget(per_cw, cs.count), 0, &g)) return rc;
+            if (int rc = gf16_for_stream(ctx, ss, st, gf16_budget(per_cw, cs.count, ctx->work_budget.load()), 0, &g))
+                return rc;
             g.cus = ctx->cus;
             e = launch_encode_gf16(cs, g, st);
         }
     }
+    if (e == hipErrorOutOfMemory) return fail(RSM_ENOMEM, "encode: GF(2^16) work arrays below one byte slab");
     if (e != hipSuccess) return hip_fail(e, "encode kernel launch");
     return RSM_OK;
 }
@@ -259,25 +269,47 @@ int launch_encode(rsm_ctx* ctx, const CodewordSet& cs0, hipStream_t st) {
 int launch_decode(rsm_ctx* ctx, const DecodeSet& ds0, hipStream_t st) {
     DecodeSet ds = ds0;
     hipError_t e;
-    // the single-pass decoders address the square's cells with 32-bit buffer offsets
-    if ((field_bits(ds.k) == 8 || !gf16_generic(ds.k)) && 4ull * ds.k * ds.k * ds.S >= (1ull << 31))
-        return fail(RSM_EUNSUPPORTED, "decode: a %ux%u square of %u-byte shares is over 2 GiB", 2 * ds.k, 2 * ds.k, ds.S);
+    // each half of a row / column (its k data or k parity cells) from its own base
+    const uint64_t es = ds.axis == 0 ? (uint64_t)ds.S : 2ull * ds.k * ds.S;
+    ds.wide = narrow_ok(ctx, ds.k, es, ds.S) ? 0u : 1u;
+    // (the five-pass diagnostic GF(2^16) form addresses the whole square with 32-bit offsets)
+    if (field_bits(ds.k) == 16 && dec16_needs_work() && 4ull * ds.k * ds.k * ds.S >= kOffsetLimit) ds.wide = 1u;
+    if (ds.wide && (ds.in_base || ds.mirror))
+        return fail(RSM_EUNSUPPORTED, "decode: zero-copy form of a codeword over the offset limit");
+    if (ds.wide) ds.pitch = ds.S;
     if (field_bits(ds.k) == 8) {
-        ds.chunks = (ds.S + 255) / 256;
-        e = launch_decode_gf8(ds, st);
+        if (ds.wide) {
+            e = launch_decode_gf8_wide(ds, st);
+        } else {
+            ds.chunks = (ds.S + 255) / 256;
+            e = launch_decode_gf8(ds, st);
+        }
     } else {
         if (!gf16_supported(ds.k)) return fail(RSM_EUNSUPPORTED, "decode: k=%u exceeds 32768", ds.k);
-        if ((uint64_t)ceil_pow2(ds.k) * 2 * ds.S >= (1ull << 31))
-            return fail(RSM_EUNSUPPORTED, "decode: k=%u with %u-byte shares exceeds the 2 GiB work-array offsets", ds.k, ds.S);
         const uint64_t n = 2ull * ceil_pow2(ds.k);
-        const uint64_t per_cw = 2ull * n * ds.S;
-        const uint64_t budget = gf16_budget(per_cw, ds.count);
         StreamScratch& ss = stream_scratch(ctx, st);
         std::lock_guard<std::mutex> lk(ss.mu);
         Gf16Dev g;
-        if (int rc = gf16_for_stream(ctx, ss, st, budget, (budget / per_cw) * n * sizeof(uint16_t), &g)) return rc;
+        if (!gf16_generic(ds.k) && !ds.wide && !dec16_needs_work()) {
+            // single pass per codeword: only the error locators of every codeword
+            if (int rc = gf16_for_stream(ctx, ss, st, 0, ds.count * n * sizeof(uint16_t), &g)) return rc;
+        } else {
+            if (gf16_generic(ds.k)) {
+                ds.wide = 1u;
+                ds.pitch = ds.S;
+            }
+            const uint64_t per_cw = 2ull * n * ds.S;
+            const uint64_t budget = gf16_budget(per_cw, ds.count, ctx->work_budget.load());
+            // codewords per batch: of whole shares, or of the byte slab the launcher
+            // cuts when one codeword's arrays exceed the budget (kernels_gf16.hip g16_slab)
+            const uint64_t slab = per_cw <= budget ? ds.S : budget / (2 * n) / 64 * 64;
+            uint64_t cws = slab ? budget / (2 * n * slab) : 1u;
+            if (cws > ds.count) cws = ds.count;
+            if (int rc = gf16_for_stream(ctx, ss, st, budget, (cws ? cws : 1u) * n * sizeof(uint16_t), &g)) return rc;
+        }
         e = launch_decode_gf16(ds, g, st);
     }
+    if (e == hipErrorOutOfMemory) return fail(RSM_ENOMEM, "decode: GF(2^16) work arrays below one byte slab");
     if (e != hipSuccess) return hip_fail(e, "decode kernel launch");
     return RSM_OK;
 }
@@ -361,8 +393,9 @@ int extend_squares_queue(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, u
                          uint32_t delay, uint32_t margin) {
     if (field_bits(k) != 8 || count == 0) return RSM_EUNSUPPORTED;
     QueuePlan p{};
-    p.rows = rows_set(d_eds, k, S, count);
-    p.cols = cols_set(d_eds, k, S, count);
+    // parity from its own base: the symbol offsets span one half (narrow_fits)
+    p.rows = rebased(rows_set(d_eds, k, S, count));
+    p.cols = rebased(cols_set(d_eds, k, S, count));
     // persistent grid: every CU, or the row-pass cap of rsm_ctx_set_pass_grid
     const uint32_t cap = ctx->pass_grid[0].load(std::memory_order_relaxed);
     p.rows.grid = p.cols.grid = cap && cap < ctx->cus ? cap : ctx->cus;
@@ -437,11 +470,14 @@ int extend_squares_split(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, u
 int extend_squares(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, uint32_t count, hipStream_t st,
                    int phases) {
     const uint64_t W = 2ull * k;
-    if (phases == 3 && count <= ctx->split_max.load(std::memory_order_relaxed)) {
+    // the latency and queue forms address the column halves with 32-bit offsets; wider
+    // squares take the two passes below, whose launches pick the wide forms
+    const bool narrow = narrow_ok(ctx, k, W * S, S);
+    if (phases == 3 && narrow && count <= ctx->split_max.load(std::memory_order_relaxed)) {
         const int rc = extend_squares_split(ctx, d_eds, k, S, count, st);
         if (rc != RSM_EUNSUPPORTED) return rc;
     }
-    if (phases == 3) {  // k = 128: one queue-driven launch
+    if (phases == 3 && narrow) {  // k = 128: one queue-driven launch
         const int rc = extend_squares_queue(ctx, d_eds, k, S, count, st);
         if (rc != RSM_EUNSUPPORTED) return rc;
     }
@@ -620,6 +656,14 @@ int rsm_ctx_set_pass_grid(rsm_ctx* ctx, int pass, int cus, int* previous) {
         return fail(RSM_EINVAL, "rsm_ctx_set_pass_grid: pass must be 0 (rows) or 1 (columns), cus >= 0");
     const uint32_t prev = ctx->pass_grid[pass].exchange((uint32_t)cus);
     if (previous) *previous = (int)prev;
+    return RSM_OK;
+}
+
+int rsm_ctx_set_limits(rsm_ctx* ctx, uint64_t offset_limit, uint64_t work_budget) {
+    if (!ctx) return fail(RSM_EINVAL, "rsm_ctx_set_limits: NULL ctx");
+    if (offset_limit > kOffsetLimit) return fail(RSM_EINVAL, "rsm_ctx_set_limits: offset limit above 2^31");
+    ctx->offset_limit.store(offset_limit ? offset_limit : kOffsetLimit);
+    ctx->work_budget.store(work_budget ? work_budget : (1ull << 30));
     return RSM_OK;
 }
 

@@ -148,6 +148,9 @@ hipError_t launch_decode_gf16(const DecodeSet& ds, const Gf16Dev& g, hipStream_t
     touch_decode(ds);
     return hipSuccess;
 }
+hipError_t launch_encode_gf8_wide(const CodewordSet& cs, hipStream_t st) { return launch_encode_gf8(cs, st); }
+hipError_t launch_decode_gf8_wide(const DecodeSet& ds, hipStream_t st) { return launch_decode_gf8(ds, st); }
+bool dec16_needs_work() { return false; }
 bool bs128_applicable(const CodewordSet&) { return false; }
 hipError_t launch_encode_gf8_bs128(const CodewordSet& cs, hipStream_t st) { return launch_encode_gf8(cs, st); }
 bool split_fused_enabled() { return false; }  // the stub runs the two-launch form

@@ -400,27 +400,3 @@ def test_multi_gpu_inplace_pinned_world1(lib, multi, sched):
         assert np.array_equal(eds, oracle.extend_square(ods, nthreads=8))
     finally:
         R._check(lib.rsm_multi_host_free(multi, p))
-
-
-def test_over_2gib_square_refused(lib):
-    """The single-pass kernels address cells with 32-bit buffer offsets: a k = 512 square of
-    2 KiB shares (2 GiB) is refused with RSM_EUNSUPPORTED, not extended or decoded wrongly."""
-    k, S = 512, 2048
-    W = 2 * k
-    ctx = R.device_context()
-    p = ctypes.c_void_p()
-    R._check(lib.rsm_dev_alloc(ctx, W * W * S, ctypes.byref(p)))
-    try:
-        assert lib.rsm_extend_squares_dev(ctx, p.value, k, S, 1, None) == R.RSM_EUNSUPPORTED
-        R._check(lib.rsm_sync(ctx))
-        pres, idx = ctypes.c_void_p(), ctypes.c_void_p()
-        R._check(lib.rsm_dev_alloc(ctx, W * W, ctypes.byref(pres)))
-        R._check(lib.rsm_dev_alloc(ctx, 4 * W, ctypes.byref(idx)))
-        try:
-            assert lib.rsm_decode_vectors_dev(ctx, p.value, pres.value, k, S, 0, idx.value, 1, None) == R.RSM_EUNSUPPORTED
-        finally:
-            R._check(lib.rsm_dev_free(ctx, pres))
-            R._check(lib.rsm_dev_free(ctx, idx))
-    finally:
-        R._check(lib.rsm_sync(ctx))
-        R._check(lib.rsm_dev_free(ctx, p))
