@@ -53,6 +53,10 @@ int rsm_diag_set_dec16_mode(uint32_t mode);
 /* GF(2^8) split decoder A/B: the upper half of the grid delays its point loads by
  * `ticks` of the 100 MHz s_memrealtime clock (0 = off, production). */
 int rsm_diag_set_dec_delay(uint32_t ticks);
+/* GF(2^8) split decoder A/B: 1 = the other error-locator form than production (every
+ * wave computing the locator itself with scalar-loaded tables, or wave 0 staging the
+ * per-point tables in LDS for all waves); 0 = production. */
+int rsm_diag_set_dec8_mode(uint32_t mode);
 /* Both passes of `count` in-place k = 128 squares in ONE persistent launch
  * (extend_gf8_bs128q_kernel: row and Q0-column sets from one queue, Q1-column sets
  * from a ready list; `delay` squares of row sets lead the Q0-column sets).

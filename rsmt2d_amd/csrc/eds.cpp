@@ -506,7 +506,10 @@ int fast_repair_rows_zero_copy(rsm_eds* e, DevSquare& dev, const std::vector<uin
                                const uint8_t* row_roots, const uint8_t* col_roots, const DevTree& dt) {
     const uint32_t W = e->width, k = W / 2;
     const size_t S = e->S, row = (size_t)W * S;
-    if (!e->data.pinned || ceil_pow2(k) != 128 || !narrow_ok(dev.ctx, k, S, S)) return 1;
+    // the zero-copy decoders: GF(2^8) 65 <= k <= 128 (decode_gf8_split_zc_kernel) and the
+    // GF(2^16) single passes, k <= 512 (dec16f_kernel / dec16h_kernel)
+    const bool zc_decoder = field_bits(k) == 8 ? ceil_pow2(k) == 128 : ceil_pow2(k) <= 512;
+    if (!e->data.pinned || !zc_decoder || !narrow_ok(dev.ctx, k, S, S)) return 1;
     void* hmap = nullptr;
     hipError_t r = hipHostGetDevicePointer(&hmap, e->data.data(), 0);
     if (r != hipSuccess || !hmap) {

@@ -1317,7 +1317,10 @@ __device__ __forceinline__ void deriv_plane(uint32_t (&v)[E], uint32_t (*xch)[64
 // (enc16_kernel<256>'s scheme; a scalar table load from L2 per butterfly block left
 // the 16-wave kernels waiting, ~6.6 cycles per VALU instruction): the exchange
 // buffer is half the elements (two passes per plane) so the tables fit beside it.
-template <int M>
+// ZC: the zero-copy form for Repair (DecodeSet in_base / mirror: present cells read
+// from host-mapped memory and stored into the device square too, rebuilt cells written
+// to both)
+template <int M, bool ZC = false>
 __global__ __launch_bounds__(1024, 4) void dec16f_kernel(Dec16 p) {
     constexpr int N = 2 * M, E = 32, R = N / E, WAVES = N / E;
     static_assert(WAVES == 16 && R == 16, "n = 512: 16 waves of 32 elements, residues of 16");
@@ -1350,7 +1353,10 @@ __global__ __launch_bounds__(1024, 4) void dec16f_kernel(Dec16 p) {
     // this wave's half of the codeword (slots e < M: parity shares, waves w < 8; else
     // data) from its own 64-bit base, 32-bit offsets within it (narrow_fits)
     const uint32_t hfirst = w < (uint32_t)WAVES / 2 ? k : 0u, cstep = p.ds.axis == 0 ? 1u : Wd;
-    const auto sq = rsrc(p.ds.base + ((uint64_t)cell(0) + (uint64_t)hfirst * cstep) * S);
+    const uint64_t hbase = ((uint64_t)cell(0) + (uint64_t)hfirst * cstep) * S;
+    const auto sq = rsrc(p.ds.base + hbase);
+    const auto si = rsrc((ZC ? p.ds.in_base : p.ds.base) + hbase);  // present cells
+    const auto sm = rsrc((ZC ? p.ds.mirror : p.ds.base) + hbase);   // rebuilt cells, host copy
     auto hoff = [&](uint32_t s) -> uint32_t { return (s - hfirst) * cstep * S; };
     const uint32_t my_s = lane < (uint32_t)E ? share_of(E * w + lane) : 0xFFFFFFFFu;
     const uint32_t my_p = my_s != 0xFFFFFFFFu ? (uint32_t)p.ds.presence[cell(my_s)] : 0u;
@@ -1362,8 +1368,12 @@ __global__ __launch_bounds__(1024, 4) void dec16f_kernel(Dec16 p) {
         constexpr int i = decltype(I)::value;
         const uint32_t src = share_of(E * w + i);
         const uint32_t so = ((have >> i) & 1u) ? hoff(src) : kOob16;
-        l[i] = ld(sq, ln.lo, so);
-        h[i] = ld(sq, ln.lo + 32, so);
+        l[i] = ld(si, ln.lo, so);
+        h[i] = ld(si, ln.lo + 32, so);
+        if constexpr (ZC) {  // the present cell lands in the device square as well
+            st(sq, l[i], ln.lo, so);
+            st(sq, h[i], ln.lo + 32, so);
+        }
     });
     store_elem_tabs<N, 1024>(etab, etv);
     __syncthreads();  // twiddle and scale tables staged
@@ -1407,6 +1417,10 @@ __global__ __launch_bounds__(1024, 4) void dec16f_kernel(Dec16 p) {
             const uint32_t so = hoff(dst);
             st(sq, l[i], ln.lo, so);
             st(sq, h[i], ln.lo + 32, so);
+            if constexpr (ZC) {
+                st(sm, l[i], ln.lo, so);
+                st(sm, h[i], ln.lo + 32, so);
+            }
         }
     });
     __syncthreads();  // the next task's scale tables reuse the exchange buffer
@@ -1507,7 +1521,7 @@ __device__ __forceinline__ void deriv_halfwave(uint32_t (&v)[R], uint32_t (*x2)[
     });
 }
 
-template <int M>
+template <int M, bool ZC = false>
 __global__ __launch_bounds__(1024, 4) void dec16h_kernel(Dec16 p) {
     constexpr int N = 2 * M, E = 32, G = N / E, R = N / E;
     static_assert(G == 32 && R == 32, "n = 1024: 32 halves of 32 elements, residues of 32");
@@ -1541,7 +1555,10 @@ __global__ __launch_bounds__(1024, 4) void dec16h_kernel(Dec16 p) {
     // this wave's half of the codeword (elements < M: parity shares, waves w < 8; else
     // data) from its own 64-bit base, 32-bit offsets within it (narrow_fits)
     const uint32_t hfirst = w < 8u ? k : 0u, cstep = p.ds.axis == 0 ? 1u : Wd;
-    const auto sq = rsrc(p.ds.base + ((uint64_t)cell(0) + (uint64_t)hfirst * cstep) * S);
+    const uint64_t hbase = ((uint64_t)cell(0) + (uint64_t)hfirst * cstep) * S;
+    const auto sq = rsrc(p.ds.base + hbase);
+    const auto si = rsrc((ZC ? p.ds.in_base : p.ds.base) + hbase);  // present cells
+    const auto sm = rsrc((ZC ? p.ds.mirror : p.ds.base) + hbase);   // rebuilt cells, host copy
     auto hoff = [&](uint32_t s) -> uint32_t { return (s - hfirst) * cstep * S; };
     const uint32_t my_s = share_of(64u * w + lane);
     const uint32_t my_p = my_s != 0xFFFFFFFFu ? (uint32_t)p.ds.presence[cell(my_s)] : 0u;
@@ -1565,8 +1582,12 @@ __global__ __launch_bounds__(1024, 4) void dec16h_kernel(Dec16 p) {
 #ifdef RSM_DIAG
         if (p.diag & 2u) vo = kOob16;  // A/B bit 1: no point loads (wrong output)
 #endif
-        l[i] = ld(sq, vo, 0u);
-        h[i] = ld(sq, vo + 32u, 0u);
+        l[i] = ld(si, vo, 0u);
+        h[i] = ld(si, vo + 32u, 0u);
+        if constexpr (ZC) {  // the present cell lands in the device square as well
+            st(sq, l[i], vo, 0u);
+            st(sq, h[i], vo + 32u, 0u);
+        }
     });
 #ifdef RSM_DIAG
     if (!(p.diag & 1u))
@@ -1638,6 +1659,10 @@ __global__ __launch_bounds__(1024, 4) void dec16h_kernel(Dec16 p) {
             const uint32_t vo = (cc == kOob16 || !lane_ok) ? kOob16 : cc + off;
             st(sq, xl, vo, 0u);
             st(sq, xh, vo + 32u, 0u);
+            if constexpr (ZC) {
+                st(sm, xl, vo, 0u);
+                st(sm, xh, vo + 32u, 0u);
+            }
         }
     });
     d16_stamp(p, 12);
@@ -2008,6 +2033,7 @@ hipError_t run_decode(const DecodeSet& ds, const Gf16Dev& g, const uint16_t* log
         if (wbatch < batch) batch = wbatch;
     }
     if (batch == 0) return hipErrorOutOfMemory;
+    if ((ds.in_base || ds.mirror) && dec16_five_pass()) return hipErrorInvalidValue;  // no zero-copy five passes
     for (uint32_t q0 = 0; q0 < ds.count; q0 += batch) {
         Dec16 p{ds, Res{g.perm, g.skew}, logwalsh, g.errs, g.scratch, q0,
                 ds.count - q0 < batch ? ds.count - q0 : batch, chunks, g.skewperm};
@@ -2019,7 +2045,8 @@ hipError_t run_decode(const DecodeSet& ds, const Gf16Dev& g, const uint16_t* log
                 const uint32_t ch = (ds.S + 255) / 256;
                 Dec16 ph = p;
                 ph.chunks = ch;
-                hipLaunchKernelGGL(dec16h_kernel<M>, dim3(p.count * ch), dim3(1024), 0, st, ph);
+                if (ds.in_base) hipLaunchKernelGGL((dec16h_kernel<M, true>), dim3(p.count * ch), dim3(1024), 0, st, ph);
+                else hipLaunchKernelGGL((dec16h_kernel<M, false>), dim3(p.count * ch), dim3(1024), 0, st, ph);
                 if (hipError_t e = hipGetLastError()) return e;
                 continue;
             }
@@ -2027,7 +2054,9 @@ hipError_t run_decode(const DecodeSet& ds, const Gf16Dev& g, const uint16_t* log
         if constexpr (M == 256) {
             if (!dec16_five_pass()) {  // the single-pass form (diagnostic builds can A/B the five passes)
                 const uint32_t tk = p.count * chunks;
-                hipLaunchKernelGGL(dec16f_kernel<M>, dim3(tk > g.cus ? g.cus : tk), dim3(1024), 0, st, p);
+                const uint32_t grid = tk > g.cus ? g.cus : tk;
+                if (ds.in_base) hipLaunchKernelGGL((dec16f_kernel<M, true>), dim3(grid), dim3(1024), 0, st, p);
+                else hipLaunchKernelGGL((dec16f_kernel<M, false>), dim3(grid), dim3(1024), 0, st, p);
                 if (hipError_t e = hipGetLastError()) return e;
                 continue;
             }

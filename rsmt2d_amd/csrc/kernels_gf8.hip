@@ -590,7 +590,12 @@ __device__ __forceinline__ void dec_stamp(const DecodeSet& ds, int i) {
 #endif
 }
 
-template <int NW, bool ZC>
+// WE ("wave error locator", round 5): every wave computes the error locator itself
+// (the 256-entry FWHT pair, beside the other waves' identical copies) and multiplies
+// its points by tables read with scalar loads (d_perm8, scalar-cache resident), so no
+// wave waits for wave 0's locator, its per-point table resolution or the barrier
+// after it; without WE wave 0 stages the tables in LDS (ptab) for all waves.
+template <int NW, bool ZC, bool WE = false>
 __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t task, uint32_t (&xch)[256][64],
                                                   PermTab (&ptab)[2][256], PermTab (&stab)[257]) {
     constexpr int PW = 256 / NW, HALF = NW / 2;
@@ -650,7 +655,10 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
     uint32_t lw[4] = {0, 0, 0, 0};
     constexpr int kTabWords = 256 * 5 / 64;
     uint32_t sv[kTabWords];
-    if (w == 0) {
+    if constexpr (WE) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) lw[j] = d_gf8.logwalsh[lane * 4u + j];
+    } else if (w == 0) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) lw[j] = d_gf8.logwalsh[lane * 4u + j];
         const uint32_t* tw = reinterpret_cast<const uint32_t*>(&d_perm8.t[0]);
@@ -667,7 +675,7 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
     }
 #endif
     if constexpr (!ZC) load_points(valid);
-    if (w == 0) {
+    if (!WE && w == 0) {
         uint32_t* st = reinterpret_cast<uint32_t*>(&stab[0]);
 #pragma unroll
         for (int i = 0; i < kTabWords; ++i) st[i * 64 + lane] = sv[i];
@@ -686,7 +694,24 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
     // wave 0 alone: it resolves each point's multiply table (ptab: the staged table of
     // exp(err) / exp(-err), so every wave's per-point multiply is ONE uniform LDS read)
     // the staged table of its own points
-    if (w == 0) {
+    uint32_t er_packed = 0;  // (WE) this wave's copy of the locator, 4 entries per lane
+    if constexpr (WE) {
+        uint32_t er[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t i = lane * 4u + j;
+            uint32_t x = 0;
+            if (i < k) x = present(k + i) ? 0u : 1u;
+            else if (i < 128u) x = 1u;
+            else if (i < 128u + k) x = present(i - 128u) ? 0u : 1u;
+            er[j] = x;
+        }
+        fwht256(er, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) er[j] = (er[j] * lw[j]) % 255u;
+        fwht256(er, lane);
+        er_packed = er[0] | (er[1] << 8) | (er[2] << 16) | (er[3] << 24);
+    } else if (w == 0) {
         uint32_t er[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -717,13 +742,18 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
             __builtin_amdgcn_raw_buffer_store_b32(v[j], rs, off, so, 0);
         });
     }
-    __syncthreads();
+    if constexpr (!WE) __syncthreads();
     if constexpr (!ZC) dec_stamp(ds, 2);
+    // (WE) locator entry of point e: byte e & 3 of lane e >> 2 (a wave-uniform readlane)
+    auto err_of = [&](uint32_t e) -> uint32_t {
+        return (__builtin_amdgcn_readlane(er_packed, e >> 2) >> (8u * (e & 3u))) & 255u;
+    };
 
     // 1. S layout: scale every point by the error locator (absent -> 0)
     static_for<PW>([&](auto J) {
         constexpr int j = decltype(J)::value;
-        v[j] = gf8_mul_tab(v[j], ptab[0][PW * w + j]);
+        if constexpr (WE) v[j] = ((have >> j) & 1ull) ? gf8_mul_rt(v[j], err_of(PW * w + j)) : 0u;
+        else v[j] = gf8_mul_tab(v[j], ptab[0][PW * w + j]);
     });
     // 2. IFFT layers 1..PW/2 (per-wave twiddles)
     split_low<NW, PW, false>(v, w);
@@ -771,7 +801,9 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
         constexpr int j = decltype(J)::value;
         const uint32_t e = PW * w + j;
         const uint32_t so = ((reveal >> j) & 1ull) ? sbase + (uint32_t)j * sstep : kOob;
-        const uint32_t x = gf8_mul_tab(v[j], ptab[1][e]);
+        uint32_t x;
+        if constexpr (WE) x = ((reveal >> j) & 1ull) ? gf8_mul_rt(v[j], 255u - err_of(e)) : 0u;
+        else x = gf8_mul_tab(v[j], ptab[1][e]);
         __builtin_amdgcn_raw_buffer_store_b32(x, rs, off, so, 0);
         if (mirror) __builtin_amdgcn_raw_buffer_store_b32(x, rm, off, so, 0);
     });
@@ -781,12 +813,13 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
 constexpr int kSplitWaves = 16;
 
 // one workgroup per task (device-resident square)
-template <int NW>
+template <int NW, bool WE = false>
 __global__ __launch_bounds__(64 * NW, NW / 2) void decode_gf8_split_kernel(DecodeSet ds) {
     __shared__ uint32_t xch[256][64];
-    __shared__ PermTab ptab[2][256];
-    __shared__ PermTab stab[257];
-    decode_split_task<NW, false>(ds, blockIdx.x, xch, ptab, stab);
+    __shared__ PermTab ptab[WE ? 1 : 2][256];  // (unused by WE)
+    __shared__ PermTab stab[WE ? 1 : 257];
+    decode_split_task<NW, false, WE>(ds, blockIdx.x, xch, reinterpret_cast<PermTab (&)[2][256]>(ptab),
+                                     reinterpret_cast<PermTab (&)[257]>(stab));
 }
 
 // zero-copy form: a capped grid loops over the tasks
@@ -1166,6 +1199,16 @@ static hipError_t launch_dec(const DecodeSet& ds, hipStream_t st) {
     return hipGetLastError();
 }
 
+// The split decoder's locator: per wave (WE) or wave 0 + LDS tables (round 4 form).
+constexpr bool kDecWaveErr = false;
+#ifdef RSM_DIAG
+static std::atomic<uint32_t> g_dec8_mode{0};  // 1: the other locator form (A/B)
+void set_dec8_diag_mode(uint32_t m) { g_dec8_mode.store(m); }
+static bool dec8_wave_err() { return g_dec8_mode.load() == 1 ? !kDecWaveErr : kDecWaveErr; }
+#else
+void set_dec8_diag_mode(uint32_t) {}
+static bool dec8_wave_err() { return kDecWaveErr; }
+#endif
 #ifdef RSM_DIAG
 static std::atomic<uint32_t*> g_dec_trace{nullptr};
 static std::atomic<uint32_t> g_dec_delay{0};
@@ -1196,7 +1239,10 @@ hipError_t launch_decode_gf8(const DecodeSet& ds0, hipStream_t st) {
             hipLaunchKernelGGL(decode_gf8_split_zc_kernel<4>, dim3(grid), dim3(256), 0, st, ds);
         } else {
             constexpr int NW = kSplitWaves;
-            hipLaunchKernelGGL(decode_gf8_split_kernel<NW>, dim3((uint32_t)tasks), dim3(64 * NW), 0, st, ds);
+            if (dec8_wave_err())
+                hipLaunchKernelGGL((decode_gf8_split_kernel<NW, true>), dim3((uint32_t)tasks), dim3(64 * NW), 0, st, ds);
+            else
+                hipLaunchKernelGGL((decode_gf8_split_kernel<NW, false>), dim3((uint32_t)tasks), dim3(64 * NW), 0, st, ds);
         }
         return hipGetLastError();
     }

@@ -94,6 +94,11 @@ int rsm_diag_set_dec_delay(uint32_t ticks) {
     return RSM_OK;
 }
 
+int rsm_diag_set_dec8_mode(uint32_t mode) {
+    set_dec8_diag_mode(mode);
+    return RSM_OK;
+}
+
 int rsm_diag_set_bs_row_mode(int mode) {
     set_bs128_diag_row_mode(mode);
     return RSM_OK;

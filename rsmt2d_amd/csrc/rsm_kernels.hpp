@@ -70,10 +70,10 @@ struct DecodeSet {
     uint32_t k;
     uint32_t S;
     uint32_t chunks;
-    // Zero-copy forms (M = 128 split decoder only; both nullable): `in_base` (a
-    // host-mapped copy of the square): read the present cells from there instead of
-    // `base` and store them into `base` as well; `mirror`: write every rebuilt cell
-    // there too.
+    // Zero-copy forms (the M = 128 split decoder and the GF(2^16) single-pass decoders;
+    // both nullable): `in_base` (a host-mapped copy of the square): read the present
+    // cells from there instead of `base` and store them into `base` as well; `mirror`:
+    // write every rebuilt cell there too.
     const uint8_t* in_base;
     uint8_t* mirror;
     // Workgroups of the M = 128 split decoder (0: one per task).  A smaller grid
@@ -99,6 +99,7 @@ void set_dec_diag_trace(uint32_t* d);
 uint32_t* dec_diag_trace_ptr();  // (diagnostic builds; the GF(2^16) single-pass decoders stamp kDec16TraceWords)
 constexpr int kDec16TraceWords = 16;
 void set_dec_diag_delay(uint32_t ticks);
+void set_dec8_diag_mode(uint32_t mode);  // diagnostic builds only: 1 = the other split-decoder locator form
 
 hipError_t launch_encode_gf8(const CodewordSet& cs, hipStream_t st);
 // wide forms of the byte-table GF(2^8) kernels (any k <= 128): 64-bit per-symbol

@@ -83,10 +83,12 @@ int extend_sharded(rsm_multi* m, uint8_t* const* d_eds, uint32_t k, uint32_t S, 
                 return hip_fail(e, "hipMalloc (all-to-all staging)");
             uint8_t* snd = static_cast<uint8_t*>(m->pack[0][g].ptr);
             const uint8_t* mine = d_eds[g] + (size_t)g * rk * row;
-            for (int h = 0; h < G; ++h)
+            for (int h = 0; h < G; ++h) {
+                if (h == g) continue;  // GPU g's own block stays where its column pass reads it
                 if ((e = hipMemcpy2DAsync(snd + h * blk, (size_t)ck * S, mine + (size_t)h * ck * S, row, (size_t)ck * S, rk,
                                           hipMemcpyDeviceToDevice, m->ctx[g]->stream)) != hipSuccess)
                     return hip_fail(e, "all-to-all pack");
+            }
         }
         if ((r = ncclGroupStart()) != ncclSuccess) return nccl_fail(r, "ncclGroupStart");
         for (int g = 0; g < G && r == ncclSuccess; ++g) {

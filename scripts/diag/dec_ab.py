@@ -2,8 +2,9 @@
 erased, BenchmarkRepair), S = 512, decoded by rsm_decode_vectors_dev:
   k = 256, 200 (GF(2^16), m = 256): the single-pass decoder (dec16f_kernel,
           production) or the five global passes (rsm_diag_set_dec16_five_pass);
-  k = 128 (GF(2^8) split decoder): the upper half of the grid delays its point loads by
-          DECAB_DELAYS ticks of the 100 MHz clock (rsm_diag_set_dec_delay; 0 = production).
+  k = 128 (GF(2^8) split decoder): DECAB_V8 variants -- 0 production, 1 the other
+          error-locator form (rsm_diag_set_dec8_mode), 100 + t the upper half of the grid
+          delaying its point loads by t ticks of the 100 MHz clock (rsm_diag_set_dec_delay).
 DECAB_KS picks the k values (default 256,200); DECAB_V16 the GF(2^16) variants (0 production,
 1 the five passes, other values rsm_diag_set_dec16_mode bits).  Every rebuilt square compared with the original EDS.  One JSON line per configuration.
 usage: python3 scripts/diag/dec_ab.py"""
@@ -57,9 +58,12 @@ def main():
             chk(D.rsm_diag_set_dec16_five_pass(1 if v == 1 else 0))
             chk(D.rsm_diag_set_dec16_mode(0 if v == 1 else v))
             return 0
-        setter = set16 if k > 128 else D.rsm_diag_set_dec_delay
+        def set8(v):  # DECAB_V8: 0 production, 1 the other locator form, >= 100: load delay v - 100 ticks
+            chk(D.rsm_diag_set_dec8_mode(v if v < 100 else 0))
+            return D.rsm_diag_set_dec_delay(v - 100 if v >= 100 else 0)
+        setter = set16 if k > 128 else set8
         variants = ([int(x) for x in os.environ.get("DECAB_V16", "0,1").split(",")] if k > 128
-                    else [int(x) for x in os.environ.get("DECAB_DELAYS", "0,150,300,450").split(",")])
+                    else [int(x) for x in os.environ.get("DECAB_V8", "0,1").split(",")])
         for rep in range(2):
             for five in variants:
                 chk(setter(five))
@@ -74,7 +78,7 @@ def main():
                     chk(D.rsm_decode_vectors_dev(ctx, buf.value, pres.value, k, S, 0, idx.value, W, None))
                 chk(D.rsm_sync(ctx))
                 dt = (time.perf_counter() - t0) / reps
-                print(json.dumps({"k": k, "S": S, ("delay_ticks" if k <= 128 else "five_pass"): five, "rep": rep,
+                print(json.dumps({"k": k, "S": S, ("variant" if k <= 128 else "five_pass"): five, "rep": rep,
                                   "sweep_ms": round(dt * 1e3, 4),
                                   "frac": round(W * W * S / dt / 8e12, 4), "rebuilt_equal": bool(eq.value)}),
                       flush=True)

@@ -22,6 +22,21 @@ for s in ${STEPS:-smoke tests}; do
     pmc) step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE -d "$PWD/$OUT/pmc_fetch" -o run --output-format csv -- python3 bench.py --headline-only --steps 3 --warmup 1 || exit 8
          step pmc_write 300 rocprofv3 --pmc WRITE_SIZE -d "$PWD/$OUT/pmc_write" -o run --output-format csv -- python3 bench.py --headline-only --steps 3 --warmup 1 || exit 9
          python3 scripts/pmc_summary.py $OUT/pmc_fetch $OUT/pmc_write $OUT/pmc_latest.json > $OUT/pmc_summary.log 2>&1 ;;
+    gf16pmc)  # counters of the production GF(2^16) encoders (c4 k=256 S=2048, c5 k=512 S=512)
+         i=0
+         for C in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_ACTIVE_INST_VALU" \
+                  "SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_SCA" \
+                  "SQ_INST_LEVEL_VMEM SQ_INSTS_SMEM SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM_RD GRBM_GUI_ACTIVE GRBM_COUNT"; do
+           i=$((i+1))
+           step gf16_sq$i 120 rocprofv3 --pmc $C -d "$PWD/$OUT/gf16_sq$i" -o run --output-format csv -- python3 scripts/diag/run_gf16.py 3 || exit 10
+         done
+         step gf16_fetch 120 rocprofv3 --pmc FETCH_SIZE -d "$PWD/$OUT/gf16_fetch" -o run --output-format csv -- python3 scripts/diag/run_gf16.py 3 || exit 11
+         step gf16_write 120 rocprofv3 --pmc WRITE_SIZE -d "$PWD/$OUT/gf16_write" -o run --output-format csv -- python3 scripts/diag/run_gf16.py 3 || exit 12
+         step gf16_stats 120 rocprofv3 --kernel-trace --stats -d "$PWD/$OUT/gf16_prof" -o run --output-format csv -- python3 scripts/diag/run_gf16.py 20 || exit 13
+         python3 scripts/sq_summary.py $OUT/gf16_sq.json $OUT/gf16_sq1 $OUT/gf16_sq2 $OUT/gf16_sq3 > $OUT/gf16_sq_summary.log 2>&1
+         python3 scripts/pmc_summary.py $OUT/gf16_fetch $OUT/gf16_write $OUT/gf16_pmc.json > $OUT/gf16_pmc_summary.log 2>&1 ;;
+    decab) DECAB_KS=${DECAB_KS:-128,256,512} DECAB_V8=${DECAB_V8:-0,1} DECAB_V16=${DECAB_V16:-0} \
+             step decab 300 python3 scripts/diag/dec_ab.py || exit 14 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
