@@ -537,7 +537,12 @@ def bench_c5(world, rank, local, dist, steps, L, R):
     out = {"workload": "c5: 512x512->1024x1024 square, 512 B shares, GF(2^16)"
                        + ("" if world == 1 else f", rows sharded over {world} GPUs + RCCL all-to-all of column slices"),
            "n_gpus": world, "ms_per_square": round(dt * 1e3, 4), "ods_GiB_s": round(k * k * S / dt / 2**30, 3),
-           "scaling": "strong (one square)"}
+           "scaling": "strong (one square)",
+           "frac": round(4 * k * k * S / dt / 1e9 / HBM_PEAK_GBS, 4)}
+    if world == 1:
+        tr = gf16_square_traffic("enc16h512_kernel")
+        if tr:
+            out["traffic"] = tr
     if dist is None:
         out["c_abi"] = multi
     if dist is not None:
@@ -762,6 +767,19 @@ def bench_small_squares(local, L, R, S=512, ks=(4, 8, 16, 32, 64)):
                     "stream); batch = 1 GiB of EDS per call; frac = 4 k^2 S per square / time / 8 TB/s"}
 
 
+def gf16_square_traffic(kernel):
+    """HBM bytes per square of the GF(2^16) encoder `kernel` (row + column launch) from the
+    committed counter passes (profiles/r05d_gf16_enc_pmc.json: rocprofv3 --pmc FETCH_SIZE /
+    WRITE_SIZE over scripts/diag/run_gf16.py, one square per call: c4 for enc16h_kernel, c5
+    for enc16h512_kernel), or None when the file lacks the kernel."""
+    try:
+        rows = json.load(open(os.path.join(ROOT, "profiles", "r05d_gf16_enc_pmc.json")))["launches"]
+    except (OSError, ValueError, KeyError):
+        return None
+    t = [r["traffic_bytes"] for r in rows if f"::{kernel}<" in r["kernel"]]
+    return {"traffic_bytes_per_square": round(sum(t)), "source": "profiles/r05d_gf16_enc_pmc.json"} if len(t) == 2 else None
+
+
 def bench_c4(local, L, R, steps, B=2, k=256, S=2048):
     """Config 4: 256x256 -> 512x512 squares of 2048 B shares (GF(2^16), enc16h_kernel: m = 256),
     device-resident, B squares (1 GiB of EDS) per step, steps alternating over two
@@ -800,7 +818,9 @@ def bench_c4(local, L, R, steps, B=2, k=256, S=2048):
     for b in bufs:
         b.free()
     algo = 4 * k * k * S * B
-    return {"workload": (f"{'c4: ' if (k, S) == (256, 2048) else ''}{k}x{k}->{W}x{W} squares, {S} B shares, "
+    tr = gf16_square_traffic("enc16h_kernel") if (k, S) == (256, 2048) else None
+    return {**({"traffic": tr} if tr else {}),
+            "workload": (f"{'c4: ' if (k, S) == (256, 2048) else ''}{k}x{k}->{W}x{W} squares, {S} B shares, "
                          "GF(2^16)"), "squares_per_step": B,
             "ms_per_square": round(dt / B * 1e3, 4), "ods_GiB_s": round(k * k * S * B / dt / 2**30, 3),
             "frac": round(algo / dt / 1e9 / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_square": 4 * k * k * S,
