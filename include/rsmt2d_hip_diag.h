@@ -41,8 +41,10 @@ int rsm_diag_set_split_fused(int on);
  * persistent, LDS tables beside a half exchange buffer, 5 = form 4 with just-in-time
  * table reads, 8 / 9 = forms 4 / 5 with the merged middle pair, 16 = the half-wave form
  * with compiler-scheduled table reads.  m = 256: 6 = 16 waves x 16 elements, 7 = 8 waves
- * x 32 elements, 14 = the half-wave form with compiler-scheduled reads, any other value
- * the production half-wave form. */
+ * x 32 elements, 14 = the half-wave form with compiler-scheduled reads, 19 = the half-wave
+ * form prefetching the next task's points, 20 = the half-wave form with three workgroups per
+ * CU (quarter-lane exchange passes, 49 KiB of LDS, 80 registers), any other value the
+ * production half-wave form. */
 int rsm_diag_set_enc16_e64(int mode);
 /* GF(2^16) m = 256 / 512 decoders: 1 = the five global passes (A/B), 0 = the single-pass kernels
  * (production: dec16f_kernel for m = 256, the half-wave dec16h_kernel for m = 512). */

@@ -734,12 +734,37 @@ __device__ __forceinline__ void xch_halfwave(uint32_t (&v)[E], uint32_t (*xch)[3
     __syncthreads();
 }
 
+// The group <-> residue exchange of enc16h_body through an [M][XL] buffer: XL = 32 moves
+// a whole half per pass (xch_halfwave), XL = 8 a quarter of its lanes per pass (four
+// passes, a quarter of the LDS).
+template <int E, int XL>
+__device__ __forceinline__ void xch_part(uint32_t (&v)[E], uint32_t (*xch)[XL], uint32_t g, uint32_t l32, bool to_res) {
+    const uint32_t ls = l32 % XL, sub = l32 / XL;
+    sfor<32 / XL>([&](auto Pc) {
+        constexpr uint32_t pp = decltype(Pc)::value;
+        if (sub == pp)
+            sfor<E>([&](auto I) {
+                constexpr int i = decltype(I)::value;
+                xch[to_res ? E * g + i : g + E * i][ls] = v[i];
+            });
+        __syncthreads();
+        if (sub == pp)
+            sfor<E>([&](auto I) {
+                constexpr int i = decltype(I)::value;
+                v[i] = xch[to_res ? g + E * i : E * g + i][ls];
+            });
+        __syncthreads();
+    });
+}
+
 // PF: the next task's points are loaded while the current one transforms
-template <bool JIT, bool PF = false>
-__global__ __launch_bounds__(512, 4) void enc16h_kernel(Enc16 p) {
+// XL: lanes per exchange pass (32: production, two workgroups per CU; 8: the 49 KiB form,
+// enc16h3_kernel, three workgroups per CU at 80 registers)
+template <bool JIT, bool PF, int XL>
+__device__ __forceinline__ void enc16h_body(const Enc16& p) {
     constexpr int M = 256, E = 16, G = 16, R = 16, THREADS = 512;
     constexpr int GT = G * (E - 1) * kTabW;
-    __shared__ uint32_t xch[M][32];
+    __shared__ uint32_t xch[M][XL];
     __shared__ uint32_t tabs[2 * GT + 2 * (R - 1) * kTabW];
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
     const uint32_t hh = lane >> 5, l32 = lane & 31u, g = 2u * w + hh;
@@ -792,13 +817,13 @@ __global__ __launch_bounds__(512, 4) void enc16h_kernel(Enc16 p) {
             load_task(task, l, h);
         }
         grp_xform<E, false, JIT>(l, h, tI);
-        xch_halfwave<E>(l, xch, g, l32, true);
-        xch_halfwave<E>(h, xch, g, l32, true);
+        xch_part<E, XL>(l, xch, g, l32, true);
+        xch_part<E, XL>(h, xch, g, l32, true);
         res_xform<E, R, false, true, JIT>(l, h, rtab);
         res_mid<E, R>(l, h, p.mid);
         res_xform<E, R, true, true, JIT>(l, h, rtab);
-        xch_halfwave<E>(l, xch, g, l32, false);
-        xch_halfwave<E>(h, xch, g, l32, false);
+        xch_part<E, XL>(l, xch, g, l32, false);
+        xch_part<E, XL>(h, xch, g, l32, false);
         grp_xform<E, true, JIT>(l, h, tF);
         const auto out = rsrc(p.cs.out_base + rel);
         sfor<E>([&](auto I) {
@@ -809,6 +834,15 @@ __global__ __launch_bounds__(512, 4) void enc16h_kernel(Enc16 p) {
             st(out, h[i], v + 32u, so);
         });
     }
+}
+
+template <bool JIT, bool PF = false>
+__global__ __launch_bounds__(512, 4) void enc16h_kernel(Enc16 p) {
+    enc16h_body<JIT, PF, 32>(p);
+}
+// three workgroups per CU: 6 waves per SIMD (80 registers), 49 KiB of LDS each
+__global__ __launch_bounds__(512, 6) void enc16h3_kernel(Enc16 p) {
+    enc16h_body<true, false, 8>(p);
 }
 
 // Half-wave form of the m = 512 encoder (round 4): one task per (codeword, 256-byte
@@ -1993,7 +2027,9 @@ hipError_t run_encode(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st) {
             const uint64_t th = (uint64_t)cs.count * ph.chunks;
             if (th >= (1ull << 31)) return hipErrorInvalidValue;
             const uint32_t gh = th > 2ull * g.cus ? 2u * g.cus : (uint32_t)th;
-            if (form == 19) hipLaunchKernelGGL((enc16h_kernel<true, true>), dim3(gh), dim3(512), 0, st, ph);
+            const uint32_t gh3 = th > 3ull * g.cus ? 3u * g.cus : (uint32_t)th;
+            if (form == 20) hipLaunchKernelGGL(enc16h3_kernel, dim3(gh3), dim3(512), 0, st, ph);
+            else if (form == 19) hipLaunchKernelGGL((enc16h_kernel<true, true>), dim3(gh), dim3(512), 0, st, ph);
             else if (form == 14) hipLaunchKernelGGL(enc16h_kernel<false>, dim3(gh), dim3(512), 0, st, ph);
             else hipLaunchKernelGGL(enc16h_kernel<true>, dim3(gh), dim3(512), 0, st, ph);
             return hipGetLastError();

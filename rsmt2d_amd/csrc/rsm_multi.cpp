@@ -59,9 +59,10 @@ int extend_sharded(rsm_multi* m, uint8_t* const* d_eds, uint32_t k, uint32_t S, 
             if (hipError_t e = hipEventRecord(rows_done[g], m->ctx[g]->stream)) return hip_fail(e, "hipEventRecord");
         }
     }
-    // 2. exchange
+    // 2. exchange (one GPU: its rows are the whole top half already)
     ncclResult_t r;
-    if (schedule == RSM_SCHED_ALLGATHER) {
+    if (G == 1) {
+    } else if (schedule == RSM_SCHED_ALLGATHER) {
         if ((r = ncclGroupStart()) != ncclSuccess) return nccl_fail(r, "ncclGroupStart");
         for (int g = 0; g < G; ++g) {
             uint8_t* top = d_eds[g];

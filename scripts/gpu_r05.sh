@@ -37,6 +37,8 @@ for s in ${STEPS:-smoke tests}; do
          python3 scripts/pmc_summary.py $OUT/gf16_fetch $OUT/gf16_write $OUT/gf16_pmc.json > $OUT/gf16_pmc_summary.log 2>&1 ;;
     decab) DECAB_KS=${DECAB_KS:-128,256,512} DECAB_V8=${DECAB_V8:-0,1} DECAB_V16=${DECAB_V16:-0} \
              step decab 300 python3 scripts/diag/dec_ab.py || exit 14 ;;
+    gf16ab) GF16AB_FORMS=${GF16AB_FORMS:-0} GF16AB_C4FORMS=${GF16AB_C4FORMS:-0,20} GF16AB_REPS=${GF16AB_REPS:-3} \
+             step gf16ab 300 python3 scripts/diag/gf16_ab.py || exit 15 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
