@@ -59,6 +59,11 @@ int rsm_diag_set_dec_delay(uint32_t ticks);
  * wave computing the locator itself with scalar-loaded tables, or wave 0 staging the
  * per-point tables in LDS for all waves); 0 = production. */
 int rsm_diag_set_dec8_mode(uint32_t mode);
+/* Repair's zero-copy first sweep: 0 = production (one zero-copy decoder kernel that
+ * both reads present cells and writes rebuilt cells over PCIe), 1 = the split transport
+ * (a gather kernel on a loader stream reads present cells chunk by chunk while the
+ * device decoder of the previous chunk writes rebuilt cells back; measured slower). */
+int rsm_diag_set_repair_mode(int mode);
 /* Both passes of `count` in-place k = 128 squares in ONE persistent launch
  * (extend_gf8_bs128q_kernel: row and Q0-column sets from one queue, Q1-column sets
  * from a ready list; `delay` squares of row sets lead the Q0-column sets).

@@ -1390,7 +1390,8 @@ __global__ __launch_bounds__(1024, 4) void dec16f_kernel(Dec16 p) {
     const uint64_t hbase = ((uint64_t)cell(0) + (uint64_t)hfirst * cstep) * S;
     const auto sq = rsrc(p.ds.base + hbase);
     const auto si = rsrc((ZC ? p.ds.in_base : p.ds.base) + hbase);  // present cells
-    const auto sm = rsrc((ZC ? p.ds.mirror : p.ds.base) + hbase);   // rebuilt cells, host copy
+    const bool mirror = p.ds.mirror != nullptr;                       // rebuilt cells also written there
+    const auto sm = rsrc((mirror ? p.ds.mirror : p.ds.base) + hbase);
     auto hoff = [&](uint32_t s) -> uint32_t { return (s - hfirst) * cstep * S; };
     const uint32_t my_s = lane < (uint32_t)E ? share_of(E * w + lane) : 0xFFFFFFFFu;
     const uint32_t my_p = my_s != 0xFFFFFFFFu ? (uint32_t)p.ds.presence[cell(my_s)] : 0u;
@@ -1451,7 +1452,7 @@ __global__ __launch_bounds__(1024, 4) void dec16f_kernel(Dec16 p) {
             const uint32_t so = hoff(dst);
             st(sq, l[i], ln.lo, so);
             st(sq, h[i], ln.lo + 32, so);
-            if constexpr (ZC) {
+            if (mirror) {
                 st(sm, l[i], ln.lo, so);
                 st(sm, h[i], ln.lo + 32, so);
             }
@@ -1592,7 +1593,8 @@ __global__ __launch_bounds__(1024, 4) void dec16h_kernel(Dec16 p) {
     const uint64_t hbase = ((uint64_t)cell(0) + (uint64_t)hfirst * cstep) * S;
     const auto sq = rsrc(p.ds.base + hbase);
     const auto si = rsrc((ZC ? p.ds.in_base : p.ds.base) + hbase);  // present cells
-    const auto sm = rsrc((ZC ? p.ds.mirror : p.ds.base) + hbase);   // rebuilt cells, host copy
+    const bool mirror = p.ds.mirror != nullptr;                       // rebuilt cells also written there
+    const auto sm = rsrc((mirror ? p.ds.mirror : p.ds.base) + hbase);
     auto hoff = [&](uint32_t s) -> uint32_t { return (s - hfirst) * cstep * S; };
     const uint32_t my_s = share_of(64u * w + lane);
     const uint32_t my_p = my_s != 0xFFFFFFFFu ? (uint32_t)p.ds.presence[cell(my_s)] : 0u;
@@ -1693,7 +1695,7 @@ __global__ __launch_bounds__(1024, 4) void dec16h_kernel(Dec16 p) {
             const uint32_t vo = (cc == kOob16 || !lane_ok) ? kOob16 : cc + off;
             st(sq, xl, vo, 0u);
             st(sq, xh, vo + 32u, 0u);
-            if constexpr (ZC) {
+            if (mirror) {
                 st(sm, xl, vo, 0u);
                 st(sm, xh, vo + 32u, 0u);
             }

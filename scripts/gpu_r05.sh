@@ -39,6 +39,8 @@ for s in ${STEPS:-smoke tests}; do
              step decab 300 python3 scripts/diag/dec_ab.py || exit 14 ;;
     gf16ab) GF16AB_FORMS=${GF16AB_FORMS:-0} GF16AB_C4FORMS=${GF16AB_C4FORMS:-0,20} GF16AB_REPS=${GF16AB_REPS:-3} \
              step gf16ab 300 python3 scripts/diag/gf16_ab.py || exit 15 ;;
+    repairtrace) step repair_trace 300 rocprofv3 --kernel-trace --memory-copy-trace -d "$PWD/$OUT/rtrace" -o run --output-format csv -- python3 scripts/diag/repair_trace.py ${RT_REPS:-6} || exit 16 ;;
+    repab) step repair_ab 400 python3 scripts/diag/repair_ab.py || exit 17 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
