@@ -17,6 +17,7 @@
 #include <atomic>
 #include <cmath>
 #include <cstring>
+#include <memory>
 #include <thread>
 #include <vector>
 
@@ -583,20 +584,25 @@ int fast_repair_rows_zero_copy(rsm_eds* e, DevSquare& dev, const std::vector<uin
     // measured 75 GB/s for that pattern against ~56-58 for one kernel doing both) -- but
     // slower end to end here (see repair_split_transport).
     const bool split_transport = repair_split_transport();
-    LaneGuard gl(dev.ctx);
-    if (!gl.lane) return gl.rc;
-    hipStream_t sl = gl.lane->stream;
-    hipEvent_t evl[3];
-    for (auto& x : evl) (void)hipEventCreateWithFlags(&x, hipEventDisableTiming);
+    std::unique_ptr<LaneGuard> gl;
+    hipStream_t sl = nullptr;
+    hipEvent_t evl[3] = {};
     struct EvGuard3 {
         hipEvent_t* e;
         ~EvGuard3() {
-            for (int c = 0; c < 3; ++c) (void)hipEventDestroy(e[c]);
+            for (int c = 0; c < 3; ++c)
+                if (e[c]) (void)hipEventDestroy(e[c]);
         }
     } evg3{evl};
-    // the loader's gathers read the presence and index uploads queued on st
-    (void)hipEventRecord(evl[2], st);
-    (void)hipStreamWaitEvent(sl, evl[2], 0);
+    if (split_transport) {
+        gl = std::make_unique<LaneGuard>(dev.ctx);
+        if (!gl->lane) return gl->rc;
+        sl = gl->lane->stream;
+        for (auto& x : evl) (void)hipEventCreateWithFlags(&x, hipEventDisableTiming);
+        // the loader's gathers read the presence and index uploads queued on st
+        (void)hipEventRecord(evl[2], st);
+        (void)hipStreamWaitEvent(sl, evl[2], 0);
+    }
     uint32_t nchunk = 0;
     auto sweep = [&](size_t t0, size_t t1) -> int {
         if (t1 <= t0) return RSM_OK;
