@@ -351,6 +351,12 @@ template <int NS>
 __host__ __device__ constexpr uint32_t wnode_words() { return 2 * WNode<NS>::kW + 8; }
 template <int NS>
 __host__ __device__ constexpr uint32_t wtree_lds_words(uint32_t W) { return ((W + 1) / 2) * wnode_words<NS>(); }
+// one wave's LDS: its trees, then a spare node that lanes past a level's last node
+// store to (so every lane hashes: see the level loops)
+template <int NS>
+__host__ __device__ constexpr uint32_t wwave_lds_words(uint32_t W, uint32_t tpw) {
+    return tpw * wtree_lds_words<NS>(W) + wnode_words<NS>();
+}
 constexpr uint32_t kNmtTreesPerBlock = 4;  // one wave per tree group
 
 template <int NS, int TPW>
@@ -367,8 +373,9 @@ __global__ __launch_bounds__(256) void nmt_tree_wave_kernel(const uint32_t* __re
     roots += (uint64_t)blockIdx.y * 2 * W * (2 * NS + 32);
     if (status) status += (uint64_t)blockIdx.y * 2 * W;
     extern __shared__ uint32_t lds_raw[];
-    uint32_t* const base = lds_raw + (size_t)wv * TPW * wtree_lds_words<NS>(W);
+    uint32_t* const base = lds_raw + (size_t)wv * wwave_lds_words<NS>(W, TPW);
     auto lvl = [&](uint32_t u) { return base + (size_t)u * wtree_lds_words<NS>(W); };
+    uint32_t* const spare = base + (size_t)TPW * wtree_lds_words<NS>(W);
     const bool ig = ignore_max != 0;
     auto leaf_at = [&](uint32_t tree, uint32_t pos, WNode<NS>& n) {
         const uint32_t axis = tree >= W ? 1u : 0u, idx = tree - axis * W;
@@ -408,8 +415,16 @@ __global__ __launch_bounds__(256) void nmt_tree_wave_kernel(const uint32_t* __re
     };
     uint32_t bad = 0;  // bit u: tree u of this wave failed (push order / sibling order)
     // level 1 from the leaf records (push order checked on every consecutive pair)
+    // Every lane hashes in every pass of a level: past the level's last node a lane
+    // repeats node v0 + lane % rem and stores it to the wave's spare node (a wave
+    // with <= 8 lanes active runs its SHA rounds 2-3.5x slower per compression:
+    // kernels_sha.hip; the store keeps the compiler from shrinking the hash to the
+    // owning lanes).
     uint32_t cnt = W, next = (W + 1) / 2;
-    for (uint32_t v = lane; v < nt * next; v += 64u) {
+    for (uint32_t v0 = 0; v0 < nt * next; v0 += 64u) {
+        const uint32_t rem = nt * next - v0;
+        const bool own = lane < rem;
+        const uint32_t v = v0 + (own ? lane : lane % rem);
         const uint32_t u = v / next, j = v - u * next;
         WNode<NS> a, b, o;
         leaf_at(t0 + u, 2 * j, a);
@@ -426,24 +441,27 @@ __global__ __launch_bounds__(256) void nmt_tree_wave_kernel(const uint32_t* __re
         } else {
             o = a;
         }
-        st(lvl(u) + (size_t)j * NW, o);
-        if (!ok) bad |= 1u << u;
+        st(own ? lvl(u) + (size_t)j * NW : spare, o);
+        if (own && !ok) bad |= 1u << u;
     }
     wave_sync();
     for (cnt = next; cnt > 1; cnt = next) {
         next = (cnt + 1) / 2;
-        for (uint32_t v = lane; v < nt * next; v += 64u) {
+        for (uint32_t v0 = 0; v0 < nt * next; v0 += 64u) {
+            const uint32_t rem = nt * next - v0;
+            const bool own = lane < rem;
+            const uint32_t v = v0 + (own ? lane : lane % rem);
             const uint32_t u = v / next, j = v - u * next;
             WNode<NS> a, b, o;
             ld(lvl(u) + (size_t)(2 * j) * NW, a);
             if (2 * j + 1 < cnt) {
                 ld(lvl(u) + (size_t)(2 * j + 1) * NW, b);
-                if (!hash_node_w<NS>(a, b, ig, o)) bad |= 1u << u;
+                if (!hash_node_w<NS>(a, b, ig, o) && own) bad |= 1u << u;
             } else {
                 o = a;
             }
             wave_sync();  // every lane's reads of this level before any write (j < 2j)
-            st(lvl(u) + (size_t)j * NW, o);
+            st(own ? lvl(u) + (size_t)j * NW : spare, o);
         }
         wave_sync();
     }
@@ -471,7 +489,7 @@ __global__ __launch_bounds__(256) void nmt_tree_wave_kernel(const uint32_t* __re
 template <int NS>
 inline uint32_t nmt_trees_per_wave(uint32_t W) {
     for (uint32_t t = 4; t > 1; t >>= 1)
-        if ((size_t)kNmtTreesPerBlock * t * wtree_lds_words<NS>(W) * 4u <= 52u * 1024u) return t;
+        if ((size_t)kNmtTreesPerBlock * wwave_lds_words<NS>(W, t) * 4u <= 52u * 1024u) return t;
     return 1;
 }
 template <int NS>
@@ -479,7 +497,7 @@ hipError_t launch_nmt_tree_wave(const uint32_t* d_leaf, uint32_t W, uint32_t ign
                                 uint32_t* d_status, uint32_t squares, hipStream_t st) {
     const uint32_t tpw = nmt_trees_per_wave<NS>(W);
     const uint32_t blocks = (2 * W + kNmtTreesPerBlock * tpw - 1) / (kNmtTreesPerBlock * tpw);
-    const size_t lds = (size_t)kNmtTreesPerBlock * tpw * wtree_lds_words<NS>(W) * 4u;
+    const size_t lds = (size_t)kNmtTreesPerBlock * wwave_lds_words<NS>(W, tpw) * 4u;
     switch (tpw) {
         case 4: hipLaunchKernelGGL((nmt_tree_wave_kernel<NS, 4>), dim3(blocks, squares), dim3(256), lds, st, d_leaf, W, ignore_max, d_roots, d_status); break;
         case 2: hipLaunchKernelGGL((nmt_tree_wave_kernel<NS, 2>), dim3(blocks, squares), dim3(256), lds, st, d_leaf, W, ignore_max, d_roots, d_status); break;
@@ -504,7 +522,7 @@ hipError_t launch_nmt_roots(const uint8_t* d_eds, uint32_t W, uint32_t S, uint32
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     // Celestia's namespace size: the wave-per-tree kernel (its LDS permitting)
-    if (ns == 29 && (size_t)kNmtTreesPerBlock * wtree_lds_words<29>(W) * 4u <= kLdsCap)
+    if (ns == 29 && (size_t)kNmtTreesPerBlock * wwave_lds_words<29>(W, 1) * 4u <= kLdsCap)
         return launch_nmt_tree_wave<29>(d_leaf, W, ignore_max, d_roots, d_status, squares, st);
     const size_t lds = tree_lds_bytes(W, ns);
     hipLaunchKernelGGL(nmt_tree_kernel, dim3(2 * W, squares), dim3(256), lds, st, d_leaf, W, ns, ignore_max, d_roots,

@@ -130,8 +130,18 @@ __global__ __launch_bounds__(256) void tree_root_kernel(const uint32_t* __restri
         for (int i = 0; i < 8; ++i) sub(lane)[i] = d[i];
     }
     for (uint32_t hgt = 1; (n >> hgt) > 0; ++hgt) {
-        const uint32_t cnt = n >> hgt;
-        for (uint32_t v = lane; v < nt * cnt; v += 64u) {
+        const uint32_t cnt = n >> hgt, tot = nt * cnt;
+        for (uint32_t v0 = 0; v0 < tot; v0 += 64u) {
+            // Every lane hashes: past the level's last node a lane repeats node
+            // v0 + lane % rem and stores it to the tree's spare slot (sub slot 15:
+            // heights stay below 12), so the compiler cannot shrink the hash to the
+            // owning lanes.  A wave with <= 8 of its lanes active runs its SHA
+            // rounds 2-3.5x slower per compression than a full wave
+            // (profiles/r05j_sha_lanes.txt), and a tree's upper levels have 1-8
+            // nodes.
+            const uint32_t rem = tot - v0;
+            const bool own = lane < rem;
+            const uint32_t v = v0 + (own ? lane : lane % rem);
             const uint32_t u = v / cnt, j = v - u * cnt;
             uint32_t L[8], R[8], o[8];
             if (hgt == 1) {
@@ -146,20 +156,21 @@ __global__ __launch_bounds__(256) void tree_root_kernel(const uint32_t* __restri
                 }
             }
             node_hash(L, R, o);
-            uint32_t* lv = lvl(u);
+            uint32_t* dst = own ? lvl(u) + j * 8u : sub(u) + 15u * 8u;
 #pragma unroll
-            for (int i = 0; i < 8; ++i) lv[j * 8u + i] = o[i];
-            if (((n >> hgt) & 1u) && j == cnt - 1) {
+            for (int i = 0; i < 8; ++i) dst[i] = o[i];
+            if (own && ((n >> hgt) & 1u) && j == cnt - 1) {
 #pragma unroll
                 for (int i = 0; i < 8; ++i) sub(u)[hgt * 8u + i] = o[i];
             }
         }
         wave_sync();
     }
-    if (lane < nt) {
-        const uint32_t tree = t0 + first + lane;
+    {  // fold the carried subtrees (a W that is not a power of two); all lanes, as above
+        const uint32_t ul = lane % nt;
+        const uint32_t tree = t0 + first + ul;
         const uint32_t axis = tree >= W ? 1u : 0u, idx = tree - axis * W;
-        const uint32_t* sb = sub(lane);
+        const uint32_t* sb = sub(ul);
         uint32_t acc[8];
         const int lo = __builtin_ctz(n);
 #pragma unroll
@@ -173,22 +184,31 @@ __global__ __launch_bounds__(256) void tree_root_kernel(const uint32_t* __restri
 #pragma unroll
             for (int i = 0; i < 8; ++i) acc[i] = o[i];
         }
-        uint32_t* r = reinterpret_cast<uint32_t*>(roots + ((uint64_t)axis * W + idx) * 32u);
+        if (lane < nt) {
+            uint32_t* r = reinterpret_cast<uint32_t*>(roots + ((uint64_t)axis * W + idx) * 32u);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) r[i] = __builtin_bswap32(acc[i]);
+            for (int i = 0; i < 8; ++i) r[i] = __builtin_bswap32(acc[i]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) sub(ul)[15u * 8u + i] = acc[i];  // keeps every lane hashing
+        }
     }
 }
 
 // trees per wave: as many as keep four waves' LDS within a third of the CU (so
-// three workgroups share it), at least one
+// three workgroups share it), at least one.  A latency launch (one square's 2W
+// trees, too few waves to fill the chip) takes one tree per wave: a lone wave's
+// compressions run back to back, so the launch time is the tree depth in
+// compressions per lane -- at W = 256, 18 (two level-1 nodes per lane, then one
+// per level) against 24 at two trees per wave.
 inline uint32_t trees_per_wave(uint32_t W) {
     for (uint32_t t = 4; t > 1; t >>= 1)
         if ((size_t)kTreesPerBlock * t * tree_lds_words(W) * 4u <= 52u * 1024u) return t;
     return 1;
 }
 hipError_t launch_tree_kernel(const uint32_t* d_leaf, uint32_t W, uint8_t* d_roots, uint32_t first, uint32_t count,
-                              uint32_t squares, hipStream_t st) {
-    const uint32_t tpw = trees_per_wave(W);
+                              uint32_t squares, bool latency, hipStream_t st) {
+    const uint32_t tpw = latency ? 1u : trees_per_wave(W);
     const uint32_t blocks = (count + kTreesPerBlock * tpw - 1) / (kTreesPerBlock * tpw);
     const size_t lds = (size_t)kTreesPerBlock * tpw * tree_lds_words(W) * 4u;
     switch (tpw) {
@@ -212,7 +232,7 @@ hipError_t launch_roots(const uint8_t* d_eds, uint32_t W, uint32_t S, uint32_t s
     hipLaunchKernelGGL(leaf_hash_kernel, dim3((cells + 255) / 256), dim3(256), 0, st, d_eds, cells, S, d_leaf);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    return launch_tree_kernel(d_leaf, W, d_roots, 0u, 2 * W, squares, st);
+    return launch_tree_kernel(d_leaf, W, d_roots, 0u, 2 * W, squares, squares == 1, st);
 }
 
 // Pieces of launch_roots for one square, so a caller can hash rows as they become
@@ -227,7 +247,7 @@ hipError_t launch_leaf_hashes(const uint8_t* d_cells, uint32_t cells, uint32_t S
 hipError_t launch_tree_roots(const uint32_t* d_leaf, uint32_t W, uint32_t first, uint32_t count, uint8_t* d_roots,
                              hipStream_t st) {
     if (count == 0) return hipSuccess;
-    return launch_tree_kernel(d_leaf, W, d_roots, first, count, 1, st);
+    return launch_tree_kernel(d_leaf, W, d_roots, first, count, 1, true, st);
 }
 
 }  // namespace rsm
