@@ -212,6 +212,79 @@ def test_random_byzantine_8x8_matches_oracle(lib, rng):
         assert got == want, trial
 
 
+def _oracle_repair_keep(flat, rr, cr):
+    """oracle crossword.repair, returning ("ok" | "unrepairable" | (axis, index, shares),
+    the square's cells afterwards): the reference leaves the cells it solved in place
+    when it gives up (extendeddatacrossword.go:74-122)."""
+    sq = crossword.Square(list(flat))
+    try:
+        crossword.pre_repair_sanity_check(sq, rr, cr)
+        while True:
+            solved, progress = True, False
+            for i in range(sq.w):
+                s1, p1 = crossword.solve_vector(sq, crossword.Row, i, rr, cr)
+                s2, p2 = crossword.solve_vector(sq, crossword.Col, i, cr, rr)
+                solved = solved and s1 and s2
+                progress = progress or p1 or p2
+            if solved:
+                return "ok", sq.flattened()
+            if not progress:
+                return "unrepairable", sq.flattened()
+    except crossword.Byzantine as b:
+        return (b.axis, b.index, b.shares), sq.flattened()
+
+
+def test_err_rand_byzantine_incremental(lib, rng):
+    """TestErrRandByzantine's protocol (extendeddatacrossword_test.go:612-744): one
+    random share of a k = 8 square replaced (its first 29 bytes kept), set first into an
+    empty square, then random cells of the corrupted square one at a time with a Repair
+    after each, until Repair reports ErrByzantineData -- whose index must be the
+    corrupted cell's row or column (checkErrByzantine).  Every Repair's outcome and the
+    cells it leaves behind (solved cells stay when it gives up) are compared with the
+    oracle crossword on the same cells."""
+    k, W = 8, 16
+    for trial in range(12):
+        ods = [rng.integers(0, 256, S, dtype=np.uint8).tobytes() for _ in range(k * k)]
+        original = R.ComputeExtendedDataSquare(ods, R.NewLeoRSCodec(), R.NewDefaultTree)
+        flat = original.Flattened()
+        idx = int(rng.integers(len(flat)))
+        bad = bytearray(rng.integers(0, 256, S, dtype=np.uint8).tobytes())
+        bad[:29] = flat[idx][:29]
+        flat[idx] = bytes(bad)
+        corrupted = R.ImportExtendedDataSquare(flat, R.NewLeoRSCodec(), R.NewDefaultTree)
+        assert not original.Equals(corrupted)
+        rr, cr = corrupted.RowRoots(), corrupted.ColRoots()
+        square = R.NewExtendedDataSquare(R.NewLeoRSCodec(), R.NewDefaultTree, W, S)
+        cx, cy = divmod(idx, W)
+        square.SetCell(cx, cy, corrupted.GetCell(cx, cy))
+        byz = None
+        for step in range(40 * W * W):
+            x, y = int(rng.integers(W)), int(rng.integers(W))
+            if square.GetCell(x, y) is not None:
+                continue
+            square.SetCell(x, y, corrupted.GetCell(x, y))
+            before = square.Flattened()
+            want, after = _oracle_repair_keep(before, rr, cr)
+            try:
+                square.Repair(rr, cr)
+                got = "ok"
+            except R.ErrByzantineData as b:
+                got = (b.Axis, b.Index, b.Shares)
+            except R.RSMError as e:
+                assert e is R.ErrUnrepairableDataSquare
+                got = "unrepairable"
+            assert got == want, (trial, step)
+            assert got != "ok", "no byzantine error"  # repairNewFromCorrupted
+            if got == "unrepairable":
+                assert square.Flattened() == after, (trial, step)
+                continue
+            byz = got
+            break
+        assert byz is not None
+        axis, index, _ = byz
+        assert index == (cx if axis == R.Row else cy)  # checkErrByzantine
+
+
 @pytest.mark.parametrize("k", [16, 128])
 def test_repair_half_of_each_row(lib, rng, k):
     """BenchmarkRepair's erasure scheme (extendeddatacrossword_test.go:443-453):
