@@ -10,6 +10,7 @@
 // go.mod dependency absent from /root/reference) as rsmt2d's NMT wrappers push it
 // (nmtwrapper_test.go:94-120, nmtbuffered_tree_test.go:118-152): see
 // rsm_nmt_tree_root below; the device form is kernels_nmt.hip.
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
 #include <vector>
@@ -76,6 +77,52 @@ __attribute__((target("sha,sse4.1,ssse3"))) void sha256_block_ni(uint32_t h[8], 
     _mm_storeu_si128(reinterpret_cast<__m128i*>(h + 4), s1);
 }
 const bool kShaNi = cpu_has_sha_ni();
+
+// N independent compressions interleaved (multi-buffer SHA-NI): one message's
+// sha256rnds2 chain is latency-bound, N independent chains keep the SHA unit busy.
+// Same rounds as sha256_block_ni, per state.
+template <int N>
+__attribute__((target("sha,sse4.1,ssse3"))) void sha256_blocks_ni(uint32_t (*h)[8], const uint8_t* const* p) {
+    const __m128i bswap = _mm_set_epi64x(0x0c0d0e0f08090a0bLL, 0x0405060700010203LL);
+    __m128i s0[N], s1[N], abef[N], cdgh[N], w[N][4];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const __m128i t = _mm_shuffle_epi32(_mm_loadu_si128(reinterpret_cast<const __m128i*>(h[i])), 0xB1);
+        const __m128i u = _mm_shuffle_epi32(_mm_loadu_si128(reinterpret_cast<const __m128i*>(h[i] + 4)), 0x1B);
+        s0[i] = _mm_alignr_epi8(t, u, 8);
+        s1[i] = _mm_blend_epi16(u, t, 0xF0);
+        abef[i] = s0[i];
+        cdgh[i] = s1[i];
+    }
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+        const __m128i kg = _mm_load_si128(reinterpret_cast<const __m128i*>(kShaK + 4 * g));
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            __m128i m;
+            if (g < 4) {
+                m = _mm_shuffle_epi8(_mm_loadu_si128(reinterpret_cast<const __m128i*>(p[i] + 16 * g)), bswap);
+            } else {
+                m = _mm_sha256msg1_epu32(w[i][g & 3], w[i][(g + 1) & 3]);
+                m = _mm_add_epi32(m, _mm_alignr_epi8(w[i][(g + 3) & 3], w[i][(g + 2) & 3], 4));
+                m = _mm_sha256msg2_epu32(m, w[i][(g + 3) & 3]);
+            }
+            w[i][g & 3] = m;
+            const __m128i wk = _mm_add_epi32(m, kg);
+            s1[i] = _mm_sha256rnds2_epu32(s1[i], s0[i], wk);
+            s0[i] = _mm_sha256rnds2_epu32(s0[i], s1[i], _mm_shuffle_epi32(wk, 0x0E));
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const __m128i a = _mm_add_epi32(s0[i], abef[i]);
+        const __m128i c = _mm_add_epi32(s1[i], cdgh[i]);
+        const __m128i t = _mm_shuffle_epi32(a, 0x1B);  // FEBA
+        const __m128i u = _mm_shuffle_epi32(c, 0xB1);  // DCHG
+        _mm_storeu_si128(reinterpret_cast<__m128i*>(h[i]), _mm_blend_epi16(t, u, 0xF0));      // DCBA
+        _mm_storeu_si128(reinterpret_cast<__m128i*>(h[i] + 4), _mm_alignr_epi8(u, t, 8));     // HGFE
+    }
+}
 #endif
 
 struct Sha256 {
@@ -154,15 +201,6 @@ constexpr uint32_t Sha256::K[64];
 
 struct Digest { uint8_t b[32]; };
 
-Digest leaf_hash(const uint8_t* d, uint32_t n) {
-    Sha256 s;
-    uint8_t pre = 0x00;
-    s.update(&pre, 1);
-    s.update(d, n);
-    Digest o;
-    s.final(o.b);
-    return o;
-}
 Digest node_hash(const Digest& l, const Digest& r) {
     Sha256 s;
     uint8_t pre = 0x01;
@@ -172,6 +210,59 @@ Digest node_hash(const Digest& l, const Digest& r) {
     Digest o;
     s.final(o.b);
     return o;
+}
+
+// SHA-256 of prefix || msg[i][0, len) for `count` <= kHashBatch messages of one length,
+// compressed side by side (sha256_blocks_ni<kHashBatch>; the scalar Sha256 without the
+// SHA extensions).  Block b of a message is assembled in a 64-byte buffer: the 1-byte
+// prefix shifts the payload off the block grid.  Eight at a time: one DefaultTree root
+// of 256 leaves x 512 B on the GPU box's EPYC 9575F takes 55.8 us against 77 at four
+// and 121 one message at a time (profiles/r05p_host_tree.txt).
+constexpr int kHashBatch = 8;
+void hash_prefixed(uint8_t prefix, const uint8_t* const* msg, int count, uint32_t len, Digest* out) {
+#if defined(__x86_64__)
+    if (kShaNi) {
+        const uint64_t total = 1ull + len, bits = total * 8;
+        const uint64_t nblk = (total + 8) / 64 + 1;
+        uint32_t h[kHashBatch][8];
+        static constexpr uint32_t H0[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                                           0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+        for (auto& x : h) memcpy(x, H0, sizeof(H0));
+        alignas(16) uint8_t buf[kHashBatch][64];
+        const uint8_t* bp[kHashBatch];
+        for (int i = 0; i < kHashBatch; ++i) bp[i] = buf[i];
+        for (uint64_t b = 0; b < nblk; ++b) {
+            const uint64_t t0 = 64 * b;  // message bytes [t0, t0 + 64) of prefix || payload || padding
+            for (int i = 0; i < kHashBatch; ++i) {
+                const uint8_t* m = msg[i < count ? i : count - 1];
+                uint8_t* d = buf[i];
+                memset(d, 0, 64);
+                // payload byte j sits at message position 1 + j
+                const uint64_t lo = t0 > 0 ? t0 - 1 : 0, hi = std::min<uint64_t>(t0 + 63, len);
+                if (hi > lo) memcpy(d + (1 + lo - t0), m + lo, hi - lo);
+                if (t0 == 0) d[0] = prefix;
+                if (total >= t0 && total < t0 + 64) d[total - t0] = 0x80;
+                if (b == nblk - 1)
+                    for (int q = 0; q < 8; ++q) d[56 + q] = (uint8_t)(bits >> (56 - 8 * q));
+            }
+            sha256_blocks_ni<kHashBatch>(h, bp);
+        }
+        for (int i = 0; i < count; ++i)
+            for (int q = 0; q < 8; ++q) {
+                out[i].b[4 * q] = (uint8_t)(h[i][q] >> 24);
+                out[i].b[4 * q + 1] = (uint8_t)(h[i][q] >> 16);
+                out[i].b[4 * q + 2] = (uint8_t)(h[i][q] >> 8);
+                out[i].b[4 * q + 3] = (uint8_t)h[i][q];
+            }
+        return;
+    }
+#endif
+    for (int i = 0; i < count; ++i) {
+        Sha256 s;
+        s.update(&prefix, 1);
+        s.update(msg[i], len);
+        s.final(out[i].b);
+    }
 }
 
 // ---- namespaced Merkle tree (celestiaorg/nmt v0.24.3, published algorithm) ----
@@ -271,20 +362,38 @@ extern "C" int rsm_default_tree_root(void* /*user*/, int /*axis*/, uint32_t /*in
         *root_len = 0;
         return RSM_OK;
     }
-    struct Sub { Digest d; int height; };
-    std::vector<Sub> stack;
-    stack.reserve(40);
-    for (uint32_t i = 0; i < n_leaves; ++i) {
+    for (uint32_t i = 0; i < n_leaves; ++i)
         if (!leaves[i]) return RSM_ETREE;
-        Sub cur{leaf_hash(leaves[i], leaf_size), 0};
-        while (!stack.empty() && stack.back().height == cur.height) {
-            cur = Sub{node_hash(stack.back().d, cur.d), cur.height + 1};
-            stack.pop_back();
+    // The push/join stack ends as the perfect subtrees of the set bits of n (largest
+    // first) folded from the newest: root = node(sub_0, node(sub_1, ... sub_last)).
+    // Leaves, then each subtree's levels, are hashed kHashBatch messages at a time.
+    std::vector<Digest> d(n_leaves);
+    for (uint32_t i = 0; i < n_leaves; i += kHashBatch)
+        hash_prefixed(0x00, leaves + i, (int)std::min<uint32_t>(kHashBatch, n_leaves - i), leaf_size, &d[i]);
+    std::vector<Digest> subs;
+    std::vector<uint8_t> pairs;
+    for (uint32_t s0 = 0, bit = 31; s0 < n_leaves; --bit) {
+        const uint32_t size = 1u << bit;
+        if (!(n_leaves & size)) continue;
+        for (uint32_t cnt = size; cnt > 1; cnt /= 2) {  // level by level, in place in d[s0 ..)
+            const uint32_t np = cnt / 2;
+            pairs.resize((size_t)np * 64);
+            for (uint32_t j = 0; j < np; ++j) {
+                memcpy(&pairs[(size_t)j * 64], d[s0 + 2 * j].b, 32);
+                memcpy(&pairs[(size_t)j * 64 + 32], d[s0 + 2 * j + 1].b, 32);
+            }
+            for (uint32_t j = 0; j < np; j += kHashBatch) {
+                const uint8_t* m[kHashBatch];
+                const int c = (int)std::min<uint32_t>(kHashBatch, np - j);
+                for (int q = 0; q < c; ++q) m[q] = &pairs[(size_t)(j + q) * 64];
+                hash_prefixed(0x01, m, c, 64, &d[s0 + j]);
+            }
         }
-        stack.push_back(cur);
+        subs.push_back(d[s0]);
+        s0 += size;
     }
-    Digest acc = stack.back().d;
-    for (int i = (int)stack.size() - 2; i >= 0; --i) acc = node_hash(stack[i].d, acc);
+    Digest acc = subs.back();
+    for (int i = (int)subs.size() - 2; i >= 0; --i) acc = node_hash(subs[i], acc);
     memcpy(root_out, acc.b, 32);
     *root_len = 32;
     return RSM_OK;

@@ -4,6 +4,7 @@ matches the reference semantics.  No compute call runs without a GPU."""
 import os
 import re
 
+import numpy as np
 import pytest
 
 import rsmt2d_amd as R
@@ -82,6 +83,15 @@ def test_shape_errors(lib):
 @pytest.mark.parametrize("n", [1, 2, 3, 4, 5, 7, 8, 13, 16, 70])
 def test_default_tree_matches_restatement(lib, rng, n):
     leaves = rand_shares(rng, n, 64)
+    assert R._default_root(leaves) == crossword.merkle_root(leaves)
+
+
+@pytest.mark.parametrize("n,size", [(9, 1), (17, 55), (33, 56), (256, 512), (257, 119), (100, 575)])
+def test_default_tree_batched_hashing(lib, rng, n, size):
+    """merkle.cpp hashes leaves and nodes eight messages at a time (multi-buffer
+    SHA-NI): ragged batches, odd lengths and every padding boundary (a 1-byte prefix
+    plus 55 / 56 payload bytes: the length field in the same block or the next)."""
+    leaves = [rng.integers(0, 256, size, dtype=np.uint8).tobytes() for _ in range(n)]
     assert R._default_root(leaves) == crossword.merkle_root(leaves)
 
 
