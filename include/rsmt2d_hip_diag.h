@@ -59,6 +59,9 @@ int rsm_diag_set_dec_delay(uint32_t ticks);
  * wave computing the locator itself with scalar-loaded tables, or wave 0 staging the
  * per-point tables in LDS for all waves); 0 = production. */
 int rsm_diag_set_dec8_mode(uint32_t mode);
+/* Codec calls (rsm_encode / rsm_decode) spin on hipStreamQuery for up to `us`
+ * microseconds before blocking in hipStreamSynchronize (0: block at once, production). */
+int rsm_diag_set_codec_spin(uint32_t us);
 /* Repair's zero-copy first sweep: 0 = production (one zero-copy decoder kernel that
  * both reads present cells and writes rebuilt cells over PCIe), 1 = the split transport
  * (a gather kernel on a loader stream reads present cells chunk by chunk while the

@@ -99,6 +99,11 @@ int rsm_diag_set_dec8_mode(uint32_t mode) {
     return RSM_OK;
 }
 
+int rsm_diag_set_codec_spin(uint32_t us) {
+    set_codec_spin_diag(us);
+    return RSM_OK;
+}
+
 int rsm_diag_set_bs_row_mode(int mode) {
     set_bs128_diag_row_mode(mode);
     return RSM_OK;

@@ -100,6 +100,7 @@ uint32_t* dec_diag_trace_ptr();  // (diagnostic builds; the GF(2^16) single-pass
 constexpr int kDec16TraceWords = 16;
 void set_dec_diag_delay(uint32_t ticks);
 void set_dec8_diag_mode(uint32_t mode);  // diagnostic builds only: 1 = the other split-decoder locator form
+void set_codec_spin_diag(uint32_t us);  // diagnostic builds only (rsm_runtime.cpp)
 
 hipError_t launch_encode_gf8(const CodewordSet& cs, hipStream_t st);
 // wide forms of the byte-table GF(2^8) kernels (any k <= 128): 64-bit per-symbol

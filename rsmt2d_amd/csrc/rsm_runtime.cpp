@@ -16,6 +16,7 @@
 #include "rsm_internal.hpp"
 
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -592,6 +593,27 @@ static void fill_q0(const uint8_t* ods, uint8_t* eds, uint32_t k, uint32_t S) {
     for (uint32_t r = 0; r < k; ++r) memcpy(eds + r * row, ods + r * half, half);
 }
 
+// Completion wait of a Codec call's lane.  Diagnostic builds may spin on
+// hipStreamQuery for up to `codec_spin_us` before blocking (A/B of the wake-up
+// latency of hipStreamSynchronize for ~20 us calls).
+#ifdef RSM_DIAG
+static std::atomic<uint32_t> g_codec_spin_us{0};
+void set_codec_spin_diag(uint32_t us) { g_codec_spin_us.store(us); }
+static uint32_t codec_spin_us() { return g_codec_spin_us.load(); }
+#else
+static uint32_t codec_spin_us() { return 0; }
+#endif
+static hipError_t lane_wait(hipStream_t s) {
+    if (const uint32_t spin = codec_spin_us()) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (;;) {
+            const hipError_t q = hipStreamQuery(s);
+            if (q != hipErrorNotReady) return q;
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin)) break;
+        }
+    }
+    return hipStreamSynchronize(s);
+}
 }  // namespace rsm
 
 using namespace rsm;
@@ -735,7 +757,7 @@ int rsm_encode(rsm_ctx* ctx, const uint8_t* const* data, uint32_t k, uint32_t sh
             } else if (int rc = launch_encode(ctx, cs, L.stream)) {
                 return rc;
             }
-            if ((e = hipStreamSynchronize(L.stream)) != hipSuccess) return hip_fail(e, "encode");
+            if ((e = lane_wait(L.stream)) != hipSuccess) return hip_fail(e, "encode");
             for (uint32_t i = 0; i < k; ++i) memcpy(parity[i], h + (k + i) * S, S);
             return RSM_OK;
         }
@@ -754,7 +776,7 @@ int rsm_encode(rsm_ctx* ctx, const uint8_t* const* data, uint32_t k, uint32_t sh
     if (int rc = launch_encode(ctx, cs, L.stream)) return rc;
     if ((e = hipMemcpyAsync(h + k * S, d + k * S, k * S, hipMemcpyDeviceToHost, L.stream)) != hipSuccess)
         return hip_fail(e, "hipMemcpyAsync D2H");
-    if ((e = hipStreamSynchronize(L.stream)) != hipSuccess) return hip_fail(e, "encode");
+    if ((e = lane_wait(L.stream)) != hipSuccess) return hip_fail(e, "encode");
     for (uint32_t i = 0; i < k; ++i) memcpy(parity[i], h + (k + i) * S, S);
     return RSM_OK;
 }
@@ -801,7 +823,7 @@ int rsm_decode(rsm_ctx* ctx, uint8_t* const* shares, const uint8_t* present, uin
             ds.k = k;
             ds.S = share_size;
             if (int rc = launch_decode(ctx, ds, L.stream)) return rc;
-            if ((e = hipStreamSynchronize(L.stream)) != hipSuccess) return hip_fail(e, "decode");
+            if ((e = lane_wait(L.stream)) != hipSuccess) return hip_fail(e, "decode");
             for (uint32_t i = 0; i < n; ++i)
                 if (!present[i]) memcpy(shares[i], h + i * S, S);
             return RSM_OK;
@@ -823,7 +845,7 @@ int rsm_decode(rsm_ctx* ctx, uint8_t* const* shares, const uint8_t* present, uin
     if (int rc = launch_decode(ctx, ds, L.stream)) return rc;
     if ((e = hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, L.stream)) != hipSuccess)
         return hip_fail(e, "hipMemcpyAsync D2H");
-    if ((e = hipStreamSynchronize(L.stream)) != hipSuccess) return hip_fail(e, "decode");
+    if ((e = lane_wait(L.stream)) != hipSuccess) return hip_fail(e, "decode");
     for (uint32_t i = 0; i < n; ++i)
         if (!present[i]) memcpy(shares[i], h + i * S, S);
     return RSM_OK;

@@ -47,6 +47,7 @@ hipError_t hipStreamDestroy(hipStream_t s) {
     return hipSuccess;
 }
 hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
+hipError_t hipStreamQuery(hipStream_t) { return hipSuccess; }
 hipError_t hipMalloc(void** p, size_t n) {
     *p = calloc(1, n ? n : 1);
     return *p ? hipSuccess : hipErrorOutOfMemory;
