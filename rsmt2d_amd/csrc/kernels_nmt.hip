@@ -47,8 +47,8 @@ constexpr size_t kLdsCap = 160 * 1024 - 256;  // per workgroup, less the static 
 
 // SHA blocks of a node message 0x01 || l || r (nodes of 2 ns + 32 bytes)
 __host__ __device__ constexpr uint32_t node_blocks(uint32_t ns) { return (1 + 2 * (2 * ns + 32) + 8) / 64 + 1; }
-size_t tree_lds_bytes(uint32_t W, uint32_t ns) {
-    return ((size_t)2 * (W / 2) * kNodeWords + (size_t)256 * 16 * node_blocks(ns)) * 4;
+size_t tree_lds_bytes(uint32_t W, uint32_t ns) {  // two levels, a spare node, 256 message buffers
+    return ((size_t)(2 * (W / 2) + 1) * kNodeWords + (size_t)256 * 16 * node_blocks(ns)) * 4;
 }
 
 // the first n bytes of a big-endian word (n clamped to 0..4)
@@ -212,7 +212,9 @@ __global__ __launch_bounds__(256) void nmt_tree_kernel(const uint32_t* __restric
     if (status) status += (uint64_t)blockIdx.y * 2 * W;
     const uint32_t half = W / 2;
     auto lvl = [&](uint32_t which) -> uint32_t* { return lds + (size_t)which * half * kNodeWords; };
-    uint8_t* mb = reinterpret_cast<uint8_t*>(lds + (size_t)2 * half * kNodeWords) + threadIdx.x * (64u * node_blocks(ns));
+    // the spare node: lanes past a level's last node store their repeat there (below)
+    uint32_t* const spare = lds + (size_t)2 * half * kNodeWords;
+    uint8_t* mb = reinterpret_cast<uint8_t*>(spare + kNodeWords) + threadIdx.x * (64u * node_blocks(ns));
     __shared__ uint32_t bad;
     if (threadIdx.x == 0) bad = 0;
     __syncthreads();
@@ -224,39 +226,58 @@ __global__ __launch_bounds__(256) void nmt_tree_kernel(const uint32_t* __restric
     uint32_t my_bad = 0;
     // level 1 from the leaf records: pairs (2j, 2j+1); push order checked on
     // every consecutive leaf pair
+    // A level's pass runs every lane of the wave that holds its last node: lanes past
+    // it repeat node j0 + tid % rem and store to the spare node (a wave with few lanes
+    // active hashes 2-3.5x slower per compression: kernels_sha.hip); whole waves past
+    // it stay idle.
+    auto pass_lane = [&](uint32_t j0, uint32_t n, uint32_t& j, bool& own) -> bool {
+        const uint32_t rem = n - j0;
+        own = threadIdx.x < rem;
+        if (!own && (threadIdx.x >> 6) != ((rem - 1) >> 6)) return false;
+        j = j0 + (own ? threadIdx.x : threadIdx.x % rem);
+        return true;
+    };
     uint32_t cnt = W;
     uint32_t next = (cnt + 1) / 2;
-    for (uint32_t j = threadIdx.x; j < next; j += 256u) {
+    for (uint32_t j0 = 0; j0 < next; j0 += 256u) {
+        uint32_t j;
+        bool own;
+        if (!pass_lane(j0, next, j, own)) continue;
         Node a, b, o;
+        uint32_t bad_here = 0;
         leaf_node(leaf, cell_of(2 * j), a);
         if (2 * j + 1 < cnt) {
             leaf_node(leaf, cell_of(2 * j + 1), b);
-            if (ns_less(b.mn, a.mn)) my_bad = 1;
+            if (ns_less(b.mn, a.mn)) bad_here = 1;
             if (2 * j + 2 < cnt) {
                 Node c;
                 leaf_node(leaf, cell_of(2 * j + 2), c);
-                if (ns_less(c.mn, b.mn)) my_bad = 1;
+                if (ns_less(c.mn, b.mn)) bad_here = 1;
             }
-            if (!hash_node(a, b, ns, ig, mb, o)) my_bad = 1;
+            if (!hash_node(a, b, ns, ig, mb, o)) bad_here = 1;
         } else {
             o = a;
         }
-        lds_store(lvl(0) + (size_t)j * kNodeWords, o);
+        if (own) my_bad |= bad_here;
+        lds_store(own ? lvl(0) + (size_t)j * kNodeWords : spare, o);
     }
     __syncthreads();
     uint32_t cur = 0;
     for (cnt = next; cnt > 1; cnt = next) {
         next = (cnt + 1) / 2;
-        for (uint32_t j = threadIdx.x; j < next; j += 256u) {
+        for (uint32_t j0 = 0; j0 < next; j0 += 256u) {
+            uint32_t j;
+            bool own;
+            if (!pass_lane(j0, next, j, own)) continue;
             Node a, b, o;
             lds_node(lvl(cur) + (size_t)(2 * j) * kNodeWords, a);
             if (2 * j + 1 < cnt) {
                 lds_node(lvl(cur) + (size_t)(2 * j + 1) * kNodeWords, b);
-                if (!hash_node(a, b, ns, ig, mb, o)) my_bad = 1;
+                if (!hash_node(a, b, ns, ig, mb, o) && own) my_bad = 1;
             } else {
                 o = a;
             }
-            lds_store(lvl(cur ^ 1u) + (size_t)j * kNodeWords, o);
+            lds_store(own ? lvl(cur ^ 1u) + (size_t)j * kNodeWords : spare, o);
         }
         __syncthreads();
         cur ^= 1u;
