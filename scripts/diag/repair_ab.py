@@ -1,9 +1,12 @@
 """Repair transport A/B (diagnostic library): BenchmarkRepair's scheme (k of the 2k cells of
 every row erased, extendeddatacrossword_test.go:443-453), S = 512, k = 128 / 256 / 512,
 repaired through rsm_eds_repair with the zero-copy first sweep in production form (mode 0:
-one zero-copy decoder reading present and writing rebuilt cells) or the split transport
-(mode 1: gather kernel on a loader stream + device decoder writing rebuilt cells back,
-chunk by chunk).  (The run in profiles/r05h_repair_transport_ab.jsonl predates the swap
+one zero-copy decoder per half reading present and writing rebuilt cells, the halves one
+after the other) or the split transport (mode 1: gather kernel on a loader stream + device
+decoder writing rebuilt cells back, chunk by chunk).  REPAB_MODES picks the modes (default
+0,1), REPAB_KS the k values.  (profiles/r05t_repair_concurrent_ab.jsonl was taken with a
+since-removed mode: mode 0 there ran the two halves on two lanes at once, mode 2 is the
+production form.)  (The run in profiles/r05h_repair_transport_ab.jsonl predates the swap
 of the two mode numbers: there mode 0 is the split transport.)  Every repaired
 square is compared with the original.  One JSON line per (k, mode, rep).
 usage: python3 scripts/diag/repair_ab.py"""
@@ -60,7 +63,7 @@ def main():
         fptrs[present.reshape(-1) == 0] = 0
         reps = int(os.environ.get("REPAB_REPS", "5"))
         for rep in range(2):
-            for mode in (0, 1):
+            for mode in [int(x) for x in os.environ.get("REPAB_MODES", "0,1").split(",")]:
                 chk(D.rsm_diag_set_repair_mode(mode))
                 times, fast, ok = [], 0, True
                 for i in range(reps):
