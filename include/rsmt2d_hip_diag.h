@@ -62,11 +62,6 @@ int rsm_diag_set_dec8_mode(uint32_t mode);
 /* Codec calls (rsm_encode / rsm_decode) spin on hipStreamQuery for up to `us`
  * microseconds before blocking in hipStreamSynchronize (0: block at once, production). */
 int rsm_diag_set_codec_spin(uint32_t us);
-/* Repair's zero-copy first sweep: 0 = production (one zero-copy decoder kernel that
- * both reads present cells and writes rebuilt cells over PCIe), 1 = the split transport
- * (a gather kernel on a loader stream reads present cells chunk by chunk while the
- * device decoder of the previous chunk writes rebuilt cells back; measured slower). */
-int rsm_diag_set_repair_mode(int mode);
 /* Both passes of `count` in-place k = 128 squares in ONE persistent launch
  * (extend_gf8_bs128q_kernel: row and Q0-column sets from one queue, Q1-column sets
  * from a ready list; `delay` squares of row sets lead the Q0-column sets).

@@ -491,21 +491,6 @@ int pre_repair_sanity_check(rsm_eds* e, DevSquare& dev, const uint8_t* row_roots
 
 // Device fast path.  Returns RSM_OK with the square repaired, 1 to request the
 // exact sequential path (e is untouched in that case), or an RSM_E* error.
-// The split transport below measured SLOWER than one zero-copy decoder doing both
-// directions (c3 1.06 against 0.91 ms, k = 256 3.14 against 2.81, k = 512 9.9 against
-// 8.7; profiles/r05h_repair_transport_ab.jsonl): production keeps the one-kernel form.
-#ifdef RSM_DIAG
-static std::atomic<int> g_repair_mode{0};  // 1: the split transport (A/B)
-static bool repair_split_transport() { return g_repair_mode.load() == 1; }
-}  // namespace
-extern "C" int rsm_diag_set_repair_mode(int mode) {
-    g_repair_mode.store(mode);
-    return RSM_OK;
-}
-namespace {
-#else
-static bool repair_split_transport() { return false; }
-#endif
 enum { kFallbackStuck = 1, kFallbackEncoding = 2, kFallbackRoots = 3 };
 
 // Zero-copy form of the common first sweep (BenchmarkRepair's shape: every
@@ -577,58 +562,11 @@ int fast_repair_rows_zero_copy(rsm_eds* e, DevSquare& dev, const std::vector<uin
     // a quarter of the CUs (A/B on MI355X, profiles/r02c_repair_ab.txt: 64 workgroups
     // 0.87 ms, 128 0.89 ms, one per task 0.91 ms)
     const uint32_t zc_grid = dev.ctx->cus / 4 ? dev.ctx->cus / 4 : 1;
-    // Split transport (round 5, diagnostic): a gather kernel on a loader stream reads the
-    // present cells of a chunk of rows over PCIe into the device square while the
-    // device-resident decoder of the previous chunk writes its rebuilt cells back (mirror
-    // stores), so reads and writes come from different kernels (profiles/r02c_zcprobe.jsonl
-    // measured 75 GB/s for that pattern against ~56-58 for one kernel doing both) -- but
-    // slower end to end here (see repair_split_transport).
-    const bool split_transport = repair_split_transport();
-    std::unique_ptr<LaneGuard> gl;
-    hipStream_t sl = nullptr;
-    hipEvent_t evl[3] = {};
-    struct EvGuard3 {
-        hipEvent_t* e;
-        ~EvGuard3() {
-            for (int c = 0; c < 3; ++c)
-                if (e[c]) (void)hipEventDestroy(e[c]);
-        }
-    } evg3{evl};
-    if (split_transport) {
-        gl = std::make_unique<LaneGuard>(dev.ctx);
-        if (!gl->lane) return gl->rc;
-        sl = gl->lane->stream;
-        for (auto& x : evl) (void)hipEventCreateWithFlags(&x, hipEventDisableTiming);
-        // the loader's gathers read the presence and index uploads queued on st
-        (void)hipEventRecord(evl[2], st);
-        (void)hipStreamWaitEvent(sl, evl[2], 0);
-    }
-    uint32_t nchunk = 0;
+    // (A split transport -- a gather kernel reading the present cells on a second lane while
+    // the device decoder of the previous chunk writes its rebuilt cells back -- and the two
+    // halves' sweeps on two lanes at once both measured no faster: DESIGN.md §5.)
     auto sweep = [&](size_t t0, size_t t1) -> int {
         if (t1 <= t0) return RSM_OK;
-        if (split_transport) {
-            const size_t per = (t1 - t0 + 3) / 4;  // four chunks per half: a five-stage pipeline
-            for (size_t c0 = t0; c0 < t1; c0 += per) {
-                const size_t c1 = std::min(t1, c0 + per);
-                hipEvent_t evc = evl[nchunk++ & 1u];
-                if ((r = launch_zc_gather_rows(static_cast<const uint8_t*>(hmap), dev.d_eds, dev.d_pres, dev.d_idx + c0,
-                                               (uint32_t)(c1 - c0), W, e->S, sl)) != hipSuccess)
-                    return hip_fail(r, "zero-copy gather");
-                (void)hipEventRecord(evc, sl);
-                (void)hipStreamWaitEvent(st, evc, 0);
-                DecodeSet ds{};
-                ds.base = dev.d_eds;
-                ds.presence = dev.d_pres;
-                ds.indices = dev.d_idx + c0;
-                ds.count = (uint32_t)(c1 - c0);
-                ds.axis = RSM_AXIS_ROW;
-                ds.k = k;
-                ds.S = e->S;
-                ds.mirror = static_cast<uint8_t*>(hmap);
-                if (int rc = launch_decode(dev.ctx, ds, st)) return rc;
-            }
-            return RSM_OK;
-        }
         DecodeSet ds{};
         ds.base = dev.d_eds;
         ds.presence = dev.d_pres;

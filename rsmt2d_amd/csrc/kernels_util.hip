@@ -83,35 +83,4 @@ hipError_t launch_compare_parity(const uint8_t* a, const uint8_t* b, uint32_t k,
     return hipGetLastError();
 }
 
-// Zero-copy gather for Repair: the present cells (presence byte non-zero) of `nrows`
-// listed rows of a host-mapped [W][W][S] square, read over PCIe into the same cells of
-// the device square; 16 bytes per thread.  Absent cells are left as they are (the
-// decoders multiply them by zero).
-__global__ __launch_bounds__(256) void zc_gather_rows_kernel(const uint8_t* host, uint8_t* dev, const uint8_t* pres,
-                                                             const uint32_t* rows, uint32_t nrows, uint32_t W,
-                                                             uint32_t S) {
-    const uint32_t per = S / 16;
-    const uint64_t total = (uint64_t)nrows * W * per;
-    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < total; i += (uint64_t)gridDim.x * 256ull) {
-        const uint64_t q = i / per;
-        const uint32_t piece = (uint32_t)(i - q * per);
-        const uint64_t cell = (uint64_t)rows[q / W] * W + q % W;
-        if (pres[cell]) {
-            const uint64_t off = cell * S + (uint64_t)piece * 16;
-            *reinterpret_cast<uint4*>(dev + off) = *reinterpret_cast<const uint4*>(host + off);
-        }
-    }
-}
-
-hipError_t launch_zc_gather_rows(const uint8_t* host, uint8_t* dev, const uint8_t* pres, const uint32_t* rows,
-                                 uint32_t nrows, uint32_t W, uint32_t S, hipStream_t st) {
-    const uint64_t total = (uint64_t)nrows * W * (S / 16);
-    if (total == 0) return hipSuccess;
-    uint64_t blocks = (total + 255) / 256;
-    if (blocks > 1024) blocks = 1024;
-    hipLaunchKernelGGL(zc_gather_rows_kernel, dim3((uint32_t)blocks), dim3(256), 0, st, host, dev, pres, rows, nrows,
-                       W, S);
-    return hipGetLastError();
-}
-
 }  // namespace rsm

@@ -149,9 +149,6 @@ hipError_t launch_tree_roots(const uint32_t* d_leaf, uint32_t W, uint32_t first,
                              hipStream_t st);
 hipError_t launch_fill_random(void* p, uint64_t bytes, uint64_t seed, hipStream_t st);
 hipError_t launch_compare(const uint8_t* a, const uint8_t* b, uint64_t n, uint32_t* mismatch, hipStream_t st);
-// Repair's zero-copy gather: present cells of listed rows, host-mapped square -> device square
-hipError_t launch_zc_gather_rows(const uint8_t* host, uint8_t* dev, const uint8_t* pres, const uint32_t* rows,
-                                 uint32_t nrows, uint32_t W, uint32_t S, hipStream_t st);
 hipError_t launch_compare_parity(const uint8_t* a, const uint8_t* b, uint32_t k, uint32_t S, uint32_t axis,
                                  const uint32_t* indices, uint32_t count, uint32_t* flags, hipStream_t st);
 

@@ -1,14 +1,10 @@
-"""Repair transport A/B (diagnostic library): BenchmarkRepair's scheme (k of the 2k cells of
-every row erased, extendeddatacrossword_test.go:443-453), S = 512, k = 128 / 256 / 512,
-repaired through rsm_eds_repair with the zero-copy first sweep in production form (mode 0:
-one zero-copy decoder per half reading present and writing rebuilt cells, the halves one
-after the other) or the split transport (mode 1: gather kernel on a loader stream + device
-decoder writing rebuilt cells back, chunk by chunk).  REPAB_MODES picks the modes (default
-0,1), REPAB_KS the k values.  (profiles/r05t_repair_concurrent_ab.jsonl was taken with a
-since-removed mode: mode 0 there ran the two halves on two lanes at once, mode 2 is the
-production form.)  (The run in profiles/r05h_repair_transport_ab.jsonl predates the swap
-of the two mode numbers: there mode 0 is the split transport.)  Every repaired
-square is compared with the original.  One JSON line per (k, mode, rep).
+"""Repair timing (diagnostic library): BenchmarkRepair's scheme (k of the 2k cells of every
+row erased, extendeddatacrossword_test.go:443-453), S = 512, k = 128 / 256 / 512, repaired
+through rsm_eds_repair (zero-copy sweeps); every repaired square is compared with the
+original.  One JSON line per (k, rep).  The A/B lines in profiles/r05h_repair_transport_ab.jsonl
+(split transport) and profiles/r05t_repair_concurrent_ab.jsonl (the halves on two lanes)
+were taken with diagnostic modes of rsm_eds_repair that were removed once measured slower.
+REPAB_KS picks the k values.
 usage: python3 scripts/diag/repair_ab.py"""
 import ctypes
 import json
@@ -63,8 +59,7 @@ def main():
         fptrs[present.reshape(-1) == 0] = 0
         reps = int(os.environ.get("REPAB_REPS", "5"))
         for rep in range(2):
-            for mode in [int(x) for x in os.environ.get("REPAB_MODES", "0,1").split(",")]:
-                chk(D.rsm_diag_set_repair_mode(mode))
+            for mode in (0,):
                 times, fast, ok = [], 0, True
                 for i in range(reps):
                     h = ctypes.c_void_p()
@@ -85,7 +80,6 @@ def main():
                                   "repair_ms_p50": round(sorted(times)[len(times) // 2] * 1e3, 3),
                                   "repair_ms_min": round(min(times) * 1e3, 3), "fast_path": fast,
                                   "repaired_equal": ok}), flush=True)
-        chk(D.rsm_diag_set_repair_mode(0))
 
 
 if __name__ == "__main__":

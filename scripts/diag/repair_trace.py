@@ -1,6 +1,6 @@
 """Repair (config 3) under a copy + kernel trace: k=128, S=512, 128 of 256 cells of
-every row erased (BenchmarkRepair), repaired `reps` times.  REPAIR_TRACE_SPLIT=1: the
-diagnostic library with the split transport (rsm_diag_set_repair_mode(1)).
+every row erased (BenchmarkRepair), repaired `reps` times.  (The split-transport trace of
+DESIGN.md §5 was taken with a diagnostic Repair mode since removed.)
 usage: repair_trace.py [reps]"""
 import ctypes
 import os
@@ -16,8 +16,7 @@ reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
 k, S = 128, 512
 W = 2 * k
 L = R.library()
-SPLIT = os.environ.get("REPAIR_TRACE_SPLIT") == "1"
-LR = R.diag_library() if SPLIT else L  # the library the timed repairs run through
+LR = L
 ctx = R.device_context(0)
 buf = R.DeviceBuffer(W * W * S)
 buf.fill_random(0xC3)
@@ -43,11 +42,6 @@ L.rsm_eds_free(h)
 fp = (ctypes.c_void_p * (W * W))(*[base + i * S if present.flat[i] else None for i in range(W * W)])
 fl = (ctypes.c_uint32 * (W * W))(*[S if present.flat[i] else 0 for i in range(W * W)])
 ctx_r = ctx
-if SPLIT:
-    c = ctypes.c_void_p()
-    R._check_with(LR, LR.rsm_ctx_create(0, ctypes.byref(c)))
-    ctx_r = c.value
-    R._check_with(LR, LR.rsm_diag_set_repair_mode(1))
 for i in range(reps):
     h = ctypes.c_void_p()
     R._check_with(LR, LR.rsm_eds_import(None, fp, fl, W * W, ctypes.byref(h)))

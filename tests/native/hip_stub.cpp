@@ -149,15 +149,6 @@ hipError_t launch_decode_gf16(const DecodeSet& ds, const Gf16Dev& g, hipStream_t
     touch_decode(ds);
     return hipSuccess;
 }
-hipError_t launch_zc_gather_rows(const uint8_t* host, uint8_t* dev, const uint8_t* pres, const uint32_t* rows,
-                                 uint32_t nrows, uint32_t W, uint32_t S, hipStream_t) {
-    for (uint32_t q = 0; q < nrows; ++q)
-        for (uint32_t c = 0; c < W; ++c) {
-            const uint64_t cell = (uint64_t)rows[q] * W + c;
-            if (pres[cell]) memcpy(dev + cell * S, host + cell * S, S);
-        }
-    return hipSuccess;
-}
 hipError_t launch_encode_gf8_wide(const CodewordSet& cs, hipStream_t st) { return launch_encode_gf8(cs, st); }
 hipError_t launch_decode_gf8_wide(const DecodeSet& ds, hipStream_t st) { return launch_decode_gf8(ds, st); }
 bool dec16_needs_work() { return false; }
