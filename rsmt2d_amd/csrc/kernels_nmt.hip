@@ -17,7 +17,8 @@
 //
 // Two kernels, as for the DefaultTree (kernels_sha.hip):
 //   nmt_leaf_kernel : one thread per cell, streams ns || share through SHA-256;
-//                     one leaf record (ns, digest) serves the cell's row and column.
+//                     one leaf record (ns, digest) serves the cell's row and column
+//                     (nmt_leaf29_kernel: the same for 29-byte namespaces, 16-byte loads);
 //   nmt_tree_kernel : one workgroup per tree, levels ping-pong in LDS; each thread
 //                     lays its node message out in its own LDS bytes and hashes it.
 // Namespace sizes up to 32 bytes (Celestia: 29), widths up to 1024 (LDS permitting).
@@ -112,6 +113,80 @@ __global__ __launch_bounds__(256) void nmt_leaf_kernel(const uint8_t* __restrict
     uint32_t* o = leaf + (uint64_t)cell * kLeafWords;
 #pragma unroll
     for (int i = 0; i < (int)kNsWords; ++i) o[i] = (q0 ? d0[i] : 0xFFFFFFFFu) & head_mask((int)ns - 4 * i);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[kNsWords + i] = h[i];
+}
+
+// The same leaf records for Celestia's 29-byte namespace and shares a multiple of 64
+// bytes, streamed like kernels_sha.hip's leaf_hash_kernel: 16-byte loads of 64-byte
+// share chunks, big-endian words.  The message 0x00 || ns || share puts share byte j
+// at message byte 30 + j, so message word m >= 8 is the funnel shift of share words
+// m - 8 and m - 7 by 16 bits; words 0..7 carry the prefix (for a Q0 cell ns is the
+// share's first 29 bytes: share words shifted by 8 bits, as the DefaultTree leaf).
+// Block b (of S/64 + 1) takes chunk b - 1's upper half and chunk b's first nine
+// words; the last block's share word S/4 is the 0x80 pad (at message byte 30 + S, byte
+// 2 of word S/4 + 7), word 15 the bit length.  The generic kernel above reads each
+// word with its own 4-byte load and runtime masks.
+typedef uint32_t nv4u __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void nmt_leaf29_kernel(const uint8_t* __restrict__ eds, uint32_t W, uint32_t S,
+                                                         uint32_t k, uint32_t* __restrict__ leaf) {
+    const uint32_t cell = blockIdx.x * 256u + threadIdx.x;
+    if (cell >= W * W) return;
+    eds += (uint64_t)blockIdx.y * W * W * S;
+    leaf += (uint64_t)blockIdx.y * W * W * kLeafWords;
+    const uint32_t r = cell / W, c = cell - r * W;
+    const bool q0 = r < k && c < k;
+    const nv4u* p = reinterpret_cast<const nv4u*>(eds + (uint64_t)cell * S);
+    const uint32_t chunks = S / 64u, L = 30u + S;
+    uint32_t h[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) h[i] = kH0[i];
+    uint32_t hi[8];   // words 8..15 of the previous chunk
+    uint32_t nsw[8];  // the namespace words (chunk 0's first eight)
+    for (uint32_t b = 0; b <= chunks; ++b) {
+        uint32_t cw[16];
+        if (b < chunks) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const nv4u v = p[b * 4u + q];
+                cw[4 * q + 0] = __builtin_bswap32(v.x);
+                cw[4 * q + 1] = __builtin_bswap32(v.y);
+                cw[4 * q + 2] = __builtin_bswap32(v.z);
+                cw[4 * q + 3] = __builtin_bswap32(v.w);
+            }
+        } else {
+            cw[0] = 0x80000000u;  // the pad byte after the share
+#pragma unroll
+            for (int i = 1; i < 16; ++i) cw[i] = 0u;
+        }
+        uint32_t w[16];
+        if (b == 0) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) nsw[i] = cw[i];
+#pragma unroll
+            for (int i = 0; i < 7; ++i)
+                w[i] = q0 ? __builtin_amdgcn_alignbit(i == 0 ? 0u : cw[i - 1], cw[i], 8)
+                          : (i == 0 ? 0x00FFFFFFu : 0xFFFFFFFFu);
+            w[7] = (q0 ? (__builtin_amdgcn_alignbit(cw[6], cw[7], 8) & 0xFFFF0000u) : 0xFFFF0000u) | (cw[0] >> 16);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) w[i] = __builtin_amdgcn_alignbit(hi[i], i < 7 ? hi[i + 1] : cw[0], 16);
+        }
+        if (b < chunks) {
+#pragma unroll
+            for (int i = 8; i < 16; ++i) w[i] = __builtin_amdgcn_alignbit(cw[i - 8], cw[i - 7], 16);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) hi[i] = cw[8 + i];
+        } else {
+#pragma unroll
+            for (int i = 8; i < 15; ++i) w[i] = 0u;
+            w[15] = 8u * L;
+        }
+        sha_block(h, w);
+    }
+    uint32_t* o = leaf + (uint64_t)cell * kLeafWords;
+#pragma unroll
+    for (int i = 0; i < (int)kNsWords; ++i) o[i] = (q0 ? nsw[i] : 0xFFFFFFFFu) & head_mask(29 - 4 * i);
 #pragma unroll
     for (int i = 0; i < 8; ++i) o[kNsWords + i] = h[i];
 }
@@ -378,16 +453,17 @@ template <int NS>
 __host__ __device__ constexpr uint32_t wwave_lds_words(uint32_t W, uint32_t tpw) {
     return tpw * wtree_lds_words<NS>(W) + wnode_words<NS>();
 }
-constexpr uint32_t kNmtTreesPerBlock = 4;  // one wave per tree group
+constexpr uint32_t kNmtTreesPerBlock = 4;  // waves per workgroup of the one-tree-per-wave form
 
-template <int NS, int TPW>
-__global__ __launch_bounds__(256) void nmt_tree_wave_kernel(const uint32_t* __restrict__ leaf, uint32_t W,
-                                                            uint32_t ignore_max, uint8_t* __restrict__ roots,
-                                                            uint32_t* __restrict__ status) {
+// WPB waves per workgroup, TPW trees per wave
+template <int NS, int TPW, int WPB>
+__global__ __launch_bounds__(64 * WPB) void nmt_tree_wave_kernel(const uint32_t* __restrict__ leaf, uint32_t W,
+                                                                 uint32_t ignore_max, uint8_t* __restrict__ roots,
+                                                                 uint32_t* __restrict__ status) {
     constexpr int kW = WNode<NS>::kW;
     constexpr uint32_t NW = wnode_words<NS>();
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    const uint32_t t0 = (blockIdx.x * kNmtTreesPerBlock + wv) * TPW, count = 2 * W;
+    const uint32_t t0 = (blockIdx.x * WPB + wv) * TPW, count = 2 * W;
     if (t0 >= count) return;  // whole wave (no workgroup barrier in this kernel)
     const uint32_t nt = count - t0 < (uint32_t)TPW ? count - t0 : (uint32_t)TPW;
     leaf += (uint64_t)blockIdx.y * W * W * kLeafWords;
@@ -506,24 +582,42 @@ __global__ __launch_bounds__(256) void nmt_tree_wave_kernel(const uint32_t* __re
     }
 }
 
-// trees per wave: as many as keep four waves' LDS within a third of the CU
+// Trees per wave and waves per workgroup.  A batch takes the most trees per wave
+// whose workgroup of at least two waves keeps its LDS within a third of the CU: the
+// upper levels of a tree leave lanes idle (or, since round 5, hashing repeats), so
+// packing trees cuts the batch's wave-instructions (W = 256: two trees per wave in
+// two-wave workgroups, 49 KiB, against one tree per wave).  One square (latency:
+// Repair's checks) takes one tree per wave in four-wave workgroups.
 template <int NS>
-inline uint32_t nmt_trees_per_wave(uint32_t W) {
+inline void nmt_tree_shape(uint32_t W, bool latency, uint32_t* tpw, uint32_t* wpb) {
+    *tpw = 1;
+    *wpb = kNmtTreesPerBlock;
+    if (latency) return;
     for (uint32_t t = 4; t > 1; t >>= 1)
-        if ((size_t)kNmtTreesPerBlock * wwave_lds_words<NS>(W, t) * 4u <= 52u * 1024u) return t;
-    return 1;
+        for (uint32_t b = 4; b >= 2; b >>= 1)
+            if ((size_t)b * wwave_lds_words<NS>(W, t) * 4u <= 52u * 1024u) {
+                *tpw = t;
+                *wpb = b;
+                return;
+            }
 }
 template <int NS>
 hipError_t launch_nmt_tree_wave(const uint32_t* d_leaf, uint32_t W, uint32_t ignore_max, uint8_t* d_roots,
                                 uint32_t* d_status, uint32_t squares, hipStream_t st) {
-    const uint32_t tpw = nmt_trees_per_wave<NS>(W);
-    const uint32_t blocks = (2 * W + kNmtTreesPerBlock * tpw - 1) / (kNmtTreesPerBlock * tpw);
-    const size_t lds = (size_t)kNmtTreesPerBlock * wwave_lds_words<NS>(W, tpw) * 4u;
-    switch (tpw) {
-        case 4: hipLaunchKernelGGL((nmt_tree_wave_kernel<NS, 4>), dim3(blocks, squares), dim3(256), lds, st, d_leaf, W, ignore_max, d_roots, d_status); break;
-        case 2: hipLaunchKernelGGL((nmt_tree_wave_kernel<NS, 2>), dim3(blocks, squares), dim3(256), lds, st, d_leaf, W, ignore_max, d_roots, d_status); break;
-        default: hipLaunchKernelGGL((nmt_tree_wave_kernel<NS, 1>), dim3(blocks, squares), dim3(256), lds, st, d_leaf, W, ignore_max, d_roots, d_status); break;
-    }
+    uint32_t tpw, wpb;
+    nmt_tree_shape<NS>(W, squares == 1, &tpw, &wpb);
+    const uint32_t blocks = (2 * W + wpb * tpw - 1) / (wpb * tpw);
+    const size_t lds = (size_t)wpb * wwave_lds_words<NS>(W, tpw) * 4u;
+    const dim3 grid(blocks, squares);
+#define RSM_NMT_WAVE(T, B)                                                                                        \
+    hipLaunchKernelGGL((nmt_tree_wave_kernel<NS, T, B>), grid, dim3(64 * B), lds, st, d_leaf, W, ignore_max, d_roots, \
+                       d_status)
+    if (tpw == 4 && wpb == 4) RSM_NMT_WAVE(4, 4);
+    else if (tpw == 4) RSM_NMT_WAVE(4, 2);
+    else if (tpw == 2 && wpb == 4) RSM_NMT_WAVE(2, 4);
+    else if (tpw == 2) RSM_NMT_WAVE(2, 2);
+    else RSM_NMT_WAVE(1, 4);
+#undef RSM_NMT_WAVE
     return hipGetLastError();
 }
 
@@ -539,7 +633,10 @@ hipError_t launch_nmt_roots(const uint8_t* d_eds, uint32_t W, uint32_t S, uint32
                             uint32_t* d_leaf, uint8_t* d_roots, uint32_t* d_status, hipStream_t st, uint32_t squares) {
     if (squares == 0) return hipSuccess;
     const uint32_t cells = W * W;
-    hipLaunchKernelGGL(nmt_leaf_kernel, dim3((cells + 255) / 256, squares), dim3(256), 0, st, d_eds, W, S, ns, k, d_leaf);
+    if (ns == 29 && S % 64 == 0 && S >= 64)  // Celestia's namespace: the streaming leaf kernel
+        hipLaunchKernelGGL(nmt_leaf29_kernel, dim3((cells + 255) / 256, squares), dim3(256), 0, st, d_eds, W, S, k, d_leaf);
+    else
+        hipLaunchKernelGGL(nmt_leaf_kernel, dim3((cells + 255) / 256, squares), dim3(256), 0, st, d_eds, W, S, ns, k, d_leaf);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     // Celestia's namespace size: the wave-per-tree kernel (its LDS permitting)

@@ -94,11 +94,13 @@ def test_nmt_roots_dev_vs_oracle(lib, k, ns, S):
     assert [bytes(got[(W + i) * RL:(W + i + 1) * RL]) for i in range(W)] == want_c
 
 
-@pytest.mark.parametrize("k,ns,S,count", [(4, 29, 64, 3), (16, 29, 512, 5), (8, 8, 128, 2)])
+@pytest.mark.parametrize("k,ns,S,count", [(4, 29, 64, 3), (16, 29, 512, 5), (8, 8, 128, 2), (64, 29, 512, 3),
+                                         (128, 29, 512, 2)])
 def test_nmt_roots_squares_dev_batched(lib, k, ns, S, count):
     """rsm_nmt_roots_squares_dev over a batch of squares (one launch pair) == the
     oracle's roots of every square; one square with an unordered namespace reports its
-    failing trees in its own status words only."""
+    failing trees in its own status words only.  k = 64 / 128 take the packed batch
+    shapes of the wave kernel (four / two trees per wave in two-wave workgroups)."""
     ctx = R.device_context(0)
     W = 2 * k
     RL = 2 * ns + 32
