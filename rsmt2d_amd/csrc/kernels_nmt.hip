@@ -446,17 +446,21 @@ __device__ __forceinline__ bool hash_node_w(const WNode<NS>& l, const WNode<NS>&
 template <int NS>
 __host__ __device__ constexpr uint32_t wnode_words() { return 2 * WNode<NS>::kW + 8; }
 template <int NS>
-__host__ __device__ constexpr uint32_t wtree_lds_words(uint32_t W) { return ((W + 1) / 2) * wnode_words<NS>(); }
+__host__ __device__ constexpr uint32_t wtree_lds_words(uint32_t W, bool f2 = false) {
+    return (f2 ? W / 4 : (W + 1) / 2) * wnode_words<NS>();  // f2: levels 1 and 2 in one pass
+}
 // one wave's LDS: its trees, then a spare node that lanes past a level's last node
 // store to (so every lane hashes: see the level loops)
 template <int NS>
-__host__ __device__ constexpr uint32_t wwave_lds_words(uint32_t W, uint32_t tpw) {
-    return tpw * wtree_lds_words<NS>(W) + wnode_words<NS>();
+__host__ __device__ constexpr uint32_t wwave_lds_words(uint32_t W, uint32_t tpw, bool f2 = false) {
+    return tpw * wtree_lds_words<NS>(W, f2) + wnode_words<NS>();
 }
 constexpr uint32_t kNmtTreesPerBlock = 4;  // waves per workgroup of the one-tree-per-wave form
 
-// WPB waves per workgroup, TPW trees per wave
-template <int NS, int TPW, int WPB>
+// WPB waves per workgroup, TPW trees per wave.  F2 (W a multiple of 4): the first pass
+// hashes leaves 4j .. 4j + 3 into level-1 nodes 2j, 2j + 1 and on into level-2 node j,
+// so LDS holds W/4 nodes per tree instead of W/2 (more trees, or more waves, per CU).
+template <int NS, int TPW, int WPB, bool F2>
 __global__ __launch_bounds__(64 * WPB) void nmt_tree_wave_kernel(const uint32_t* __restrict__ leaf, uint32_t W,
                                                                  uint32_t ignore_max, uint8_t* __restrict__ roots,
                                                                  uint32_t* __restrict__ status) {
@@ -470,9 +474,9 @@ __global__ __launch_bounds__(64 * WPB) void nmt_tree_wave_kernel(const uint32_t*
     roots += (uint64_t)blockIdx.y * 2 * W * (2 * NS + 32);
     if (status) status += (uint64_t)blockIdx.y * 2 * W;
     extern __shared__ uint32_t lds_raw[];
-    uint32_t* const base = lds_raw + (size_t)wv * wwave_lds_words<NS>(W, TPW);
-    auto lvl = [&](uint32_t u) { return base + (size_t)u * wtree_lds_words<NS>(W); };
-    uint32_t* const spare = base + (size_t)TPW * wtree_lds_words<NS>(W);
+    uint32_t* const base = lds_raw + (size_t)wv * wwave_lds_words<NS>(W, TPW, F2);
+    auto lvl = [&](uint32_t u) { return base + (size_t)u * wtree_lds_words<NS>(W, F2); };
+    uint32_t* const spare = base + (size_t)TPW * wtree_lds_words<NS>(W, F2);
     const bool ig = ignore_max != 0;
     auto leaf_at = [&](uint32_t tree, uint32_t pos, WNode<NS>& n) {
         const uint32_t axis = tree >= W ? 1u : 0u, idx = tree - axis * W;
@@ -518,28 +522,54 @@ __global__ __launch_bounds__(64 * WPB) void nmt_tree_wave_kernel(const uint32_t*
     // kernels_sha.hip; the store keeps the compiler from shrinking the hash to the
     // owning lanes).
     uint32_t cnt = W, next = (W + 1) / 2;
-    for (uint32_t v0 = 0; v0 < nt * next; v0 += 64u) {
-        const uint32_t rem = nt * next - v0;
-        const bool own = lane < rem;
-        const uint32_t v = v0 + (own ? lane : lane % rem);
-        const uint32_t u = v / next, j = v - u * next;
-        WNode<NS> a, b, o;
-        leaf_at(t0 + u, 2 * j, a);
-        bool ok = true;
-        if (2 * j + 1 < cnt) {
-            leaf_at(t0 + u, 2 * j + 1, b);
-            if (ns_lt(b.mn, a.mn)) ok = false;
-            if (2 * j + 2 < cnt) {
-                WNode<NS> c;
-                leaf_at(t0 + u, 2 * j + 2, c);
-                if (ns_lt(c.mn, b.mn)) ok = false;
+    if constexpr (F2) {
+        next = W / 4;
+        for (uint32_t v0 = 0; v0 < nt * next; v0 += 64u) {
+            const uint32_t rem = nt * next - v0;
+            const bool own = lane < rem;
+            const uint32_t v = v0 + (own ? lane : lane % rem);
+            const uint32_t u = v / next, j = v - u * next;
+            WNode<NS> a, b, c, d, l, r, o;
+            leaf_at(t0 + u, 4 * j, a);
+            leaf_at(t0 + u, 4 * j + 1, b);
+            leaf_at(t0 + u, 4 * j + 2, c);
+            leaf_at(t0 + u, 4 * j + 3, d);
+            bool ok = !ns_lt(b.mn, a.mn) && !ns_lt(c.mn, b.mn) && !ns_lt(d.mn, c.mn);
+            if (4 * j + 4 < cnt) {  // push order across the next group's first leaf
+                WNode<NS> e;
+                leaf_at(t0 + u, 4 * j + 4, e);
+                if (ns_lt(e.mn, d.mn)) ok = false;
             }
-            if (!hash_node_w<NS>(a, b, ig, o)) ok = false;
-        } else {
-            o = a;
+            if (!hash_node_w<NS>(a, b, ig, l)) ok = false;
+            if (!hash_node_w<NS>(c, d, ig, r)) ok = false;
+            if (!hash_node_w<NS>(l, r, ig, o)) ok = false;
+            st(own ? lvl(u) + (size_t)j * NW : spare, o);
+            if (own && !ok) bad |= 1u << u;
         }
-        st(own ? lvl(u) + (size_t)j * NW : spare, o);
-        if (own && !ok) bad |= 1u << u;
+    } else {
+        for (uint32_t v0 = 0; v0 < nt * next; v0 += 64u) {
+            const uint32_t rem = nt * next - v0;
+            const bool own = lane < rem;
+            const uint32_t v = v0 + (own ? lane : lane % rem);
+            const uint32_t u = v / next, j = v - u * next;
+            WNode<NS> a, b, o;
+            leaf_at(t0 + u, 2 * j, a);
+            bool ok = true;
+            if (2 * j + 1 < cnt) {
+                leaf_at(t0 + u, 2 * j + 1, b);
+                if (ns_lt(b.mn, a.mn)) ok = false;
+                if (2 * j + 2 < cnt) {
+                    WNode<NS> c;
+                    leaf_at(t0 + u, 2 * j + 2, c);
+                    if (ns_lt(c.mn, b.mn)) ok = false;
+                }
+                if (!hash_node_w<NS>(a, b, ig, o)) ok = false;
+            } else {
+                o = a;
+            }
+            st(own ? lvl(u) + (size_t)j * NW : spare, o);
+            if (own && !ok) bad |= 1u << u;
+        }
     }
     wave_sync();
     for (cnt = next; cnt > 1; cnt = next) {
@@ -582,41 +612,44 @@ __global__ __launch_bounds__(64 * WPB) void nmt_tree_wave_kernel(const uint32_t*
     }
 }
 
-// Trees per wave and waves per workgroup.  A batch takes the most trees per wave
-// whose workgroup of at least two waves keeps its LDS within a third of the CU: the
-// upper levels of a tree leave lanes idle (or, since round 5, hashing repeats), so
-// packing trees cuts the batch's wave-instructions (W = 256: two trees per wave in
-// two-wave workgroups, 49 KiB, against one tree per wave).  One square (latency:
-// Repair's checks) takes one tree per wave in four-wave workgroups.
+// Trees per wave and waves per workgroup.  A batch packs two trees per wave (the upper
+// levels of one tree leave most lanes repeating work, so packing cuts the batch's
+// wave-instructions) in four-wave workgroups when their LDS fits a third of the CU,
+// else two-wave ones; one square (latency: Repair's checks) takes one tree per wave.
+// W = 256, 32 squares (scripts/diag/nmtprobe.hip, profiles/r05aa_nmtprobe.txt): one tree
+// per wave 1142 us; two per wave 1012; with levels 1-2 fused (F2) 786 at 2 x 4 or 2 x 2
+// waves, 913 at four trees per wave.
 template <int NS>
-inline void nmt_tree_shape(uint32_t W, bool latency, uint32_t* tpw, uint32_t* wpb) {
+inline void nmt_tree_shape(uint32_t W, bool latency, bool f2, uint32_t* tpw, uint32_t* wpb) {
     *tpw = 1;
     *wpb = kNmtTreesPerBlock;
     if (latency) return;
-    for (uint32_t t = 4; t > 1; t >>= 1)
-        for (uint32_t b = 4; b >= 2; b >>= 1)
-            if ((size_t)b * wwave_lds_words<NS>(W, t) * 4u <= 52u * 1024u) {
-                *tpw = t;
-                *wpb = b;
-                return;
-            }
+    for (uint32_t b = 4; b >= 2; b >>= 1)
+        if ((size_t)b * wwave_lds_words<NS>(W, 2, f2) * 4u <= 52u * 1024u) {
+            *tpw = 2;
+            *wpb = b;
+            return;
+        }
 }
 template <int NS>
 hipError_t launch_nmt_tree_wave(const uint32_t* d_leaf, uint32_t W, uint32_t ignore_max, uint8_t* d_roots,
                                 uint32_t* d_status, uint32_t squares, hipStream_t st) {
+    const bool f2 = W % 4 == 0;
     uint32_t tpw, wpb;
-    nmt_tree_shape<NS>(W, squares == 1, &tpw, &wpb);
+    nmt_tree_shape<NS>(W, squares == 1, f2, &tpw, &wpb);
     const uint32_t blocks = (2 * W + wpb * tpw - 1) / (wpb * tpw);
-    const size_t lds = (size_t)wpb * wwave_lds_words<NS>(W, tpw) * 4u;
+    const size_t lds = (size_t)wpb * wwave_lds_words<NS>(W, tpw, f2) * 4u;
     const dim3 grid(blocks, squares);
-#define RSM_NMT_WAVE(T, B)                                                                                        \
-    hipLaunchKernelGGL((nmt_tree_wave_kernel<NS, T, B>), grid, dim3(64 * B), lds, st, d_leaf, W, ignore_max, d_roots, \
-                       d_status)
-    if (tpw == 4 && wpb == 4) RSM_NMT_WAVE(4, 4);
-    else if (tpw == 4) RSM_NMT_WAVE(4, 2);
-    else if (tpw == 2 && wpb == 4) RSM_NMT_WAVE(2, 4);
-    else if (tpw == 2) RSM_NMT_WAVE(2, 2);
-    else RSM_NMT_WAVE(1, 4);
+#define RSM_NMT_WAVE(T, B, F)                                                                                     \
+    hipLaunchKernelGGL((nmt_tree_wave_kernel<NS, T, B, F>), grid, dim3(64 * B), lds, st, d_leaf, W, ignore_max,    \
+                       d_roots, d_status)
+#define RSM_NMT_WAVE_F(T, B)      \
+    if (f2) RSM_NMT_WAVE(T, B, true); \
+    else RSM_NMT_WAVE(T, B, false)
+    if (tpw == 2 && wpb == 4) { RSM_NMT_WAVE_F(2, 4); }
+    else if (tpw == 2) { RSM_NMT_WAVE_F(2, 2); }
+    else { RSM_NMT_WAVE_F(1, 4); }
+#undef RSM_NMT_WAVE_F
 #undef RSM_NMT_WAVE
     return hipGetLastError();
 }
@@ -640,7 +673,7 @@ hipError_t launch_nmt_roots(const uint8_t* d_eds, uint32_t W, uint32_t S, uint32
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     // Celestia's namespace size: the wave-per-tree kernel (its LDS permitting)
-    if (ns == 29 && (size_t)kNmtTreesPerBlock * wwave_lds_words<29>(W, 1) * 4u <= kLdsCap)
+    if (ns == 29 && (size_t)kNmtTreesPerBlock * wwave_lds_words<29>(W, 1, W % 4 == 0) * 4u <= kLdsCap)
         return launch_nmt_tree_wave<29>(d_leaf, W, ignore_max, d_roots, d_status, squares, st);
     const size_t lds = tree_lds_bytes(W, ns);
     hipLaunchKernelGGL(nmt_tree_kernel, dim3(2 * W, squares), dim3(256), lds, st, d_leaf, W, ns, ignore_max, d_roots,

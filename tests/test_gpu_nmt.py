@@ -99,8 +99,8 @@ def test_nmt_roots_dev_vs_oracle(lib, k, ns, S):
 def test_nmt_roots_squares_dev_batched(lib, k, ns, S, count):
     """rsm_nmt_roots_squares_dev over a batch of squares (one launch pair) == the
     oracle's roots of every square; one square with an unordered namespace reports its
-    failing trees in its own status words only.  k = 64 / 128 take the packed batch
-    shapes of the wave kernel (four / two trees per wave in two-wave workgroups)."""
+    failing trees in its own status words only.  k = 64 / 128 take the wave kernel's
+    batch shape (two trees per wave, levels 1-2 in one pass)."""
     ctx = R.device_context(0)
     W = 2 * k
     RL = 2 * ns + 32
