@@ -270,54 +270,19 @@ void hash_prefixed(uint8_t prefix, const uint8_t* const* msg, int count, uint32_
 // with ns = ndata[:nsSize]; HashNode(l, r) = l.min || max || H(0x01 || l || r) where
 // max = l.max when IgnoreMaxNamespace and r.min is the all-0xFF namespace, else
 // r.max; the root over n leaves splits at the largest power of two below n
-// (RFC 6962 MTH).  Empty tree: zero namespaces || H("").
-struct NmtNode {
-    std::vector<uint8_t> b;  // 2*ns + 32 bytes
-};
-
-NmtNode nmt_leaf(const uint8_t* ns, uint32_t nsz, const uint8_t* share, uint32_t S) {
-    Sha256 s;
-    uint8_t pre = 0x00;
-    s.update(&pre, 1);
-    s.update(ns, nsz);
-    s.update(share, S);
-    NmtNode o;
-    o.b.resize(2 * nsz + 32);
-    memcpy(o.b.data(), ns, nsz);
-    memcpy(o.b.data() + nsz, ns, nsz);
-    s.final(o.b.data() + 2 * nsz);
-    return o;
-}
-
-bool nmt_node(const NmtNode& l, const NmtNode& r, uint32_t nsz, bool ignore_max, NmtNode& o) {
-    const uint8_t *lmin = l.b.data(), *lmax = lmin + nsz, *rmin = r.b.data(), *rmax = rmin + nsz;
-    if (memcmp(lmax, rmin, nsz) > 0) return false;  // validateSiblingsNamespaceOrder
+// (RFC 6962 MTH), i.e. the perfect subtrees of the set bits of n folded from the
+// right, as the DefaultTree's stack.  Empty tree: zero namespaces || H("").
+// Nodes of a level sit contiguously (2 ns + 32 bytes each), so a pair is already the
+// message body 0x01 || l || r; leaves and each level are hashed kHashBatch at a time.
+// HashNode's validateSiblingsNamespaceOrder: r.min < l.max is an error.
+bool nmt_pair(const uint8_t* l, const uint8_t* r, uint32_t nsz, bool ignore_max, uint8_t* out_ns) {
+    const uint8_t *lmin = l, *lmax = l + nsz, *rmin = r, *rmax = r + nsz;
+    if (memcmp(lmax, rmin, nsz) > 0) return false;
     bool rmin_is_max = true;
     for (uint32_t i = 0; i < nsz; ++i) rmin_is_max &= rmin[i] == 0xFF;
-    const uint8_t* mx = (ignore_max && rmin_is_max) ? lmax : rmax;
-    Sha256 s;
-    uint8_t pre = 0x01;
-    s.update(&pre, 1);
-    s.update(l.b.data(), l.b.size());
-    s.update(r.b.data(), r.b.size());
-    o.b.resize(2 * nsz + 32);
-    memcpy(o.b.data(), lmin, nsz);
-    memcpy(o.b.data() + nsz, mx, nsz);
-    s.final(o.b.data() + 2 * nsz);
+    memcpy(out_ns, lmin, nsz);
+    memcpy(out_ns + nsz, (ignore_max && rmin_is_max) ? lmax : rmax, nsz);
     return true;
-}
-
-bool nmt_root(const std::vector<NmtNode>& leaf, uint32_t lo, uint32_t hi, uint32_t nsz, bool ignore_max, NmtNode& out) {
-    const uint32_t n = hi - lo;
-    if (n == 1) {
-        out = leaf[lo];
-        return true;
-    }
-    uint32_t k = 1;
-    while (k * 2 < n) k *= 2;  // largest power of two < n
-    NmtNode l, r;
-    return nmt_root(leaf, lo, lo + k, nsz, ignore_max, l) && nmt_root(leaf, lo + k, hi, nsz, ignore_max, r) &&
-           nmt_node(l, r, nsz, ignore_max, out);
 }
 
 }  // namespace
@@ -326,31 +291,79 @@ extern "C" int rsm_nmt_tree_root(void* user, int /*axis*/, uint32_t index, const
                                  uint32_t n_leaves, uint32_t leaf_size, uint8_t* root_out, uint32_t* root_len) {
     const auto* p = static_cast<const rsm_nmt_params*>(user);
     if (!p || !root_len || !root_out || p->namespace_size == 0 || p->square_size == 0) return RSM_EINVAL;
-    const uint32_t nsz = p->namespace_size, k = p->square_size;
-    if (*root_len < 2 * nsz + 32) return RSM_EINVAL;
+    const uint32_t nsz = p->namespace_size, k = p->square_size, NB = 2 * nsz + 32;
+    const bool ig = p->ignore_max_namespace != 0;
+    if (*root_len < NB) return RSM_EINVAL;
     // erasuredNamespacedMerkleTree.Push (nmtwrapper_test.go:94-120)
     if (index + 1 > 2 * k || n_leaves > 2 * k) return RSM_ETREE;  // pushed past predetermined square size
     if (leaf_size < nsz) return RSM_ETREE;                         // data is too short to contain namespace ID
+    if (n_leaves == 0) {
+        Sha256 s;
+        memset(root_out, 0, NB);
+        s.final(root_out + 2 * nsz);
+        *root_len = NB;
+        return RSM_OK;
+    }
     std::vector<uint8_t> parity(nsz, 0xFF);
-    std::vector<NmtNode> leaf(n_leaves);
+    const size_t ML = (size_t)nsz + leaf_size;  // a leaf's message body: ns || share
+    std::vector<uint8_t> msg((size_t)n_leaves * ML), nodes((size_t)n_leaves * NB);
     const uint8_t* prev = nullptr;
     for (uint32_t i = 0; i < n_leaves; ++i) {
         if (!leaves[i]) return RSM_ETREE;
         const uint8_t* ns = (i < k && index < k) ? leaves[i] : parity.data();  // isQuadrantZero
         if (prev && memcmp(ns, prev, nsz) < 0) return RSM_ETREE;           // nmt: ErrInvalidPushOrder
         prev = ns;
-        leaf[i] = nmt_leaf(ns, nsz, leaves[i], leaf_size);
+        memcpy(&msg[i * ML], ns, nsz);
+        memcpy(&msg[i * ML + nsz], leaves[i], leaf_size);
+        memcpy(&nodes[(size_t)i * NB], ns, nsz);
+        memcpy(&nodes[(size_t)i * NB + nsz], ns, nsz);
     }
-    NmtNode root;
-    if (n_leaves == 0) {
-        Sha256 s;
-        root.b.assign(2 * nsz + 32, 0);
-        s.final(root.b.data() + 2 * nsz);
-    } else if (!nmt_root(leaf, 0, n_leaves, nsz, p->ignore_max_namespace != 0, root)) {
-        return RSM_ETREE;
+    std::vector<Digest> dg(kHashBatch);
+    std::vector<uint8_t> nsb((size_t)kHashBatch * 2 * nsz);  // the pairs' new min || max
+    for (uint32_t i = 0; i < n_leaves; i += kHashBatch) {
+        const int c = (int)std::min<uint32_t>(kHashBatch, n_leaves - i);
+        const uint8_t* m[kHashBatch];
+        for (int q = 0; q < c; ++q) m[q] = &msg[(size_t)(i + q) * ML];
+        hash_prefixed(0x00, m, c, (uint32_t)ML, dg.data());
+        for (int q = 0; q < c; ++q) memcpy(&nodes[(size_t)(i + q) * NB + 2 * nsz], dg[q].b, 32);
     }
-    memcpy(root_out, root.b.data(), root.b.size());
-    *root_len = (uint32_t)root.b.size();
+    std::vector<uint32_t> subs;  // first leaf of each perfect subtree, largest first
+    for (uint32_t s0 = 0, bit = 31; s0 < n_leaves; --bit) {
+        const uint32_t size = 1u << bit;
+        if (!(n_leaves & size)) continue;
+        for (uint32_t cnt = size; cnt > 1; cnt /= 2) {  // level by level, in place from node s0
+            const uint32_t np = cnt / 2;
+            for (uint32_t j = 0; j < np; j += kHashBatch) {
+                const int c = (int)std::min<uint32_t>(kHashBatch, np - j);
+                const uint8_t* m[kHashBatch];
+                for (int q = 0; q < c; ++q) {
+                    const uint8_t* l = &nodes[(size_t)(s0 + 2 * (j + q)) * NB];
+                    if (!nmt_pair(l, l + NB, nsz, ig, &nsb[(size_t)q * 2 * nsz])) return RSM_ETREE;
+                    m[q] = l;
+                }
+                hash_prefixed(0x01, m, c, 2 * NB, dg.data());  // every pair read before any write
+                for (int q = 0; q < c; ++q) {
+                    uint8_t* o = &nodes[(size_t)(s0 + j + q) * NB];
+                    memcpy(o, &nsb[(size_t)q * 2 * nsz], 2 * nsz);
+                    memcpy(o + 2 * nsz, dg[q].b, 32);
+                }
+            }
+        }
+        subs.push_back(s0);
+        s0 += size;
+    }
+    std::vector<uint8_t> acc(&nodes[(size_t)subs.back() * NB], &nodes[(size_t)subs.back() * NB] + NB);
+    std::vector<uint8_t> pair(2 * NB);
+    for (int i = (int)subs.size() - 2; i >= 0; --i) {
+        memcpy(pair.data(), &nodes[(size_t)subs[i] * NB], NB);
+        memcpy(pair.data() + NB, acc.data(), NB);
+        if (!nmt_pair(pair.data(), pair.data() + NB, nsz, ig, acc.data())) return RSM_ETREE;
+        const uint8_t* m[1] = {pair.data()};
+        hash_prefixed(0x01, m, 1, 2 * NB, dg.data());
+        memcpy(acc.data() + 2 * nsz, dg[0].b, 32);
+    }
+    memcpy(root_out, acc.data(), NB);
+    *root_len = NB;
     return RSM_OK;
 }
 

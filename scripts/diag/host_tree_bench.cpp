@@ -7,6 +7,8 @@
 #include <vector>
 #include <cstring>
 extern "C" int rsm_default_tree_root(void*, int, uint32_t, const uint8_t* const*, uint32_t, uint32_t, uint8_t*, uint32_t*);
+extern "C" int rsm_nmt_tree_root(void*, int, uint32_t, const uint8_t* const*, uint32_t, uint32_t, uint8_t*, uint32_t*);
+struct NmtP { uint32_t namespace_size, ignore_max_namespace, square_size; };  // rsm_nmt_params
 int main() {
     const int n = 256, S = 512;
     std::vector<uint8_t> buf(n * S);
@@ -20,4 +22,15 @@ int main() {
     for (int r = 0; r < R; ++r) { len = 64; rsm_default_tree_root(nullptr, 0, 0, p.data(), n, S, out, &len); }
     double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / R;
     printf("%.1f us per root; root %02x%02x%02x%02x\n", us, out[0], out[1], out[2], out[3]);
+    // NMT (29-byte namespaces, k = 128, row 7: the first 128 leaves Q0 with ascending namespaces)
+    for (int i = 0; i < n; ++i)
+        for (int b = 0; b < 29; ++b) buf[i * S + b] = b == 28 ? (uint8_t)i : 0;
+    NmtP np{29, 1, 128};
+    uint8_t nout[128];
+    for (int r = 0; r < 50; ++r) { len = 128; rsm_nmt_tree_root(&np, 0, 7, p.data(), n, S, nout, &len); }
+    t0 = std::chrono::steady_clock::now();
+    int rc = 0;
+    for (int r = 0; r < R; ++r) { len = 128; rc |= rsm_nmt_tree_root(&np, 0, 7, p.data(), n, S, nout, &len); }
+    us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / R;
+    printf("NMT: %.1f us per root (rc %d, len %u); digest %02x%02x%02x%02x\n", us, rc, len, nout[58], nout[59], nout[60], nout[61]);
 }
