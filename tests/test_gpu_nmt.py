@@ -71,7 +71,8 @@ def test_with_buffer_error_cases(pool):
         R.ComputeExtendedDataSquareWithBuffer([bytes([i + 1]) * SHARE for i in range(3)], codec, pool)
 
 
-@pytest.mark.parametrize("k,ns,S", [(4, 29, 64), (3, 8, 128), (16, 1, 64), (64, 32, 512), (5, 29, 64)])
+@pytest.mark.parametrize("k,ns,S", [(4, 29, 64), (3, 8, 128), (16, 1, 64), (64, 32, 512), (5, 29, 64), (6, 29, 64),
+                                    (10, 29, 128), (1, 29, 64)])
 def test_nmt_roots_dev_vs_oracle(lib, k, ns, S):
     """rsm_nmt_roots_dev over a device-resident square, bit-exact vs the oracle."""
     ctx = R.device_context(0)
@@ -95,7 +96,7 @@ def test_nmt_roots_dev_vs_oracle(lib, k, ns, S):
 
 
 @pytest.mark.parametrize("k,ns,S,count", [(4, 29, 64, 3), (16, 29, 512, 5), (8, 8, 128, 2), (64, 29, 512, 3),
-                                         (128, 29, 512, 2)])
+                                         (128, 29, 512, 2), (6, 29, 64, 3), (10, 29, 576, 2)])
 def test_nmt_roots_squares_dev_batched(lib, k, ns, S, count):
     """rsm_nmt_roots_squares_dev over a batch of squares (one launch pair) == the
     oracle's roots of every square; one square with an unordered namespace reports its
