@@ -555,9 +555,25 @@ int fast_repair_rows_zero_copy(rsm_eds* e, DevSquare& dev, const std::vector<uin
         }
     } evg{ev};
     hipEvent_t &ev_top = ev[0], &ev_bot = ev[1];
-    if ((r = hipMemcpyAsync(dev.d_pres, e->present.data(), e->present.size(), hipMemcpyHostToDevice, st)) != hipSuccess)
+    // the presence map and the row list go up from the lane's pinned staging: from the
+    // pageable vectors hipMemcpyAsync is a staged, synchronous copy (35 us of host time
+    // for k = 128's 64 KiB map)
+    HostBuf& hb = gv.lane->host;
+    const size_t pres_n = e->present.size();  // W * W: the row list after it stays 4-byte aligned
+    if ((r = hb.ensure(pres_n + todo.size() * 4)) != hipSuccess) return hip_fail(r, "hipHostMalloc (repair staging)");
+    uint8_t* hs = static_cast<uint8_t*>(hb.ptr);
+    memcpy(hs, e->present.data(), pres_n);
+    memcpy(hs + pres_n, todo.data(), todo.size() * 4);
+    struct DrainSt {  // an early return must not hand the lane's staging back with its DMA in flight
+        hipStream_t s;
+        bool armed = true;
+        ~DrainSt() {
+            if (armed) (void)hipStreamSynchronize(s);
+        }
+    } drain_st{st};
+    if ((r = hipMemcpyAsync(dev.d_pres, hs, pres_n, hipMemcpyHostToDevice, st)) != hipSuccess)
         return hip_fail(r, "H2D presence");
-    if ((r = hipMemcpyAsync(dev.d_idx, todo.data(), todo.size() * 4, hipMemcpyHostToDevice, st)) != hipSuccess)
+    if ((r = hipMemcpyAsync(dev.d_idx, hs + pres_n, todo.size() * 4, hipMemcpyHostToDevice, st)) != hipSuccess)
         return hip_fail(r, "H2D indices");
     // a quarter of the CUs (A/B on MI355X, profiles/r02c_repair_ab.txt: 64 workgroups
     // 0.87 ms, 128 0.89 ms, one per task 0.91 ms)
@@ -649,6 +665,7 @@ int fast_repair_rows_zero_copy(rsm_eds* e, DevSquare& dev, const std::vector<uin
                        hipSuccess) ||
         (r = hipStreamSynchronize(sv)) != hipSuccess)
         return hip_fail(r, "verify");
+    drain_st.armed = false;  // sv waited for every st step (ev_top, ev_bot)
     const bool enc_ok = mismatch == 0;
     const bool roots_ok = std::all_of(status.begin(), status.end(), [](uint32_t x) { return x == 0; }) &&
                           memcmp(got.data(), row_roots, (size_t)W * RL) == 0 &&
@@ -673,8 +690,7 @@ int fast_repair(rsm_eds* e, DevSquare& dev, const uint8_t* row_roots, const uint
         bool rows_only = true;
         for (uint32_t i = 0; i < W && rows_only; ++i) {
             const uint8_t* pr = e->present.data() + (size_t)i * W;
-            uint32_t have = 0;
-            for (uint32_t p = 0; p < W; ++p) have += pr[p] ? 1u : 0u;
+            const uint32_t have = W - (uint32_t)std::count(pr, pr + W, uint8_t{0});
             if (have < W) {
                 if (have >= k) todo.push_back(i);
                 else rows_only = false;
@@ -1000,8 +1016,7 @@ int rsm_eds_repair(rsm_eds* e, const uint8_t* row_roots, const uint8_t* col_root
         std::lock_guard<std::mutex> lk(e->ctx->eds_mu);
         if (int rc = dev.init(e->ctx, e->width, e->S)) return rc;
         if (int rc = pre_repair_sanity_check(e, dev, row_roots, col_roots, root_len, tree, byz)) return rc;
-        bool complete = true;
-        for (uint8_t p : e->present) complete = complete && p;
+        const bool complete = memchr(e->present.data(), 0, e->present.size()) == nullptr;
         if (complete) return RSM_OK;  // solveCrossword: solved on the first sweep
         int rc = fast_repair(e, dev, row_roots, col_roots, root_len, tree);
         if (rc <= 0) return rc;

@@ -48,6 +48,8 @@ for i in range(reps):
     R._check_with(LR, LR.rsm_eds_set_context(h, ctx_r))
     byz = R._Byz()
     t0 = time.perf_counter()
+    m0 = time.monotonic_ns()
     R._check_with(LR, LR.rsm_eds_repair(h, roots[0], roots[1], 32, None, None, ctypes.byref(byz)))
-    print(f"repair {i}: {(time.perf_counter() - t0) * 1e3:.3f} ms", flush=True)
+    m1 = time.monotonic_ns()
+    print(f"repair {i}: {(time.perf_counter() - t0) * 1e3:.3f} ms monotonic_ns {m0} {m1}", flush=True)
     LR.rsm_eds_free(h)
