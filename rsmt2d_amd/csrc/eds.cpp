@@ -560,7 +560,12 @@ int fast_repair_rows_zero_copy(rsm_eds* e, DevSquare& dev, const std::vector<uin
     // for k = 128's 64 KiB map)
     HostBuf& hb = gv.lane->host;
     const size_t pres_n = e->present.size();  // W * W: the row list after it stays 4-byte aligned
-    if ((r = hb.ensure(pres_n + todo.size() * 4)) != hipSuccess) return hip_fail(r, "hipHostMalloc (repair staging)");
+    // then, 16-byte aligned, the verification results coming back (mismatch flag, roots,
+    // tree statuses): the same pinned staging, so those copies are asynchronous too
+    const size_t back = (pres_n + todo.size() * 4 + 15) / 16 * 16;
+    const size_t roots_n = (size_t)2 * W * dt.root_len;
+    if ((r = hb.ensure(back + 16 + roots_n + (size_t)2 * W * 4)) != hipSuccess)
+        return hip_fail(r, "hipHostMalloc (repair staging)");
     uint8_t* hs = static_cast<uint8_t*>(hb.ptr);
     memcpy(hs, e->present.data(), pres_n);
     memcpy(hs + pres_n, todo.data(), todo.size() * 4);
@@ -641,9 +646,11 @@ int fast_repair_rows_zero_copy(rsm_eds* e, DevSquare& dev, const std::vector<uin
     (void)hipStreamWaitEvent(sv, ev_bot, 0);
     e->stats.sweeps++;
     e->stats.decoded_vectors += (uint32_t)todo.size();
-    uint32_t mismatch = 1;
-    std::vector<uint8_t> got((size_t)2 * W * RL);
-    std::vector<uint32_t> status((size_t)2 * W, 0);
+    uint32_t* const h_mismatch = reinterpret_cast<uint32_t*>(hs + back);
+    uint8_t* const got = hs + back + 16;
+    uint32_t* const status = reinterpret_cast<uint32_t*>(got + roots_n);
+    *h_mismatch = 1;
+    memset(status, 0, (size_t)2 * W * 4);
     if ((r = hipMemsetAsync(dev.d_flags, 0, 4, sv)) != hipSuccess ||
         (r = launch_compare(dev.d_eds + (size_t)k * row, dev.d_scratch + (size_t)k * row, (uint64_t)k * row,
                             dev.d_flags, sv)) != hipSuccess)
@@ -659,17 +666,16 @@ int fast_repair_rows_zero_copy(rsm_eds* e, DevSquare& dev, const std::vector<uin
                (r = launch_tree_roots(leaf, W, 0, 2 * W, d_roots, sv)) != hipSuccess) {  // latency-bound: one launch
         return hip_fail(r, "verify (roots)");
     }
-    if ((r = hipMemcpyAsync(&mismatch, dev.d_flags, 4, hipMemcpyDeviceToHost, sv)) != hipSuccess ||
-        (r = hipMemcpyAsync(got.data(), d_roots, got.size(), hipMemcpyDeviceToHost, sv)) != hipSuccess ||
-        (dt.nmt && (r = hipMemcpyAsync(status.data(), d_status, status.size() * 4, hipMemcpyDeviceToHost, sv)) !=
-                       hipSuccess) ||
+    if ((r = hipMemcpyAsync(h_mismatch, dev.d_flags, 4, hipMemcpyDeviceToHost, sv)) != hipSuccess ||
+        (r = hipMemcpyAsync(got, d_roots, roots_n, hipMemcpyDeviceToHost, sv)) != hipSuccess ||
+        (dt.nmt && (r = hipMemcpyAsync(status, d_status, (size_t)2 * W * 4, hipMemcpyDeviceToHost, sv)) != hipSuccess) ||
         (r = hipStreamSynchronize(sv)) != hipSuccess)
         return hip_fail(r, "verify");
     drain_st.armed = false;  // sv waited for every st step (ev_top, ev_bot)
-    const bool enc_ok = mismatch == 0;
-    const bool roots_ok = std::all_of(status.begin(), status.end(), [](uint32_t x) { return x == 0; }) &&
-                          memcmp(got.data(), row_roots, (size_t)W * RL) == 0 &&
-                          memcmp(got.data() + (size_t)W * RL, col_roots, (size_t)W * RL) == 0;
+    const bool enc_ok = *h_mismatch == 0;
+    const bool roots_ok = std::all_of(status, status + 2 * W, [](uint32_t x) { return x == 0; }) &&
+                          memcmp(got, row_roots, (size_t)W * RL) == 0 &&
+                          memcmp(got + (size_t)W * RL, col_roots, (size_t)W * RL) == 0;
     if (!enc_ok || !roots_ok) {
         e->stats.fallback_reason = enc_ok ? kFallbackRoots : kFallbackEncoding;
         return 1;
