@@ -570,12 +570,13 @@ int fast_repair_rows_zero_copy(rsm_eds* e, DevSquare& dev, const std::vector<uin
     memcpy(hs, e->present.data(), pres_n);
     memcpy(hs + pres_n, todo.data(), todo.size() * 4);
     struct DrainSt {  // an early return must not hand the lane's staging back with its DMA in flight
-        hipStream_t s;
+        hipStream_t s[2];
         bool armed = true;
         ~DrainSt() {
-            if (armed) (void)hipStreamSynchronize(s);
+            if (armed)
+                for (hipStream_t x : s) (void)hipStreamSynchronize(x);
         }
-    } drain_st{st};
+    } drain_st{{st, sv}};
     if ((r = hipMemcpyAsync(dev.d_pres, hs, pres_n, hipMemcpyHostToDevice, st)) != hipSuccess)
         return hip_fail(r, "H2D presence");
     if ((r = hipMemcpyAsync(dev.d_idx, hs + pres_n, todo.size() * 4, hipMemcpyHostToDevice, st)) != hipSuccess)
