@@ -460,6 +460,13 @@ constexpr uint32_t kNmtTreesPerBlock = 4;  // waves per workgroup of the one-tre
 // WPB waves per workgroup, TPW trees per wave.  F2 (W a multiple of 4): the first pass
 // hashes leaves 4j .. 4j + 3 into level-1 nodes 2j, 2j + 1 and on into level-2 node j,
 // so LDS holds W/4 nodes per tree instead of W/2 (more trees, or more waves, per CU).
+// Once a wave's TPW trees have fewer than 64 nodes in a level, the workgroup's WPB TPW
+// trees are built together (as kernels_sha.hip's COOP form): node U * next + j of the
+// workgroup on lane (U * next + j) mod 64 of wave (U * next + j) / 64, a barrier
+// between a level's reads and its in-place writes, waves past the level's last node
+// idle.  At W = 256, TPW = 2, WPB = 4: 34 wave-passes of three compressions per
+// workgroup of 8 trees instead of 48 (each wave's own top five levels were one pass
+// each for 32 .. 2 nodes).
 template <int NS, int TPW, int WPB, bool F2>
 __global__ __launch_bounds__(64 * WPB) void nmt_tree_wave_kernel(const uint32_t* __restrict__ leaf, uint32_t W,
                                                                  uint32_t ignore_max, uint8_t* __restrict__ roots,
@@ -467,13 +474,22 @@ __global__ __launch_bounds__(64 * WPB) void nmt_tree_wave_kernel(const uint32_t*
     constexpr int kW = WNode<NS>::kW;
     constexpr uint32_t NW = wnode_words<NS>();
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    const uint32_t t0 = (blockIdx.x * WPB + wv) * TPW, count = 2 * W;
-    if (t0 >= count) return;  // whole wave (no workgroup barrier in this kernel)
-    const uint32_t nt = count - t0 < (uint32_t)TPW ? count - t0 : (uint32_t)TPW;
+    const uint32_t tw0 = blockIdx.x * WPB * TPW, count = 2 * W;  // the workgroup's first tree
+    const uint32_t t0 = tw0 + wv * TPW;
+    // waves without trees stay for the workgroup barriers of the upper levels
+    const uint32_t nt = t0 >= count ? 0u : (count - t0 < (uint32_t)TPW ? count - t0 : (uint32_t)TPW);
+    const uint32_t ntw = count - tw0 < (uint32_t)(WPB * TPW) ? count - tw0 : (uint32_t)(WPB * TPW);
+    __shared__ uint32_t wg_bad;  // bit U: workgroup tree U failed
+    if (threadIdx.x == 0) wg_bad = 0;
+    __syncthreads();  // before any wave's atomicOr (a W whose levels need no other barrier)
     leaf += (uint64_t)blockIdx.y * W * W * kLeafWords;
     roots += (uint64_t)blockIdx.y * 2 * W * (2 * NS + 32);
     if (status) status += (uint64_t)blockIdx.y * 2 * W;
     extern __shared__ uint32_t lds_raw[];
+    // workgroup tree U: wave U / TPW's tree U % TPW
+    auto tlvl = [&](uint32_t U) {
+        return lds_raw + (size_t)(U / TPW) * wwave_lds_words<NS>(W, TPW, F2) + (size_t)(U % TPW) * wtree_lds_words<NS>(W, F2);
+    };
     uint32_t* const base = lds_raw + (size_t)wv * wwave_lds_words<NS>(W, TPW, F2);
     auto lvl = [&](uint32_t u) { return base + (size_t)u * wtree_lds_words<NS>(W, F2); };
     uint32_t* const spare = base + (size_t)TPW * wtree_lds_words<NS>(W, F2);
@@ -514,7 +530,7 @@ __global__ __launch_bounds__(64 * WPB) void nmt_tree_wave_kernel(const uint32_t*
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
-    uint32_t bad = 0;  // bit u: tree u of this wave failed (push order / sibling order)
+    uint32_t bad = 0;  // bit U: workgroup tree U failed (push order / sibling order)
     // level 1 from the leaf records (push order checked on every consecutive pair)
     // Every lane hashes in every pass of a level: past the level's last node a lane
     // repeats node v0 + lane % rem and stores it to the wave's spare node (a wave
@@ -544,7 +560,7 @@ __global__ __launch_bounds__(64 * WPB) void nmt_tree_wave_kernel(const uint32_t*
             if (!hash_node_w<NS>(c, d, ig, r)) ok = false;
             if (!hash_node_w<NS>(l, r, ig, o)) ok = false;
             st(own ? lvl(u) + (size_t)j * NW : spare, o);
-            if (own && !ok) bad |= 1u << u;
+            if (own && !ok) bad |= 1u << (wv * TPW + u);
         }
     } else {
         for (uint32_t v0 = 0; v0 < nt * next; v0 += 64u) {
@@ -568,12 +584,38 @@ __global__ __launch_bounds__(64 * WPB) void nmt_tree_wave_kernel(const uint32_t*
                 o = a;
             }
             st(own ? lvl(u) + (size_t)j * NW : spare, o);
-            if (own && !ok) bad |= 1u << u;
+            if (own && !ok) bad |= 1u << (wv * TPW + u);
         }
     }
     wave_sync();
     for (cnt = next; cnt > 1; cnt = next) {
         next = (cnt + 1) / 2;
+        if ((uint32_t)TPW * next < 64u) {
+            // the workgroup's trees together: at most one pass per wave (WPB TPW next < 64 WPB)
+            const uint32_t tot = ntw * next, v0 = wv * 64u;
+            __syncthreads();  // the previous level's nodes (any wave's) are written
+            uint32_t U = 0, j = 0;
+            bool own = false;
+            WNode<NS> o;
+            if (v0 < tot) {
+                const uint32_t rem = tot - v0;  // every lane of a working wave hashes
+                own = lane < rem;
+                const uint32_t v = v0 + (own ? lane : lane % rem);
+                U = v / next;
+                j = v - U * next;
+                WNode<NS> a, b;
+                ld(tlvl(U) + (size_t)(2 * j) * NW, a);
+                if (2 * j + 1 < cnt) {
+                    ld(tlvl(U) + (size_t)(2 * j + 1) * NW, b);
+                    if (!hash_node_w<NS>(a, b, ig, o) && own) bad |= 1u << U;
+                } else {
+                    o = a;
+                }
+            }
+            __syncthreads();  // every read of this level precedes its in-place writes
+            if (v0 < tot) st(own ? tlvl(U) + (size_t)j * NW : spare, o);
+            continue;
+        }
         for (uint32_t v0 = 0; v0 < nt * next; v0 += 64u) {
             const uint32_t rem = nt * next - v0;
             const bool own = lane < rem;
@@ -583,7 +625,7 @@ __global__ __launch_bounds__(64 * WPB) void nmt_tree_wave_kernel(const uint32_t*
             ld(lvl(u) + (size_t)(2 * j) * NW, a);
             if (2 * j + 1 < cnt) {
                 ld(lvl(u) + (size_t)(2 * j + 1) * NW, b);
-                if (!hash_node_w<NS>(a, b, ig, o) && own) bad |= 1u << u;
+                if (!hash_node_w<NS>(a, b, ig, o) && own) bad |= 1u << (wv * TPW + u);
             } else {
                 o = a;
             }
@@ -592,10 +634,13 @@ __global__ __launch_bounds__(64 * WPB) void nmt_tree_wave_kernel(const uint32_t*
         }
         wave_sync();
     }
-    // OR of the lanes' failure bits per tree
+    // OR of every lane's failure bits, per workgroup tree
     uint32_t all = bad;
 #pragma unroll
     for (int sft = 1; sft < 64; sft <<= 1) all |= __shfl_xor(all, sft);
+    if (lane == 0 && all) atomicOr(&wg_bad, all);
+    __syncthreads();  // the roots (written by any wave) and wg_bad
+    all = wg_bad >> (wv * TPW);
     if (lane < nt) {
         const uint32_t tree = t0 + lane;
         WNode<NS> rt;

@@ -97,19 +97,32 @@ __host__ __device__ constexpr uint32_t tree_lds_words(uint32_t W) { return (W / 
 // level-by-level workgroup form left most lanes idle behind __syncthreads: 3x
 // slower).  roots: [squares][2][W][32] bytes (big-endian digest bytes, as
 // Tree.Root() returns them).
-template <int TPW>
+// COOP (batches): once a wave's TPW trees have fewer than 64 nodes in a level, the
+// workgroup's 4 TPW trees are built together instead -- node U * cnt + j of the
+// workgroup (tree U, whose LDS is U tree-slots from the workgroup's first) on lane
+// (U * cnt + j) mod 64 of wave (U * cnt + j) / 64, a barrier between a level's reads
+// and its writes, waves past the level's last node idle.  At W = 256 and TPW = 2 the
+// workgroup then issues 34 wave-passes of two compressions for its 8 trees instead
+// of 48 (each wave's own top five levels were one pass each for 32 .. 2 nodes), and
+// a SIMD's SHA throughput is its issued wave-passes (kernels_sha.hip above).  A
+// latency launch (one square) keeps COOP off: its depth is the same either way.
+template <int TPW, bool COOP>
 __global__ __launch_bounds__(256) void tree_root_kernel(const uint32_t* __restrict__ leaf, uint32_t W,
                                                         uint8_t* __restrict__ roots, uint32_t first, uint32_t count) {
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    const uint32_t t0 = (blockIdx.x * kTreesPerBlock + wv) * TPW;
-    if (t0 >= count) return;  // whole wave (the kernel has no workgroup barrier)
-    const uint32_t nt = count - t0 < (uint32_t)TPW ? count - t0 : (uint32_t)TPW;
+    const uint32_t tw0 = blockIdx.x * kTreesPerBlock * TPW;  // the workgroup's first tree
+    const uint32_t t0 = tw0 + wv * TPW;
+    if (!COOP && t0 >= count) return;  // whole wave (no workgroup barrier without COOP)
+    const uint32_t nt = t0 >= count ? 0u : (count - t0 < (uint32_t)TPW ? count - t0 : (uint32_t)TPW);
+    const uint32_t ntw = count - tw0 < kTreesPerBlock * TPW ? count - tw0 : kTreesPerBlock * TPW;
     leaf += (uint64_t)blockIdx.y * W * W * 8u;
     roots += (uint64_t)blockIdx.y * 2u * W * 32u;
     extern __shared__ uint32_t lds_raw[];
-    uint32_t* const base = lds_raw + (size_t)wv * TPW * tree_lds_words(W);
-    auto lvl = [&](uint32_t u) { return base + (size_t)u * tree_lds_words(W); };
-    auto sub = [&](uint32_t u) { return lvl(u) + (W / 2) * 8u; };
+    // tree U of the workgroup (wave U / TPW, its tree U % TPW)
+    auto tlvl = [&](uint32_t U) { return lds_raw + (size_t)U * tree_lds_words(W); };
+    auto tsub = [&](uint32_t U) { return tlvl(U) + (W / 2) * 8u; };
+    auto lvl = [&](uint32_t u) { return tlvl(wv * TPW + u); };
+    auto sub = [&](uint32_t u) { return tsub(wv * TPW + u); };
     const uint32_t n = W;
     auto leaf_at = [&](uint32_t tree, uint32_t pos, uint32_t (&d)[8]) {
         const uint32_t axis = tree >= W ? 1u : 0u, idx = tree - axis * W;
@@ -117,6 +130,31 @@ __global__ __launch_bounds__(256) void tree_root_kernel(const uint32_t* __restri
         const v4u* s = reinterpret_cast<const v4u*>(leaf + cell * 8u);
         const v4u a = s[0], b = s[1];
         d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w; d[4] = b.x; d[5] = b.y; d[6] = b.z; d[7] = b.w;
+    };
+    // children 2j, 2j + 1 of node j of workgroup tree U at height hgt
+    auto children = [&](uint32_t U, uint32_t j, uint32_t hgt, uint32_t (&L)[8], uint32_t (&R)[8]) {
+        if (hgt == 1) {
+            leaf_at(tw0 + first + U, 2 * j, L);
+            leaf_at(tw0 + first + U, 2 * j + 1, R);
+        } else {
+            const uint32_t* lv = tlvl(U);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                L[i] = lv[(2 * j) * 8u + i];
+                R[i] = lv[(2 * j + 1) * 8u + i];
+            }
+        }
+    };
+    // node j of workgroup tree U (own: this lane's node; else a repeat, to the spare
+    // slot); the last node of an odd level is also the carried subtree of its height
+    auto put = [&](uint32_t U, uint32_t j, uint32_t hgt, uint32_t cnt, bool own, const uint32_t (&o)[8]) {
+        uint32_t* dst = own ? tlvl(U) + j * 8u : tsub(U) + 15u * 8u;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) dst[i] = o[i];
+        if (own && (cnt & 1u) && j == cnt - 1) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) tsub(U)[hgt * 8u + i] = o[i];
+        }
     };
     auto wave_sync = [] {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -130,7 +168,28 @@ __global__ __launch_bounds__(256) void tree_root_kernel(const uint32_t* __restri
         for (int i = 0; i < 8; ++i) sub(lane)[i] = d[i];
     }
     for (uint32_t hgt = 1; (n >> hgt) > 0; ++hgt) {
-        const uint32_t cnt = n >> hgt, tot = nt * cnt;
+        const uint32_t cnt = n >> hgt;
+        if (COOP && (uint32_t)TPW * cnt < 64u) {
+            // the workgroup's trees together: at most one pass per wave (4 TPW cnt < 256)
+            const uint32_t tot = ntw * cnt, v0 = wv * 64u;
+            __syncthreads();  // the previous level's nodes (any wave's) are written
+            uint32_t U = 0, j = 0, o[8];
+            bool own = false;
+            if (v0 < tot) {
+                const uint32_t rem = tot - v0;  // every lane of a working wave hashes, as below
+                own = lane < rem;
+                const uint32_t v = v0 + (own ? lane : lane % rem);
+                U = v / cnt;
+                j = v - U * cnt;
+                uint32_t L[8], R[8];
+                children(U, j, hgt, L, R);
+                node_hash(L, R, o);
+            }
+            __syncthreads();  // every read of this level precedes its in-place writes
+            if (v0 < tot) put(U, j, hgt, cnt, own, o);
+            continue;
+        }
+        const uint32_t tot = nt * cnt;
         for (uint32_t v0 = 0; v0 < tot; v0 += 64u) {
             // Every lane hashes: past the level's last node a lane repeats node
             // v0 + lane % rem and stores it to the tree's spare slot (sub slot 15:
@@ -144,27 +203,15 @@ __global__ __launch_bounds__(256) void tree_root_kernel(const uint32_t* __restri
             const uint32_t v = v0 + (own ? lane : lane % rem);
             const uint32_t u = v / cnt, j = v - u * cnt;
             uint32_t L[8], R[8], o[8];
-            if (hgt == 1) {
-                leaf_at(t0 + first + u, 2 * j, L);
-                leaf_at(t0 + first + u, 2 * j + 1, R);
-            } else {
-                const uint32_t* lv = lvl(u);
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    L[i] = lv[(2 * j) * 8u + i];
-                    R[i] = lv[(2 * j + 1) * 8u + i];
-                }
-            }
+            children(wv * TPW + u, j, hgt, L, R);
             node_hash(L, R, o);
-            uint32_t* dst = own ? lvl(u) + j * 8u : sub(u) + 15u * 8u;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) dst[i] = o[i];
-            if (own && ((n >> hgt) & 1u) && j == cnt - 1) {
-#pragma unroll
-                for (int i = 0; i < 8; ++i) sub(u)[hgt * 8u + i] = o[i];
-            }
+            put(wv * TPW + u, j, hgt, cnt, own, o);
         }
         wave_sync();
+    }
+    if constexpr (COOP) {
+        __syncthreads();  // the top levels' nodes and carried subtrees, from any wave
+        if (nt == 0) return;
     }
     {  // fold the carried subtrees (a W that is not a power of two); all lanes, as above
         const uint32_t ul = lane % nt;
@@ -211,11 +258,15 @@ hipError_t launch_tree_kernel(const uint32_t* d_leaf, uint32_t W, uint8_t* d_roo
     const uint32_t tpw = latency ? 1u : trees_per_wave(W);
     const uint32_t blocks = (count + kTreesPerBlock * tpw - 1) / (kTreesPerBlock * tpw);
     const size_t lds = (size_t)kTreesPerBlock * tpw * tree_lds_words(W) * 4u;
-    switch (tpw) {
-        case 4: hipLaunchKernelGGL(tree_root_kernel<4>, dim3(blocks, squares), dim3(256), lds, st, d_leaf, W, d_roots, first, count); break;
-        case 2: hipLaunchKernelGGL(tree_root_kernel<2>, dim3(blocks, squares), dim3(256), lds, st, d_leaf, W, d_roots, first, count); break;
-        default: hipLaunchKernelGGL(tree_root_kernel<1>, dim3(blocks, squares), dim3(256), lds, st, d_leaf, W, d_roots, first, count); break;
-    }
+    const dim3 grid(blocks, squares);
+    if (latency)
+        hipLaunchKernelGGL((tree_root_kernel<1, false>), grid, dim3(256), lds, st, d_leaf, W, d_roots, first, count);
+    else if (tpw == 4)
+        hipLaunchKernelGGL((tree_root_kernel<4, true>), grid, dim3(256), lds, st, d_leaf, W, d_roots, first, count);
+    else if (tpw == 2)
+        hipLaunchKernelGGL((tree_root_kernel<2, true>), grid, dim3(256), lds, st, d_leaf, W, d_roots, first, count);
+    else
+        hipLaunchKernelGGL((tree_root_kernel<1, true>), grid, dim3(256), lds, st, d_leaf, W, d_roots, first, count);
     return hipGetLastError();
 }
 

@@ -1,7 +1,8 @@
 // nmtprobe.hip -- kernels_nmt.hip's nmt_tree_wave_kernel<29, TPW, WPB, F2> over a batch of
 // 32 squares' leaf records (W = 256, random leaves: push-order statuses are set, the
 // hashing is the same), per shape: trees per wave, waves per workgroup, levels 1-2 fused.
-// hip-event averages over back-to-back launches.  usage: nmtprobe
+// hip-event averages over back-to-back launches (the upper levels workgroup-cooperative
+// since r05aj, so every shape differs from its r05aa figure).  usage: nmtprobe
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <vector>

@@ -57,10 +57,11 @@ def test_eds_roots_device_path(lib, rng):
     assert eds.ColRoots() == sq.roots(crossword.Col)
 
 
-def test_batched_roots_match_per_square(lib):
-    """rsm_roots_squares_dev over 3 squares == rsm_roots_dev of each (pinned above)."""
-    W, S, n = 24, 64, 3
-    eds = oracle.splitmix64_bytes(n * W * W * S, seed=77).reshape(n, W, W, S)
+@pytest.mark.parametrize("W,S,n", [(24, 64, 3), (2, 64, 5), (6, 64, 3), (10, 128, 2), (200, 64, 3), (256, 64, 3)])
+def test_batched_roots_match_per_square(lib, W, S, n):
+    """rsm_roots_squares_dev over n squares (the batch form: workgroup-cooperative upper
+    levels) == rsm_roots_dev of each (the one-square form, pinned above)."""
+    eds = oracle.splitmix64_bytes(n * W * W * S, seed=77 + W).reshape(n, W, W, S)
     buf = R.DeviceBuffer(eds.nbytes)
     buf.upload(np.ascontiguousarray(eds))
     out = R.DeviceBuffer(n * 2 * W * 32)
