@@ -62,6 +62,10 @@ int rsm_diag_set_dec8_mode(uint32_t mode);
 /* Codec calls (rsm_encode / rsm_decode) spin on hipStreamQuery for up to `us`
  * microseconds before blocking in hipStreamSynchronize (0: block at once, production). */
 int rsm_diag_set_codec_spin(uint32_t us);
+/* Zero-copy Repair A/B: 1 = the sweep as two launches (top half, then bottom half; the
+ * column re-encode of the top half overlapping the bottom sweep); 0 = production (one
+ * sweep launch over all rows, the re-encode behind it). */
+int rsm_diag_set_repair_mode(uint32_t mode);
 /* Both passes of `count` in-place k = 128 squares in ONE persistent launch
  * (extend_gf8_bs128q_kernel: row and Q0-column sets from one queue, Q1-column sets
  * from a ready list; `delay` squares of row sets lead the Q0-column sets).

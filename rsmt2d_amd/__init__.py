@@ -202,6 +202,7 @@ DIAG_SIGNATURES = {
     "rsm_diag_set_dec_delay": (_I32, [ctypes.c_uint32]),
     "rsm_diag_set_dec8_mode": (_I32, [ctypes.c_uint32]),
     "rsm_diag_set_codec_spin": (_I32, [ctypes.c_uint32]),
+    "rsm_diag_set_repair_mode": (_I32, [ctypes.c_uint32]),
     "rsm_diag_set_dec16_mode": (_I32, [ctypes.c_uint32]),
     "rsm_diag_set_bs_row_mode": (_I32, [ctypes.c_int]),
     "rsm_diag_extend_fused": (_I32, [_VP, _VP, _U32, _U32, _U32, _U32, _VP]),

@@ -88,6 +88,19 @@ struct rsm_eds {
     uint32_t cc(int axis, uint32_t idx, uint32_t pos) const { return axis == RSM_AXIS_ROW ? pos : idx; }
 };
 
+// Repair A/B (diagnostic builds): 1 = the zero-copy sweep as two launches, top half then
+// bottom half, the column re-encode of the top half overlapping the bottom sweep (the
+// form up to r05am); production: one launch, the re-encode behind all of it
+#ifdef RSM_DIAG
+static std::atomic<uint32_t> g_repair_mode{0};
+namespace rsm {
+void set_repair_diag_mode(uint32_t m) { g_repair_mode.store(m); }
+}  // namespace rsm
+static uint32_t repair_mode() { return g_repair_mode.load(); }
+#else
+static uint32_t repair_mode() { return 0; }
+#endif
+
 namespace {
 
 uint32_t get_width(uint64_t n) {  // datasquare.go:35-37
@@ -521,14 +534,16 @@ int fast_repair_rows_zero_copy(rsm_eds* e, DevSquare& dev, const std::vector<uin
     // memory reach the copy engine's ~57 GB/s, and reads plus writes together ~73
     // GB/s, more than the copy engine's duplex): only the present cells go up and
     // only the rebuilt cells come back.  The decoder runs on a capped grid so its
-    // stores of one task drain while the loads of its next task arrive.  Two sweeps
-    // (top half, bottom half) on st; the verification stream sv starts on the top
-    // half while the bottom half is still crossing PCIe:
-    //   the columns of the top half are re-encoded and compared with the bottom half
+    // stores of one task drain while the loads of its next task arrive -- ONE sweep
+    // launch over every row (two launches, top half then bottom half so that the
+    // verification could start on the top half, were 9 % slower end to end: each
+    // launch's tail leaves the link half idle; profiles/r05an_repair_sweep_ab.jsonl).
+    // Then, beside each other:
+    //   sv: the columns of the top half are re-encoded and compared with the bottom half
     //   (every row is a codeword by construction, so this makes the square a valid 2D
     //   codeword: the reference's verifyEncoding of each completed column,
-    //   extendeddatacrossword.go:184), then the DefaultTree roots of all 2W vectors
-    //   (verifyAgainstRowRoots / ColRoots, :153, :173).
+    //   extendeddatacrossword.go:184);
+    //   st: the roots of all 2W vectors (verifyAgainstRowRoots / ColRoots, :153, :173).
     hipStream_t st = dev.st;
     LaneGuard gv(dev.ctx);
     if (!gv.lane) return gv.rc;
@@ -567,6 +582,12 @@ int fast_repair_rows_zero_copy(rsm_eds* e, DevSquare& dev, const std::vector<uin
     if ((r = hb.ensure(back + 16 + roots_n + (size_t)2 * W * 4)) != hipSuccess)
         return hip_fail(r, "hipHostMalloc (repair staging)");
     uint8_t* hs = static_cast<uint8_t*>(hb.ptr);
+    void* hs_map = nullptr;  // the staging's device address: the DefaultTree roots and the
+                             // mismatch flag are written there by the kernels themselves
+    if ((r = hipHostGetDevicePointer(&hs_map, hs, 0)) != hipSuccess || !hs_map) {
+        (void)hipGetLastError();
+        return 1;
+    }
     memcpy(hs, e->present.data(), pres_n);
     memcpy(hs + pres_n, todo.data(), todo.size() * 4);
     struct DrainSt {  // an early return must not hand the lane's staging back with its DMA in flight
@@ -618,16 +639,34 @@ int fast_repair_rows_zero_copy(rsm_eds* e, DevSquare& dev, const std::vector<uin
         }
         return RSM_OK;
     };
-    size_t split = 0;
-    while (split < todo.size() && todo[split] < k) ++split;
-    if (int rc = upload_complete(0, k, 0)) return rc;
+    const bool halves = repair_mode() == 1;  // (diagnostic A/B: the two-launch form)
+    size_t split = todo.size();
+    if (halves) {
+        split = 0;
+        while (split < todo.size() && todo[split] < k) ++split;
+    }
+    if (int rc = upload_complete(0, halves ? k : W, 0)) return rc;
     if (int rc = sweep(0, split)) return rc;
-    (void)hipEventRecord(ev_top, st);
-    if (int rc = upload_complete(k, W, split)) return rc;
-    if (int rc = sweep(split, todo.size())) return rc;
+    if (halves) {
+        (void)hipEventRecord(ev_top, st);
+        if (int rc = upload_complete(k, W, split)) return rc;
+        if (int rc = sweep(split, todo.size())) return rc;
+    }
     (void)hipEventRecord(ev_bot, st);
-    // verification
-    (void)hipStreamWaitEvent(sv, ev_top, 0);
+    // verification.  sv: the column re-encode of the top half and the encoding compare;
+    // st, right behind its own sweep: the leaf digests of the WHOLE square and the trees.  (A cross-queue
+    // wait costs 11-12 us on the critical path even when its event has long completed,
+    // and one leaf launch is latency-bound -- 9 compressions per cell, one wave per SIMD
+    // for the whole square -- so hashing the top half early on sv saved nothing:
+    // profiles/r05al_repair_tail.txt.)  The mismatch flag and the DefaultTree roots land
+    // in the pinned staging straight from the kernels.
+    uint32_t* const h_mismatch = reinterpret_cast<uint32_t*>(hs + back);
+    uint8_t* const got = hs + back + 16;
+    uint32_t* const status = reinterpret_cast<uint32_t*>(got + roots_n);
+    uint8_t* const got_map = static_cast<uint8_t*>(hs_map) + back + 16;
+    *h_mismatch = 0;
+    memset(status, 0, (size_t)2 * W * 4);
+    (void)hipStreamWaitEvent(sv, halves ? ev_top : ev_bot, 0);  // (one event record on st)
     CodewordSet cols{};
     cols.base = dev.d_eds;
     cols.out_base = dev.d_scratch;
@@ -641,38 +680,30 @@ int fast_repair_rows_zero_copy(rsm_eds* e, DevSquare& dev, const std::vector<uin
     cols.S = e->S;
     cols.pass = 1;
     if (int rc = launch_encode(dev.ctx, cols, sv)) return rc;
-    // DefaultTree: the top half's leaf digests while the bottom half is in flight
-    if (!dt.nmt && (r = launch_leaf_hashes(dev.d_eds, k * W, e->S, leaf, sv)) != hipSuccess)
-        return hip_fail(r, "leaf hashes");
-    (void)hipStreamWaitEvent(sv, ev_bot, 0);
+    if (halves) (void)hipStreamWaitEvent(sv, ev_bot, 0);
     e->stats.sweeps++;
     e->stats.decoded_vectors += (uint32_t)todo.size();
-    uint32_t* const h_mismatch = reinterpret_cast<uint32_t*>(hs + back);
-    uint8_t* const got = hs + back + 16;
-    uint32_t* const status = reinterpret_cast<uint32_t*>(got + roots_n);
-    *h_mismatch = 1;
-    memset(status, 0, (size_t)2 * W * 4);
-    if ((r = hipMemsetAsync(dev.d_flags, 0, 4, sv)) != hipSuccess ||
-        (r = launch_compare(dev.d_eds + (size_t)k * row, dev.d_scratch + (size_t)k * row, (uint64_t)k * row,
-                            dev.d_flags, sv)) != hipSuccess)
+    if ((r = launch_compare(dev.d_eds + (size_t)k * row, dev.d_scratch + (size_t)k * row, (uint64_t)k * row,
+                            reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(hs_map) + back), sv)) != hipSuccess)
         return hip_fail(r, "verify (encoding)");
     if (dt.nmt) {
         // namespaced trees: leaves and nodes of the whole square in one launch pair
-        // (leaf scratch: sv's StreamScratch, held above)
+        // (leaf scratch: sv's StreamScratch, held above for the whole call, both streams
+        // drained before it is released); byte-wise root stores, so
+        // they come back by copy
         if ((r = launch_nmt_roots(dev.d_eds, W, e->S, dt.p.namespace_size, dt.p.square_size, dt.p.ignore_max_namespace,
-                                  leaf, d_roots, d_status, sv)) != hipSuccess)
+                                  leaf, d_roots, d_status, st)) != hipSuccess)
             return hip_fail(r, "NMT roots");
-    } else if ((r = launch_leaf_hashes(dev.d_eds + (size_t)k * row, k * W, e->S, leaf + (size_t)k * W * 8, sv)) !=
-                   hipSuccess ||
-               (r = launch_tree_roots(leaf, W, 0, 2 * W, d_roots, sv)) != hipSuccess) {  // latency-bound: one launch
+        if ((r = hipMemcpyAsync(got, d_roots, roots_n, hipMemcpyDeviceToHost, st)) != hipSuccess ||
+            (r = hipMemcpyAsync(status, d_status, (size_t)2 * W * 4, hipMemcpyDeviceToHost, st)) != hipSuccess)
+            return hip_fail(r, "verify (NMT roots)");
+    } else if ((r = launch_leaf_hashes(dev.d_eds, W * W, e->S, leaf, st)) != hipSuccess ||
+               (r = launch_tree_roots(leaf, W, 0, 2 * W, got_map, st)) != hipSuccess) {  // latency-bound: one launch
         return hip_fail(r, "verify (roots)");
     }
-    if ((r = hipMemcpyAsync(h_mismatch, dev.d_flags, 4, hipMemcpyDeviceToHost, sv)) != hipSuccess ||
-        (r = hipMemcpyAsync(got, d_roots, roots_n, hipMemcpyDeviceToHost, sv)) != hipSuccess ||
-        (dt.nmt && (r = hipMemcpyAsync(status, d_status, (size_t)2 * W * 4, hipMemcpyDeviceToHost, sv)) != hipSuccess) ||
-        (r = hipStreamSynchronize(sv)) != hipSuccess)
+    if ((r = hipStreamSynchronize(st)) != hipSuccess || (r = hipStreamSynchronize(sv)) != hipSuccess)
         return hip_fail(r, "verify");
-    drain_st.armed = false;  // sv waited for every st step (ev_top, ev_bot)
+    drain_st.armed = false;  // both streams drained
     const bool enc_ok = *h_mismatch == 0;
     const bool roots_ok = std::all_of(status, status + 2 * W, [](uint32_t x) { return x == 0; }) &&
                           memcmp(got, row_roots, (size_t)W * RL) == 0 &&

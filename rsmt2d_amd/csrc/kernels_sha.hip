@@ -231,10 +231,16 @@ __global__ __launch_bounds__(256) void tree_root_kernel(const uint32_t* __restri
 #pragma unroll
             for (int i = 0; i < 8; ++i) acc[i] = o[i];
         }
-        if (lane < nt) {
-            uint32_t* r = reinterpret_cast<uint32_t*>(roots + ((uint64_t)axis * W + idx) * 32u);
+        // lane ul + nt i writes word i of its tree's root: one store instruction covers the
+        // wave's nt consecutive roots (coalesced -- also when `roots` is host memory, as
+        // Repair's checks pass it)
+        const uint32_t wi = lane / nt;
+        if (wi < 8u) {
+            uint32_t x = acc[0];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) r[i] = __builtin_bswap32(acc[i]);
+            for (int i = 1; i < 8; ++i) x = wi == (uint32_t)i ? acc[i] : x;
+            uint32_t* r = reinterpret_cast<uint32_t*>(roots + ((uint64_t)axis * W + idx) * 32u);
+            r[wi] = __builtin_bswap32(x);
         } else {
 #pragma unroll
             for (int i = 0; i < 8; ++i) sub(ul)[15u * 8u + i] = acc[i];  // keeps every lane hashing

@@ -104,6 +104,11 @@ int rsm_diag_set_codec_spin(uint32_t us) {
     return RSM_OK;
 }
 
+int rsm_diag_set_repair_mode(uint32_t mode) {
+    set_repair_diag_mode(mode);
+    return RSM_OK;
+}
+
 int rsm_diag_set_bs_row_mode(int mode) {
     set_bs128_diag_row_mode(mode);
     return RSM_OK;

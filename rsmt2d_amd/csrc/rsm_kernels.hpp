@@ -101,6 +101,7 @@ constexpr int kDec16TraceWords = 16;
 void set_dec_diag_delay(uint32_t ticks);
 void set_dec8_diag_mode(uint32_t mode);  // diagnostic builds only: 1 = the other split-decoder locator form
 void set_codec_spin_diag(uint32_t us);  // diagnostic builds only (rsm_runtime.cpp)
+void set_repair_diag_mode(uint32_t m);  // diagnostic builds only (eds.cpp)
 
 hipError_t launch_encode_gf8(const CodewordSet& cs, hipStream_t st);
 // wide forms of the byte-table GF(2^8) kernels (any k <= 128): 64-bit per-symbol

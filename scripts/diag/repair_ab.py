@@ -4,7 +4,7 @@ through rsm_eds_repair (zero-copy sweeps); every repaired square is compared wit
 original.  One JSON line per (k, rep).  The A/B lines in profiles/r05h_repair_transport_ab.jsonl
 (split transport) and profiles/r05t_repair_concurrent_ab.jsonl (the halves on two lanes)
 were taken with diagnostic modes of rsm_eds_repair that were removed once measured slower.
-REPAB_KS picks the k values.
+REPAB_KS picks the k values, REPAB_MODES the rsm_diag_set_repair_mode values (default 0).
 usage: python3 scripts/diag/repair_ab.py"""
 import ctypes
 import json
@@ -59,7 +59,8 @@ def main():
         fptrs[present.reshape(-1) == 0] = 0
         reps = int(os.environ.get("REPAB_REPS", "5"))
         for rep in range(2):
-            for mode in (0,):
+            for mode in [int(x) for x in os.environ.get("REPAB_MODES", "0").split(",")]:
+                chk(D.rsm_diag_set_repair_mode(mode))
                 times, fast, ok = [], 0, True
                 for i in range(reps):
                     h = ctypes.c_void_p()
@@ -80,6 +81,7 @@ def main():
                                   "repair_ms_p50": round(sorted(times)[len(times) // 2] * 1e3, 3),
                                   "repair_ms_min": round(min(times) * 1e3, 3), "fast_path": fast,
                                   "repaired_equal": ok}), flush=True)
+    chk(D.rsm_diag_set_repair_mode(0))
 
 
 if __name__ == "__main__":
