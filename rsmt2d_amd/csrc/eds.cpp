@@ -256,7 +256,9 @@ struct DevSquare {
         DevBuf& ix = c->eds.idx;
         DevBuf& fl = c->eds.flags;
         if ((e = a.ensure(sq)) != hipSuccess || (e = b.ensure(sq)) != hipSuccess ||
-            (e = p.ensure((size_t)W * W + 64)) != hipSuccess || (e = ix.ensure(sizeof(uint32_t) * (2 * W + 16))) != hipSuccess ||
+            // presence map, then (zero-copy fast path) its row list: one staged copy
+            (e = p.ensure((size_t)W * W + sizeof(uint32_t) * (2 * W + 16) + 64)) != hipSuccess ||
+            (e = ix.ensure(sizeof(uint32_t) * (2 * W + 16))) != hipSuccess ||
             (e = fl.ensure(sizeof(uint32_t) * (2 * W + 16))) != hipSuccess)
             return hip_fail(e, "hipMalloc (repair square)");
         d_eds = static_cast<uint8_t*>(a.ptr);
@@ -598,10 +600,12 @@ int fast_repair_rows_zero_copy(rsm_eds* e, DevSquare& dev, const std::vector<uin
                 for (hipStream_t x : s) (void)hipStreamSynchronize(x);
         }
     } drain_st{{st, sv}};
-    if ((r = hipMemcpyAsync(dev.d_pres, hs, pres_n, hipMemcpyHostToDevice, st)) != hipSuccess)
-        return hip_fail(r, "H2D presence");
-    if ((r = hipMemcpyAsync(dev.d_idx, hs + pres_n, todo.size() * 4, hipMemcpyHostToDevice, st)) != hipSuccess)
-        return hip_fail(r, "H2D indices");
+    // presence map and row list in one copy kernel on st, read through the staging's
+    // device mapping (a copy-engine transfer put a 10-16 us cross-engine wait in front of
+    // the sweep); the row list lands right behind the map in the same device buffer
+    if ((r = launch_stage_copy(dev.d_pres, hs_map, pres_n + todo.size() * 4, st)) != hipSuccess)
+        return hip_fail(r, "stage presence and rows");
+    const uint32_t* const d_rows = reinterpret_cast<const uint32_t*>(dev.d_pres + pres_n);
     // a quarter of the CUs (A/B on MI355X, profiles/r02c_repair_ab.txt: 64 workgroups
     // 0.87 ms, 128 0.89 ms, one per task 0.91 ms)
     const uint32_t zc_grid = dev.ctx->cus / 4 ? dev.ctx->cus / 4 : 1;
@@ -613,7 +617,7 @@ int fast_repair_rows_zero_copy(rsm_eds* e, DevSquare& dev, const std::vector<uin
         DecodeSet ds{};
         ds.base = dev.d_eds;
         ds.presence = dev.d_pres;
-        ds.indices = dev.d_idx + t0;
+        ds.indices = d_rows + t0;
         ds.count = (uint32_t)(t1 - t0);
         ds.axis = RSM_AXIS_ROW;
         ds.k = k;

@@ -40,6 +40,24 @@ __global__ __launch_bounds__(256) void compare_kernel(const uint4* a, const uint
     if (__any(diff != 0) && (threadIdx.x & 63u) == 0) *mismatch = 1u;
 }
 
+// dst = src, 16-byte words (the byte count rounded up): a pinned host buffer, through its
+// device mapping, into device memory as a kernel on the caller's stream.  Repair stages
+// its presence map and row list this way: a copy-engine transfer put a cross-engine
+// wait of 10-16 us in front of the sweep kernel (profiles/r05ap_repair_stage.txt).
+__global__ __launch_bounds__(256) void stage_copy_kernel(uint4* dst, const uint4* src, uint64_t n16) {
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * 256ull) dst[i] = src[i];
+}
+
+hipError_t launch_stage_copy(void* dst, const void* src, uint64_t bytes, hipStream_t st) {
+    const uint64_t n16 = (bytes + 15) / 16;
+    if (n16 == 0) return hipSuccess;
+    uint64_t blocks = (n16 + 255) / 256;
+    if (blocks > 1024) blocks = 1024;
+    hipLaunchKernelGGL(stage_copy_kernel, dim3((uint32_t)blocks), dim3(256), 0, st, static_cast<uint4*>(dst),
+                       static_cast<const uint4*>(src), n16);
+    return hipGetLastError();
+}
+
 hipError_t launch_compare(const uint8_t* a, const uint8_t* b, uint64_t n, uint32_t* mismatch,
                           hipStream_t st) {
     const uint64_t n16 = n / 16;

@@ -150,6 +150,8 @@ hipError_t launch_tree_roots(const uint32_t* d_leaf, uint32_t W, uint32_t first,
                              hipStream_t st);
 hipError_t launch_fill_random(void* p, uint64_t bytes, uint64_t seed, hipStream_t st);
 hipError_t launch_compare(const uint8_t* a, const uint8_t* b, uint64_t n, uint32_t* mismatch, hipStream_t st);
+// dst = src for ceil(bytes / 16) 16-byte words (src: e.g. a pinned buffer's device mapping)
+hipError_t launch_stage_copy(void* dst, const void* src, uint64_t bytes, hipStream_t st);
 hipError_t launch_compare_parity(const uint8_t* a, const uint8_t* b, uint32_t k, uint32_t S, uint32_t axis,
                                  const uint32_t* indices, uint32_t count, uint32_t* flags, hipStream_t st);
 

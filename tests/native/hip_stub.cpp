@@ -202,6 +202,10 @@ hipError_t launch_fill_random(void* p, uint64_t bytes, uint64_t seed, hipStream_
     memset(p, (int)(seed & 0xFF), bytes);
     return hipSuccess;
 }
+hipError_t launch_stage_copy(void* dst, const void* src, uint64_t bytes, hipStream_t) {
+    memcpy(dst, src, (bytes + 15) / 16 * 16);
+    return hipSuccess;
+}
 hipError_t launch_compare(const uint8_t* a, const uint8_t* b, uint64_t n, uint32_t* mismatch, hipStream_t) {
     *mismatch = memcmp(a, b, n) != 0;
     return hipSuccess;
