@@ -804,30 +804,33 @@ int rsm_decode(rsm_ctx* ctx, uint8_t* const* shares, const uint8_t* present, uin
     if ((e = L.dev.ensure(bytes)) != hipSuccess) return hip_fail(e, "hipMalloc");
     if ((e = L.aux.ensure(n + 16)) != hipSuccess) return hip_fail(e, "hipMalloc");
     uint8_t* h = static_cast<uint8_t*>(L.host.ptr);
+    // the zero-copy decoders never use an absent share's bytes (the GF(2^8) split decoder
+    // scales them by zero, the GF(2^16) ones do not load them), so only the copy path
+    // clears them
+    uint8_t* const hd = codec_zero_copy(k) ? static_cast<uint8_t*>(lane_host_dev(L)) : nullptr;
     for (uint32_t i = 0; i < n; ++i) {
         if (present[i]) memcpy(h + i * S, shares[i], S);
-        else memset(h + i * S, 0, S);
+        else if (!hd) memset(h + i * S, 0, S);
     }
     uint8_t* hp = h + bytes;
     for (uint32_t i = 0; i < n; ++i) hp[i] = present[i] ? 1 : 0;
-    if (codec_zero_copy(k))
-        if (uint8_t* hd = static_cast<uint8_t*>(lane_host_dev(L))) {
-            // the decoder straight on the pinned buffer: it reads the points and the
-            // presence bytes over PCIe and writes only the missing shares back
-            DecodeSet ds{};
-            ds.base = hd;
-            ds.presence = hd + bytes;
-            ds.indices = static_cast<const uint32_t*>(ctx->zero_index.ptr);
-            ds.count = 1;
-            ds.axis = 0;
-            ds.k = k;
-            ds.S = share_size;
-            if (int rc = launch_decode(ctx, ds, L.stream)) return rc;
-            if ((e = lane_wait(L.stream)) != hipSuccess) return hip_fail(e, "decode");
-            for (uint32_t i = 0; i < n; ++i)
-                if (!present[i]) memcpy(shares[i], h + i * S, S);
-            return RSM_OK;
-        }
+    if (hd) {
+        // the decoder straight on the pinned buffer: it reads the points and the
+        // presence bytes over PCIe and writes only the missing shares back
+        DecodeSet ds{};
+        ds.base = hd;
+        ds.presence = hd + bytes;
+        ds.indices = static_cast<const uint32_t*>(ctx->zero_index.ptr);
+        ds.count = 1;
+        ds.axis = 0;
+        ds.k = k;
+        ds.S = share_size;
+        if (int rc = launch_decode(ctx, ds, L.stream)) return rc;
+        if ((e = lane_wait(L.stream)) != hipSuccess) return hip_fail(e, "decode");
+        for (uint32_t i = 0; i < n; ++i)
+            if (!present[i]) memcpy(shares[i], h + i * S, S);
+        return RSM_OK;
+    }
     uint8_t* d = static_cast<uint8_t*>(L.dev.ptr);
     uint8_t* dpres = static_cast<uint8_t*>(L.aux.ptr);
     if ((e = hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, L.stream)) != hipSuccess)
