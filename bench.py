@@ -213,7 +213,9 @@ def pct(xs, q):
 def bench_codec(local, L, R, k=128, S=512, calls=400, threads=64):
     """Per-codeword Encode (codec_test.go:15-35 BenchmarkEncoding, k=128, 512 B):
     latency of one rsm_encode from host memory on an idle GPU, and aggregate rate
-    with `threads` host threads calling concurrently (rsmt2d's 2k goroutines)."""
+    with `threads` host threads calling concurrently (rsmt2d's 2k goroutines).  Also
+    Decode in BenchmarkDecoding's shape (codec_test.go:50-92: the 2k shares of a k =
+    128 codeword with k/2 of them nil at random), every result checked."""
     import ctypes
     import threading
     import numpy as np
@@ -256,11 +258,30 @@ def bench_codec(local, L, R, k=128, S=512, calls=400, threads=64):
     if errs:
         raise SystemExit(f"bench codec: concurrent rsm_encode failed {errs[:3]}")
     n = threads * per
+    # BenchmarkDecoding: k/2 of the 2k shares nil
+    full = np.concatenate([d, p])
+    present = np.ones(2 * k, np.uint8)
+    present[rng.choice(2 * k, size=k // 2, replace=False)] = 0
+    work = np.empty_like(full)
+    wp = (ctypes.c_void_p * (2 * k))(*[work.ctypes.data + i * S for i in range(2 * k)])
+    dlat = []
+    for i in range(calls + 20):
+        work[:] = full * present[:, None]
+        t0 = time.perf_counter()
+        R._check(L.rsm_decode(ctx, wp, present.ctypes.data, 2 * k, S))
+        if i >= 20:
+            dlat.append(time.perf_counter() - t0)
+        if i == 0 and not np.array_equal(work, full):
+            raise SystemExit("bench codec: rsm_decode result differs")
     return {"workload": f"per-codeword Encode k={k} S={S} from host memory (BenchmarkEncoding shape)",
             "latency_us_p50": round(pct(lat, 0.5) * 1e6, 1), "latency_us_p10": round(pct(lat, 0.1) * 1e6, 1),
             "latency_us_p90": round(pct(lat, 0.9) * 1e6, 1),
             "concurrent_threads": threads, "concurrent_codewords_per_s": round(n / dt, 1),
-            "concurrent_GiB_s": round(n * k * S / dt / 2**30, 3)}
+            "concurrent_GiB_s": round(n * k * S / dt / 2**30, 3),
+            "decode_workload": f"per-codeword Decode of 2k={2 * k} shares, {k // 2} nil (BenchmarkDecoding shape)",
+            "decode_latency_us_p50": round(pct(dlat, 0.5) * 1e6, 1),
+            "decode_latency_us_p10": round(pct(dlat, 0.1) * 1e6, 1),
+            "decode_latency_us_p90": round(pct(dlat, 0.9) * 1e6, 1)}
 
 
 def bench_fraud_proof(local, L, R, k=128, S=512, reps=300):
