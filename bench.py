@@ -849,6 +849,72 @@ def bench_c4(local, L, R, steps, B=2, k=256, S=2048):
                        else f"enc16_kernel<{1 << (k - 1).bit_length()}>") + " (row pass, column pass)"}
 
 
+def bench_eds_roots(local, L, R, S=512, ods_sizes=(32, 64, 128, 256, 512), reps=20, ns=29):
+    """BenchmarkEDSRootsWithDefaultTree and BenchmarkEDSRootsWithErasuredNMT
+    (datasquare_test.go:415-473): the 2W row and column roots of ONE square of width
+    W = 2 * ods (64 .. 1024 shares of 512 B), no extension, from device memory --
+    rsm_roots_dev / rsm_nmt_roots_dev back to back on one stream, device time per call.
+    Synthetic square: random payload with namespaces non-decreasing along every row and
+    column (big-endian cell index, as genRandSortedDS gives); row 0 and column W - 1 of
+    each width checked against the host DefaultTree and oracle/nmt.py before timing."""
+    import ctypes
+    import numpy as np
+    import oracle.nmt as onmt
+    ctx = R.device_context(local)
+    e0, e1 = ctypes.c_void_p(), ctypes.c_void_p()
+    R._check(L.rsm_event_create(ctx, ctypes.byref(e0)))
+    R._check(L.rsm_event_create(ctx, ctypes.byref(e1)))
+
+    def dev_us(call):
+        call()  # warm
+        R._check(L.rsm_event_record(ctx, e0, None))
+        for _ in range(reps):
+            call()
+        R._check(L.rsm_event_record(ctx, e1, None))
+        ms = ctypes.c_float()
+        R._check(L.rsm_event_elapsed_ms(e0, e1, ctypes.byref(ms)))
+        return ms.value * 1e3 / reps
+
+    rng = np.random.default_rng(0xED5)
+    by = {}
+    for o in ods_sizes:
+        W = 2 * o
+        sq = rng.integers(0, 256, (W, W, S), dtype=np.uint8)
+        idx = np.arange(W * W, dtype=np.uint64).reshape(W, W)
+        for b in range(8):
+            sq[:, :, ns - 1 - b] = ((idx >> np.uint64(8 * b)) & np.uint64(0xFF)).astype(np.uint8)
+        sq[:, :, : ns - 8] = 0
+        buf = R.DeviceBuffer(W * W * S, local)
+        buf.upload(sq)
+        RL = 2 * ns + 32
+        droots = R.DeviceBuffer(2 * W * 32, local)
+        nroots = R.DeviceBuffer(2 * W * RL, local)
+        status = R.DeviceBuffer(2 * W * 4, local)
+        p = R.NmtParams(ns, 1, o)
+        default = lambda: R._check(L.rsm_roots_dev(ctx, buf.ptr, W, S, droots.ptr, None))
+        nmt = lambda: R._check(L.rsm_nmt_roots_dev(ctx, buf.ptr, W, S, ctypes.byref(p), nroots.ptr, status.ptr, None))
+        default()
+        nmt()
+        R._check(L.rsm_sync(ctx))
+        gd = droots.download(2 * W * 32).reshape(2 * W, 32)
+        gn = nroots.download(2 * W * RL).reshape(2 * W, RL)
+        st = status.download(2 * W * 4).view(np.uint32)
+        for axis, i in ((0, 0), (1, W - 1)):
+            vec = [bytes(c) for c in (sq[i] if axis == 0 else sq[:, i])]
+            if bytes(gd[axis * W + i]) != R._default_root(vec):
+                raise SystemExit("bench eds roots: device DefaultTree root differs from the host tree")
+            if bytes(gn[axis * W + i]) != onmt.erasured_root(vec, i, o, ns) or st.any():
+                raise SystemExit("bench eds roots: device NMT root differs from the restatement")
+        by[str(o)] = {"eds_width": W, "default_tree_us": round(dev_us(default), 1), "nmt_us": round(dev_us(nmt), 1)}
+        for b in (buf, droots, nroots, status):
+            b.free()
+    return {"workload": "BenchmarkEDSRootsWithDefaultTree / WithErasuredNMT: the 2W roots of one square of "
+                        f"{S} B shares, ODS width 32..512 (no extension)",
+            "by_ods": by,
+            "note": "device time per call of back-to-back rsm_roots_dev / rsm_nmt_roots_dev on one stream "
+                    "(one leaf launch + one tree launch each; namespace 29 B, IgnoreMaxNamespace)"}
+
+
 def bench_nmt_roots(local, L, R, k, S, squares=32, reps=5, ns=29):
     """The same with Celestia's tree: extension + NMT row/column roots (celestiaorg/nmt
     v0.24.3 as rsmt2d's erasured wrappers push it: namespace 29 bytes, parity namespace
@@ -1221,6 +1287,7 @@ def main():
     if rank == 0 and world == 1 and not a.no_roots:
         out["with_roots"] = bench_roots(local, L, R, buf, k, S, B, a.steps)
         out["with_nmt_roots"] = bench_nmt_roots(local, L, R, k, S)
+        out["eds_roots"] = bench_eds_roots(local, L, R)
     for b in bufs:
         b.free()
     for st in streams[1:]:

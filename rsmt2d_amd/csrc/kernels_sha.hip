@@ -104,8 +104,8 @@ __host__ __device__ constexpr uint32_t tree_lds_words(uint32_t W) { return (W / 
 // and its writes, waves past the level's last node idle.  At W = 256 and TPW = 2 the
 // workgroup then issues 34 wave-passes of two compressions for its 8 trees instead
 // of 48 (each wave's own top five levels were one pass each for 32 .. 2 nodes), and
-// a SIMD's SHA throughput is its issued wave-passes (kernels_sha.hip above).  A
-// latency launch (one square) keeps COOP off: its depth is the same either way.
+// a SIMD's SHA throughput is its issued wave-passes (kernels_sha.hip above).  The
+// launcher uses COOP for every form (one square's depth is the same either way).
 template <int TPW, bool COOP>
 __global__ __launch_bounds__(256) void tree_root_kernel(const uint32_t* __restrict__ leaf, uint32_t W,
                                                         uint8_t* __restrict__ roots, uint32_t first, uint32_t count) {
@@ -265,9 +265,10 @@ hipError_t launch_tree_kernel(const uint32_t* d_leaf, uint32_t W, uint8_t* d_roo
     const uint32_t blocks = (count + kTreesPerBlock * tpw - 1) / (kTreesPerBlock * tpw);
     const size_t lds = (size_t)kTreesPerBlock * tpw * tree_lds_words(W) * 4u;
     const dim3 grid(blocks, squares);
-    if (latency)
-        hipLaunchKernelGGL((tree_root_kernel<1, false>), grid, dim3(256), lds, st, d_leaf, W, d_roots, first, count);
-    else if (tpw == 4)
+    // (the cooperative upper levels in every form: one square's depth is the same either
+    // way -- W = 256: 53.6 against 54.6 us -- and a wide square's many trees, W = 1024:
+    // 2048 waves on 1024 SIMDs, need fewer wave-passes; profiles/r05av_eds_roots.json)
+    if (tpw == 4)
         hipLaunchKernelGGL((tree_root_kernel<4, true>), grid, dim3(256), lds, st, d_leaf, W, d_roots, first, count);
     else if (tpw == 2)
         hipLaunchKernelGGL((tree_root_kernel<2, true>), grid, dim3(256), lds, st, d_leaf, W, d_roots, first, count);
