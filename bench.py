@@ -915,6 +915,53 @@ def bench_eds_roots(local, L, R, S=512, ods_sizes=(32, 64, 128, 256, 512), reps=
                     "(one leaf launch + one tree launch each; namespace 29 B, IgnoreMaxNamespace)"}
 
 
+def bench_extension_with_roots(local, L, R, S=512, ks=(4, 8, 16, 32, 64, 128, 256, 512), reps=10):
+    """BenchmarkExtensionWithRoots (extendeddatasquare_test.go:309-333): ONE square's
+    extension and its DefaultTree row and column roots, from device memory
+    (rsm_extend_squares_dev count = 1, then rsm_roots_dev), k = 4 .. 512 at 512 B shares
+    (GF(2^16) past k = 128); device time per square of back-to-back pairs on one stream.
+    The k = 16 square is checked against the oracle extension and the host DefaultTree."""
+    import ctypes
+    import numpy as np
+    import oracle
+    ctx = R.device_context(local)
+    e0, e1 = ctypes.c_void_p(), ctypes.c_void_p()
+    R._check(L.rsm_event_create(ctx, ctypes.byref(e0)))
+    R._check(L.rsm_event_create(ctx, ctypes.byref(e1)))
+    by = {}
+    for k in ks:
+        W = 2 * k
+        buf = R.DeviceBuffer(W * W * S, local)
+        buf.fill_random(0xE5 + k)
+        roots = R.DeviceBuffer(2 * W * 32, local)
+
+        def pair():
+            R._check(L.rsm_extend_squares_dev(ctx, buf.ptr, k, S, 1, None))
+            R._check(L.rsm_roots_dev(ctx, buf.ptr, W, S, roots.ptr, None))
+
+        pair()
+        R._check(L.rsm_sync(ctx))
+        if k == 16:
+            got = buf.download(W * W * S).reshape(W, W, S)
+            if not np.array_equal(got, oracle.extend_square(got[:k, :k].copy(), nthreads=8)):
+                raise SystemExit("bench extension with roots: GPU EDS differs from the oracle")
+            rr = roots.download(2 * W * 32).reshape(2 * W, 32)
+            if bytes(rr[0]) != R._default_root([bytes(c) for c in got[0]]):
+                raise SystemExit("bench extension with roots: device root differs from the host tree")
+        R._check(L.rsm_event_record(ctx, e0, None))
+        for _ in range(reps):
+            pair()
+        R._check(L.rsm_event_record(ctx, e1, None))
+        ms = ctypes.c_float()
+        R._check(L.rsm_event_elapsed_ms(e0, e1, ctypes.byref(ms)))
+        by[str(k)] = round(ms.value * 1e3 / reps, 1)
+        buf.free()
+        roots.free()
+    return {"workload": f"BenchmarkExtensionWithRoots: one square extended + DefaultTree roots, {S} B shares",
+            "us_per_square_by_k": by,
+            "note": "device time per (rsm_extend_squares_dev count=1 + rsm_roots_dev) of back-to-back pairs"}
+
+
 def bench_nmt_roots(local, L, R, k, S, squares=32, reps=5, ns=29):
     """The same with Celestia's tree: extension + NMT row/column roots (celestiaorg/nmt
     v0.24.3 as rsmt2d's erasured wrappers push it: namespace 29 bytes, parity namespace
@@ -1288,6 +1335,7 @@ def main():
         out["with_roots"] = bench_roots(local, L, R, buf, k, S, B, a.steps)
         out["with_nmt_roots"] = bench_nmt_roots(local, L, R, k, S)
         out["eds_roots"] = bench_eds_roots(local, L, R)
+        out["extension_with_roots"] = bench_extension_with_roots(local, L, R)
     for b in bufs:
         b.free()
     for st in streams[1:]:
