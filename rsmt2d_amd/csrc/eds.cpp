@@ -577,8 +577,9 @@ int fast_repair_rows_zero_copy(rsm_eds* e, DevSquare& dev, const std::vector<uin
     // for k = 128's 64 KiB map)
     HostBuf& hb = gv.lane->host;
     const size_t pres_n = e->present.size();  // W * W: the row list after it stays 4-byte aligned
-    // then, 16-byte aligned, the verification results coming back (mismatch flag, roots,
-    // tree statuses): the same pinned staging, so those copies are asynchronous too
+    // then, 16-byte aligned, the verification results (mismatch flag, roots, NMT tree
+    // statuses), written into the same pinned staging by the kernels (flag, DefaultTree
+    // roots) or by asynchronous copies (NMT roots and statuses)
     const size_t back = (pres_n + todo.size() * 4 + 15) / 16 * 16;
     const size_t roots_n = (size_t)2 * W * dt.root_len;
     if ((r = hb.ensure(back + 16 + roots_n + (size_t)2 * W * 4)) != hipSuccess)
@@ -658,12 +659,12 @@ int fast_repair_rows_zero_copy(rsm_eds* e, DevSquare& dev, const std::vector<uin
     }
     (void)hipEventRecord(ev_bot, st);
     // verification.  sv: the column re-encode of the top half and the encoding compare;
-    // st, right behind its own sweep: the leaf digests of the WHOLE square and the trees.  (A cross-queue
-    // wait costs 11-12 us on the critical path even when its event has long completed,
-    // and one leaf launch is latency-bound -- 9 compressions per cell, one wave per SIMD
-    // for the whole square -- so hashing the top half early on sv saved nothing:
-    // profiles/r05al_repair_tail.txt.)  The mismatch flag and the DefaultTree roots land
-    // in the pinned staging straight from the kernels.
+    // st, right behind its own sweep: the leaf digests of the WHOLE square and the
+    // trees.  (A cross-queue wait costs 11-12 us on the critical path even when its event
+    // has long completed, and one leaf launch is latency-bound -- 9 compressions per
+    // cell, one wave per SIMD for the whole square -- so hashing the top half early on sv
+    // saved nothing: profiles/r05al_repair_tail.txt.)  The mismatch flag and the
+    // DefaultTree roots land in the pinned staging straight from the kernels.
     uint32_t* const h_mismatch = reinterpret_cast<uint32_t*>(hs + back);
     uint8_t* const got = hs + back + 16;
     uint32_t* const status = reinterpret_cast<uint32_t*>(got + roots_n);
@@ -693,8 +694,8 @@ int fast_repair_rows_zero_copy(rsm_eds* e, DevSquare& dev, const std::vector<uin
     if (dt.nmt) {
         // namespaced trees: leaves and nodes of the whole square in one launch pair
         // (leaf scratch: sv's StreamScratch, held above for the whole call, both streams
-        // drained before it is released); byte-wise root stores, so
-        // they come back by copy
+        // drained before it is released); the kernel stores roots byte-wise, so they
+        // come back by copy
         if ((r = launch_nmt_roots(dev.d_eds, W, e->S, dt.p.namespace_size, dt.p.square_size, dt.p.ignore_max_namespace,
                                   leaf, d_roots, d_status, st)) != hipSuccess)
             return hip_fail(r, "NMT roots");
