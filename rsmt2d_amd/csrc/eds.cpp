@@ -563,15 +563,9 @@ int fast_repair_rows_zero_copy(rsm_eds* e, DevSquare& dev, const std::vector<uin
     DevBuf& sb = dev.ctx->eds.status;
     if ((r = sb.ensure((size_t)2 * W * 4)) != hipSuccess) return hip_fail(r, "hipMalloc (tree status)");
     uint32_t* d_status = static_cast<uint32_t*>(sb.ptr);
-    hipEvent_t ev[2];
-    for (auto& x : ev) (void)hipEventCreateWithFlags(&x, hipEventDisableTiming);
-    struct EvGuard {
-        hipEvent_t* e;
-        ~EvGuard() {
-            for (int c = 0; c < 2; ++c) (void)hipEventDestroy(e[c]);
-        }
-    } evg{ev};
-    hipEvent_t &ev_top = ev[0], &ev_bot = ev[1];
+    // the verification lane's own events (created once per lane, not per call)
+    hipEvent_t ev_top = lane_event(*gv.lane, 0), ev_bot = lane_event(*gv.lane, 1);
+    if (!ev_top || !ev_bot) return hip_fail(hipErrorOutOfMemory, "hipEventCreate (repair)");
     // the presence map and the row list go up from the lane's pinned staging: from the
     // pageable vectors hipMemcpyAsync is a staged, synchronous copy (35 us of host time
     // for k = 128's 64 KiB map)

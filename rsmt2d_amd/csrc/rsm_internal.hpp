@@ -53,7 +53,15 @@ struct Lane {
     hipStream_t stream = nullptr;
     HostBuf host;
     DevBuf dev, aux;
+    hipEvent_t ev[2] = {nullptr, nullptr};  // created on first use (lane_event), kept with the lane
 };
+
+// Event i (< 2) of a lane the caller holds, created once (hipEventDisableTiming): Repair
+// synchronises its two streams with them instead of creating events per call.
+inline hipEvent_t lane_event(Lane& L, int i) {
+    if (!L.ev[i] && hipEventCreateWithFlags(&L.ev[i], hipEventDisableTiming) != hipSuccess) L.ev[i] = nullptr;
+    return L.ev[i];
+}
 
 // Device scratch that belongs to one stream: kernels queued on different streams
 // never share it.  `mu` is held while the scratch is grown AND while the launches

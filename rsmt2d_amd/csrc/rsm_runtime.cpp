@@ -665,7 +665,11 @@ void rsm_ctx_destroy(rsm_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     (void)hipDeviceSynchronize();
-    for (auto& l : ctx->lanes) (void)hipStreamDestroy(l->stream);
+    for (auto& l : ctx->lanes) {
+        (void)hipStreamDestroy(l->stream);
+        for (hipEvent_t ev : l->ev)
+            if (ev) (void)hipEventDestroy(ev);
+    }
     ctx->lanes.clear();
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
