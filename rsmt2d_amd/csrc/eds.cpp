@@ -525,7 +525,10 @@ int fast_repair_rows_zero_copy(rsm_eds* e, DevSquare& dev, const std::vector<uin
     // the zero-copy decoders: GF(2^8) 65 <= k <= 128 (decode_gf8_split_zc_kernel) and the
     // GF(2^16) single passes, k <= 512 (dec16f_kernel / dec16h_kernel)
     const bool zc_decoder = field_bits(k) == 8 ? ceil_pow2(k) == 128 : ceil_pow2(k) <= 512;
-    if (!e->data.pinned || !zc_decoder || !narrow_ok(dev.ctx, k, S, S)) return 1;
+    // the rows' decoders AND the columns' verification re-encode (elem_stride = row) must
+    // take the narrow forms: a wide GF(2^16) column encode runs through sv's work arrays
+    // and takes sv's scratch lock, which this function holds for the leaf digests
+    if (!e->data.pinned || !zc_decoder || !narrow_ok(dev.ctx, k, S, S) || !narrow_ok(dev.ctx, k, row, S)) return 1;
     void* hmap = nullptr;
     hipError_t r = hipHostGetDevicePointer(&hmap, e->data.data(), 0);
     if (r != hipSuccess || !hmap) {

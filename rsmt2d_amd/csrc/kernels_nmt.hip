@@ -711,7 +711,10 @@ hipError_t launch_nmt_roots(const uint8_t* d_eds, uint32_t W, uint32_t S, uint32
                             uint32_t* d_leaf, uint8_t* d_roots, uint32_t* d_status, hipStream_t st, uint32_t squares) {
     if (squares == 0) return hipSuccess;
     const uint32_t cells = W * W;
-    if (ns == 29 && S % 64 == 0 && S >= 64)  // Celestia's namespace: the streaming leaf kernel
+    // Celestia's namespace: the streaming leaf kernel (16-byte loads at eds + cell*S, so
+    // the base must be 16-byte aligned; a caller-supplied unaligned square takes the
+    // word-load kernel)
+    if (ns == 29 && S % 64 == 0 && S >= 64 && (reinterpret_cast<uintptr_t>(d_eds) & 15u) == 0)
         hipLaunchKernelGGL(nmt_leaf29_kernel, dim3((cells + 255) / 256, squares), dim3(256), 0, st, d_eds, W, S, k, d_leaf);
     else
         hipLaunchKernelGGL(nmt_leaf_kernel, dim3((cells + 255) / 256, squares), dim3(256), 0, st, d_eds, W, S, ns, k, d_leaf);

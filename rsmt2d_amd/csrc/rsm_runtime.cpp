@@ -262,7 +262,7 @@ int launch_encode(rsm_ctx* ctx, const CodewordSet& cs0, hipStream_t st) {
             e = launch_encode_gf16(cs, g, st);
         }
     }
-    if (e == hipErrorOutOfMemory) return fail(RSM_ENOMEM, "encode: GF(2^16) work arrays below one byte slab");
+    if (e == hipErrorOutOfMemory) return fail(RSM_ENOMEM, "encode: GF(2^16) scratch too small (work arrays below one byte slab)");
     if (e != hipSuccess) return hip_fail(e, "encode kernel launch");
     return RSM_OK;
 }
@@ -310,7 +310,8 @@ int launch_decode(rsm_ctx* ctx, const DecodeSet& ds0, hipStream_t st) {
         }
         e = launch_decode_gf16(ds, g, st);
     }
-    if (e == hipErrorOutOfMemory) return fail(RSM_ENOMEM, "decode: GF(2^16) work arrays below one byte slab");
+    if (e == hipErrorOutOfMemory)
+        return fail(RSM_ENOMEM, "decode: GF(2^16) scratch too small (error locators or work arrays below one codeword / byte slab)");
     if (e != hipSuccess) return hip_fail(e, "decode kernel launch");
     return RSM_OK;
 }

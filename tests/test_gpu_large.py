@@ -191,6 +191,55 @@ def test_gf16_repair_k512_byzantine_matches_oracle(lib, rng):
     assert eds.repair_stats().fast_path == 0
 
 
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("k,S", [(128, 256), (256, 128)])
+@pytest.mark.parametrize("limits", ["columns", "all", "budget"])
+def test_repair_under_lowered_limits(lib, pctx, k, S, limits):
+    """BenchmarkRepair's erasures (extendeddatacrossword_test.go:443-453) repaired on a
+    private context whose offset limit sends the columns (or every codeword) to the
+    wide forms, or whose GF(2^16) work budget is lowered.  Results never depend on the
+    limits (rsm_ctx_set_limits): the repaired square must equal the oracle's EDS.
+    The "columns" case is the shape the zero-copy Repair must decline (its column
+    verification would take the wide encoder's scratch lock on its own stream)."""
+    W = 2 * k
+    ods, _ = _square(k, S, 0x7E0 + k)
+    want = oracle.extend_square(ods, nthreads=CPU)
+    cells = np.ascontiguousarray(want.reshape(W * W, S))
+    lens = np.full(W * W, S, np.uint32)
+    rr = np.empty(W * 32, np.uint8)
+    cr = np.empty(W * 32, np.uint8)
+    ln = ctypes.c_uint32(0)
+    h = ctypes.c_void_p()
+    ptrs = _ptr_array(cells)  # (held: the C call reads it)
+    R._check(lib.rsm_eds_import(R.device_context(), ptrs.ctypes.data, lens.ctypes.data, W * W, ctypes.byref(h)))
+    try:
+        R._check(lib.rsm_eds_roots(h, 0, None, None, rr.ctypes.data, 32, ctypes.byref(ln)))
+        R._check(lib.rsm_eds_roots(h, 1, None, None, cr.ctypes.data, 32, ctypes.byref(ln)))
+    finally:
+        lib.rsm_eds_free(h)
+    limit = {"columns": (k + 1) * S + S, "all": 1, "budget": 0}[limits]
+    budget = 1 << 16 if limits == "budget" else 0
+    R._check(lib.rsm_ctx_set_limits(pctx, limit, budget))
+    rng = np.random.default_rng(k + len(limits))
+    pres = np.ones((W, W), np.uint8)
+    for r in range(W):
+        pres[r, rng.choice(W, size=k, replace=False)] = 0
+    ptrs = _ptr_array(cells, pres.reshape(-1))
+    h = ctypes.c_void_p()
+    R._check(lib.rsm_eds_import(pctx, ptrs.ctypes.data, lens.ctypes.data, W * W, ctypes.byref(h)))
+    try:
+        byz = R._Byz()
+        R._check(lib.rsm_eds_repair(h, rr.ctypes.data, cr.ctypes.data, 32, None, None, ctypes.byref(byz)))
+        got = np.empty_like(want)
+        R._check(lib.rsm_eds_flattened(h, got.ctypes.data, None))
+        assert np.array_equal(got, want)
+        st = R.RepairStats()
+        R._check(lib.rsm_eds_repair_stats(h, ctypes.byref(st)))
+        assert (st.fast_path, st.fallback_reason) == (1, 0)
+    finally:
+        lib.rsm_eds_free(h)
+
+
 # ---------------------------------------------------------------------------
 # squares of 2 GiB and more (the round-4 build refused these with RSM_EUNSUPPORTED)
 # ---------------------------------------------------------------------------
