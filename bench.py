@@ -477,6 +477,50 @@ def bench_c5_c_abi(G, L, R, steps, k=512, S=512):
     return out
 
 
+def bench_c5_g8_projection(ctx, buf, L, R, k, S, G=8, reps=20):
+    """One rank's compute at G = 8 GPUs, timed on this one GPU (the
+    row-sharded schedule of rsm_multi_extend_dev, extendeddatasquare.go:204-207):
+    rsm_extend_rows_dev of k/G Q0 rows (the row pass of one shard) and
+    rsm_extend_cols_dev of 2k/G columns (its column slice after the exchange), device
+    events around `reps` back-to-back calls each.  The exchange is NOT measured (no
+    multi-GPU node here): its bytes per GPU are reported, and `exchange_est_ms` prices
+    them at the 7 xGMI links' 153 GB/s peak each (a lower bound on the exchange)."""
+    import ctypes
+    W = 2 * k
+    e0, e1 = ctypes.c_void_p(), ctypes.c_void_p()
+    R._check(L.rsm_event_create(ctx, ctypes.byref(e0)))
+    R._check(L.rsm_event_create(ctx, ctypes.byref(e1)))
+    ms = ctypes.c_float()
+    times = {}
+    try:
+        for name, fn in (("rows", lambda: L.rsm_extend_rows_dev(ctx, buf.ptr, k, S, 0, k // G, None)),
+                         ("cols", lambda: L.rsm_extend_cols_dev(ctx, buf.ptr, k, S, 0, W // G, None))):
+            R._check(fn())
+            R._check(L.rsm_event_record(ctx, e0, None))
+            for _ in range(reps):
+                R._check(fn())
+            R._check(L.rsm_event_record(ctx, e1, None))
+            R._check(L.rsm_sync(ctx))
+            R._check(L.rsm_event_elapsed_ms(e0, e1, ctypes.byref(ms)))
+            times[name] = ms.value / reps
+    finally:
+        L.rsm_event_destroy(e0)
+        L.rsm_event_destroy(e1)
+    ag = (G - 1) * (k // G) * W * S     # all-gather of the top half: received per GPU
+    a2a = (G - 1) * (k // G) * (W // G) * S  # all-to-all of column blocks: received per GPU
+    link = 7 * 153e9
+    comp = times["rows"] + times["cols"]
+    return {"label": "projection, exchange not measured: one rank's compute at G = 8 on one GPU",
+            "rows_ms": round(times["rows"], 4), "rows": k // G, "row_tasks": (k // G) * ((S + 255) // 256),
+            "cols_ms": round(times["cols"], 4), "cols": W // G,
+            "compute_ms": round(comp, 4),
+            "allgather_received_bytes_per_gpu": ag, "alltoall_received_bytes_per_gpu": a2a,
+            "exchange_est_ms": {"allgather": round(ag / link * 1e3, 4), "alltoall": round(a2a / link * 1e3, 4)},
+            "projected_ms_per_square": {"allgather": round(comp + ag / link * 1e3, 4),
+                                        "alltoall": round(comp + a2a / link * 1e3, 4)},
+            "projected_ods_GiB_s_alltoall": round(k * k * S / ((comp + a2a / link * 1e3) / 1e3) / 2**30, 1)}
+
+
 def bench_c5(world, rank, local, dist, steps, L, R):
     """Config 5: one 512x512 -> 1024x1024 square (GF(2^16), 512 B shares).  N=1: the
     whole square on one GPU; N>1: rows sharded over the N GPUs, then an RCCL
@@ -497,6 +541,7 @@ def bench_c5(world, rank, local, dist, steps, L, R):
             R._check(L.rsm_extend_squares_dev(ctx, buf.ptr, k, S, 1, None))
         R._check(L.rsm_sync(ctx))
         dt = (time.perf_counter() - t0) / steps
+        g8 = bench_c5_g8_projection(ctx, buf, L, R, k, S)
         buf.free()
         # the C-ABI multi-GPU entry point with a clique of one
         multi = bench_c5_c_abi(1, L, R, steps)
@@ -566,6 +611,7 @@ def bench_c5(world, rank, local, dist, steps, L, R):
             out["traffic"] = tr
     if dist is None:
         out["c_abi"] = multi
+        out["g8_projection"] = g8
     if dist is not None:
         if rank == 0:
             out["c_abi"] = c_abi

@@ -209,7 +209,9 @@ DIAG_SIGNATURES = {
     "rsm_diag_queue_check": (_I32, [_VP, _VP]),
     "rsm_diag_extend_pipeline_dev": (_I32, [_VP, _VP, _VP, _U32, _U32, _U32, _VP]),
 }
-DIAG_LIB_PATH = os.path.join(_HERE, "librsmt2d_hip_diag.so")
+# (A/B runs may point the DIAGNOSTIC library at a variant build; the product library
+# path is fixed)
+DIAG_LIB_PATH = os.environ.get("RSM_DIAG_LIB") or os.path.join(_HERE, "librsmt2d_hip_diag.so")
 
 
 def build(diag: bool = True) -> str:

@@ -51,10 +51,32 @@ __device__ __forceinline__ uint32_t pm(uint32_t hi, uint32_t lo, uint32_t sel) {
     return __builtin_amdgcn_perm(hi, lo, sel);
 }
 
+// The six perm selectors of a lane's 4 symbols (lo dword yl, hi dword yh): bits 0-2,
+// 3-5 and 6-7 of every byte.  The shifted groups of both dwords come from ONE 64-bit
+// shift of the pair (yh:yl) each -- v_lshrrev_b64 issues at the rate of a 32-bit shift
+// (profiles/r03_alu64.jsonl), so 2 half-rate shifts instead of 4 per multiply; the bits
+// yh pushes into yl's top byte are masked off with the selector bits.  (Written as asm:
+// the compiler folds the masked 64-bit shift back into two 32-bit ones.)
+struct Sel16 {
+    uint32_t a, b, c, d, e, f;
+};
+__device__ __forceinline__ Sel16 sel16(uint32_t yl, uint32_t yh) {
+#ifdef RSM_SEL32  // (diagnostic A/B builds only: the round-5 selectors, four 32-bit shifts)
+    return Sel16{yl & 0x07070707u, (yl >> 3) & 0x07070707u, (yl >> 6) & 0x03030303u,
+                 yh & 0x07070707u, (yh >> 3) & 0x07070707u, (yh >> 6) & 0x03030303u};
+#endif
+    const uint64_t y = ((uint64_t)yh << 32) | yl;
+    uint64_t y3, y6;
+    asm("v_lshrrev_b64 %0, 3, %1" : "=v"(y3) : "v"(y));
+    asm("v_lshrrev_b64 %0, 6, %1" : "=v"(y6) : "v"(y));
+    return Sel16{yl & 0x07070707u,        (uint32_t)y3 & 0x07070707u, (uint32_t)y6 & 0x03030303u,
+                 yh & 0x07070707u, (uint32_t)(y3 >> 32) & 0x07070707u, (uint32_t)(y6 >> 32) & 0x03030303u};
+}
+
 // (xl, xh) ^= (yl, yh) * exp(L), tables t = PermTab16[L]
 __device__ __forceinline__ void muladd16(uint32_t& xl, uint32_t& xh, uint32_t yl, uint32_t yh, const PermTab16& t) {
-    const uint32_t sa = yl & 0x07070707u, sb = (yl >> 3) & 0x07070707u, sc = (yl >> 6) & 0x03030303u;
-    const uint32_t sd = yh & 0x07070707u, se = (yh >> 3) & 0x07070707u, sf = (yh >> 6) & 0x03030303u;
+    const Sel16 q = sel16(yl, yh);
+    const uint32_t sa = q.a, sb = q.b, sc = q.c, sd = q.d, se = q.e, sf = q.f;
     xl = x3(x3(xl, pm(t.w[1], t.w[0], sa), pm(t.w[5], t.w[4], sb)),
             x3(pm(t.w[8], t.w[8], sc), pm(t.w[13], t.w[12], sd), pm(t.w[17], t.w[16], se)), pm(t.w[20], t.w[20], sf));
     xh = x3(x3(xh, pm(t.w[3], t.w[2], sa), pm(t.w[7], t.w[6], sb)),
@@ -239,8 +261,8 @@ __device__ __forceinline__ int tab_word(int j) { return j < 9 ? j : (j == 9 ? 10
 // (xl, xh) ^= (yl, yh) * exp(L) with the compact table c in VGPRs (both v_perm
 // sources are VGPRs: no copies through the one-SGPR-per-instruction bus).
 __device__ __forceinline__ void muladd16v(uint32_t& xl, uint32_t& xh, uint32_t yl, uint32_t yh, const uint32_t (&c)[kTabW]) {
-    const uint32_t sa = yl & 0x07070707u, sb = (yl >> 3) & 0x07070707u, sc = (yl >> 6) & 0x03030303u;
-    const uint32_t sd = yh & 0x07070707u, se = (yh >> 3) & 0x07070707u, sf = (yh >> 6) & 0x03030303u;
+    const Sel16 q = sel16(yl, yh);
+    const uint32_t sa = q.a, sb = q.b, sc = q.c, sd = q.d, se = q.e, sf = q.f;
     // c: 0..7 = w0..w7, 8 = w8, 9 = w10, 10..17 = w12..w19, 18 = w20, 19 = w22
     xl = x3(x3(xl, pm(c[1], c[0], sa), pm(c[5], c[4], sb)),
             x3(pm(c[8], c[8], sc), pm(c[11], c[10], sd), pm(c[15], c[14], se)), pm(c[18], c[18], sf));

@@ -1,5 +1,5 @@
 #!/bin/bash
-# r05 GPU runner: STEPS picks what runs (space-separated):
+# r06 GPU runner: STEPS picks what runs (space-separated):
 #   smoke      __graft_entry__.smoke()
 #   large      tests/test_gpu_large.py (the 2 GiB+ squares and the wide forms)
 #   tests      every -m gpu test
@@ -9,7 +9,7 @@
 # RUN names the output directory under gpurun_out/.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=gpurun_out/${RUN:-r05}; mkdir -p $OUT
+OUT=gpurun_out/${RUN:-r06}; mkdir -p $OUT
 export TMPDIR=/tmp
 step() { local n=$1 t=$2; shift 2; echo "[$(date +%T)] $n" >> $OUT/steps.log; timeout -k 10 $t "$@" > $OUT/$n.log 2>&1; local rc=$?; echo "[$(date +%T)] $n rc=$rc" >> $OUT/steps.log; tail -n 4 $OUT/$n.log; return $rc; }
 for s in ${STEPS:-smoke tests}; do
@@ -41,6 +41,16 @@ for s in ${STEPS:-smoke tests}; do
              step gf16ab 300 python3 scripts/diag/gf16_ab.py || exit 15 ;;
     repairtrace) step repair_trace 300 rocprofv3 --kernel-trace --memory-copy-trace -d "$PWD/$OUT/rtrace" -o run --output-format csv -- python3 scripts/diag/repair_trace.py ${RT_REPS:-6} || exit 16 ;;
     repab) step repair_ab 400 python3 scripts/diag/repair_ab.py || exit 17 ;;
+    lutprobe) step lutprobe 120 scripts/diag/lutprobe ${LUT_ITERS:-4096} || exit 18 ;;
+    selab)  # same-box A/B of the production GF(2^16) kernels: this build's diagnostic library
+            # against the variant build librsmt2d_hip_diag_ab.so (make ab AB_FLAGS=...)
+         for rep in 1 2; do
+           for lib in rsmt2d_amd/librsmt2d_hip_diag.so rsmt2d_amd/librsmt2d_hip_diag_ab.so; do
+             tag=$(basename $lib .so)
+             RSM_DIAG_LIB=$lib GF16AB_FORMS=0 GF16AB_C4FORMS=0 GF16AB_REPS=2 step gf16ab_${tag}_$rep 300 python3 scripts/diag/gf16_ab.py || exit 19
+             RSM_DIAG_LIB=$lib DECAB_KS=${SELAB_KS:-256,512} DECAB_V16=0 step decab_${tag}_$rep 300 python3 scripts/diag/dec_ab.py || exit 20
+           done
+         done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
