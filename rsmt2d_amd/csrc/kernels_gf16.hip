@@ -27,6 +27,7 @@
 #include <atomic>
 #include <cstdint>
 #include <cstdlib>
+#include <type_traits>
 #include <utility>
 #include "gf16.hpp"
 #include "rsm_kernels.hpp"
@@ -36,6 +37,28 @@ namespace {
 
 constexpr uint32_t kMod16 = 65535u;
 constexpr uint32_t kOob16 = 0x80000000u;
+// The single-pass decoders load only the present cells, after the presence ballot.
+// RSM_DEC16_EAGER (diagnostic A/B builds) loads every cell right away instead, before the
+// ballot, and zeroes the absent ones: slower on MI355X (k = 256 sweep 0.233-0.236 against
+// 0.220-0.224 ms, k = 512 1.151-1.177 against 1.134-1.139; profiles/r06c_dec16_eager_ab.jsonl)
+// -- the doubled reads of a sweep whose tasks all start together cost more than the
+// presence latency they hide.
+#ifdef RSM_DEC16_EAGER
+constexpr bool kDec16Eager = true;
+#else
+constexpr bool kDec16Eager = false;
+#endif
+// dec16h_kernel stages its twiddle tables right where the pool is free.  RSM_DEC16_PREFETCH
+// (diagnostic A/B builds) issues their loads before the scale multiplies instead and stores
+// them after the barrier that frees the pool: no faster (k = 512 sweep 1.115-1.157 against
+// 1.126-1.146 ms, profiles/r06d_dec16_prefetch_ab.jsonl) -- the staging is not on the
+// critical path.  (Loading the reveal tables before the group FFT the same way spills 32
+// bytes per lane at 128 VGPRs: kDec16PrefetchRv stays off.)
+#ifdef RSM_DEC16_PREFETCH
+constexpr bool kDec16PrefetchTw = true, kDec16PrefetchRv = false;
+#else
+constexpr bool kDec16PrefetchTw = false, kDec16PrefetchRv = false;
+#endif
 
 template <int N, typename F>
 __device__ __forceinline__ void sfor(F&& f) {
@@ -1289,22 +1312,46 @@ __global__ __launch_bounds__(256) void dec16_p5(Dec16 p) {  // group: FFT low + 
 // single-pass decoders waiting most of the time).
 template <int N, int THREADS>
 constexpr int elem_tab_per() { return (N * kTabW + THREADS - 1) / THREADS; }
-template <int N, int THREADS>
+// `mid` runs between the locator loads and the dependent table gathers: loads issued
+// there (the decoders' point loads) are in flight behind the locator loads, and the
+// gathers wait only for the locator values (vmcnt retires in order).
+struct NoMid {
+    __device__ void operator()() const {}
+};
+template <int N, int THREADS, typename F = NoMid>
 __device__ __forceinline__ void load_elem_tabs(const Dec16& p, uint32_t q, bool reveal,
-                                               uint32_t (&v)[elem_tab_per<N, THREADS>()]) {
+                                               uint32_t (&v)[elem_tab_per<N, THREADS>()], F&& mid = F{}) {
     constexpr int W = N * kTabW, PER = elem_tab_per<N, THREADS>();
     uint32_t tid = threadIdx.x;
     asm volatile("" : "+v"(tid));
+    if constexpr (std::is_same_v<std::decay_t<F>, NoMid>) {  // one chain per word
+#pragma unroll
+        for (int r = 0; r < PER; ++r) {
+            const uint32_t n = tid + (uint32_t)r * THREADS;
+            const uint32_t e = n / kTabW, j = n - e * kTabW;
+            uint32_t x = 0u;
+            if (n < (uint32_t)W) {
+                const uint32_t L = p.errs[(uint64_t)q * N + e];
+                x = p.r.perm[reveal ? kMod16 - L : L].w[tab_word((int)j)];
+            }
+            v[r] = x;
+        }
+        return;
+    }
+    uint32_t L[PER];
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+        const uint32_t n = tid + (uint32_t)r * THREADS;
+        const uint32_t e = n / kTabW;
+        L[r] = n < (uint32_t)W ? (uint32_t)p.errs[(uint64_t)q * N + e] : 0u;
+    }
+    mid();
+    asm volatile("" ::: "memory");
 #pragma unroll
     for (int r = 0; r < PER; ++r) {
         const uint32_t n = tid + (uint32_t)r * THREADS;
         const uint32_t e = n / kTabW, j = n - e * kTabW;
-        uint32_t x = 0u;
-        if (n < (uint32_t)W) {
-            const uint32_t L = p.errs[(uint64_t)q * N + e];
-            x = p.r.perm[reveal ? kMod16 - L : L].w[tab_word((int)j)];
-        }
-        v[r] = x;
+        v[r] = n < (uint32_t)W ? p.r.perm[reveal ? kMod16 - L[r] : L[r]].w[tab_word((int)j)] : 0u;
     }
 }
 template <int N, int THREADS>
@@ -1418,20 +1465,36 @@ __global__ __launch_bounds__(1024, 4) void dec16f_kernel(Dec16 p) {
     const uint32_t my_s = lane < (uint32_t)E ? share_of(E * w + lane) : 0xFFFFFFFFu;
     const uint32_t my_p = my_s != 0xFFFFFFFFu ? (uint32_t)p.ds.presence[cell(my_s)] : 0u;
     uint32_t etv[elem_tab_per<N, 1024>()];
-    load_elem_tabs<N, 1024>(p, q, false, etv);
-    const uint32_t have = __builtin_amdgcn_readfirstlane((uint32_t)__ballot(my_p != 0u));
     uint32_t l[E], h[E];
-    sfor<E>([&](auto I) {
-        constexpr int i = decltype(I)::value;
-        const uint32_t src = share_of(E * w + i);
-        const uint32_t so = ((have >> i) & 1u) ? hoff(src) : kOob16;
-        l[i] = ld(si, ln.lo, so);
-        h[i] = ld(si, ln.lo + 32, so);
-        if constexpr (ZC) {  // the present cell lands in the device square as well
-            st(sq, l[i], ln.lo, so);
-            st(sq, h[i], ln.lo + 32, so);
-        }
-    });
+    // device form: every real cell loaded right away (behind the presence byte and the
+    // scale tables' locator loads, ahead of the ballot), the absent ones zeroed after it
+    // -- the loads do not wait for the presence bytes; zero-copy: only the present
+    // cells, after the ballot
+    auto load_points = [&](uint32_t m) {
+        sfor<E>([&](auto I) {
+            constexpr int i = decltype(I)::value;
+            const uint32_t src = share_of(E * w + i);
+            const uint32_t so = ((m >> i) & 1u) && src != 0xFFFFFFFFu ? hoff(src) : kOob16;
+            l[i] = ld(si, ln.lo, so);
+            h[i] = ld(si, ln.lo + 32, so);
+            if constexpr (ZC) {  // the present cell lands in the device square as well
+                st(sq, l[i], ln.lo, so);
+                st(sq, h[i], ln.lo + 32, so);
+            }
+        });
+    };
+    constexpr bool EAGER = !ZC && kDec16Eager;
+    if constexpr (EAGER) load_elem_tabs<N, 1024>(p, q, false, etv, [&] { load_points(~0u); });
+    else load_elem_tabs<N, 1024>(p, q, false, etv);
+    const uint32_t have = __builtin_amdgcn_readfirstlane((uint32_t)__ballot(my_p != 0u));
+    if constexpr (!EAGER) load_points(have);
+    if constexpr (EAGER)
+        sfor<E>([&](auto I) {
+            constexpr int i = decltype(I)::value;
+            const bool keep = (have >> i) & 1u;
+            l[i] = keep ? l[i] : 0u;
+            h[i] = keep ? h[i] : 0u;
+        });
     store_elem_tabs<N, 1024>(etab, etv);
     __syncthreads();  // twiddle and scale tables staged
     sfor<E>([&](auto I) {
@@ -1621,38 +1684,64 @@ __global__ __launch_bounds__(1024, 4) void dec16h_kernel(Dec16 p) {
     const uint32_t my_s = share_of(64u * w + lane);
     const uint32_t my_p = my_s != 0xFFFFFFFFu ? (uint32_t)p.ds.presence[cell(my_s)] : 0u;
     uint32_t etv[elem_tab_per<N, 1024>()];
+    uint32_t l[E], h[E];
+    // Device form: every real cell's points are loaded right away, absent or not (issued
+    // behind the presence byte and the scale tables' chain, before the ballot), and the
+    // absent ones are zeroed once the ballot is in -- the loads no longer wait for the
+    // presence bytes (a whole load latency per task; the absent cells' bytes cost HBM
+    // reads, not time).  Zero-copy form: only the present cells cross PCIe, after the ballot.
+    auto load_points = [&](uint32_t m0, uint32_t m1) {
+        sfor<E>([&](auto I) {  // the two halves' elements of register i: E (2 w) + i, E (2 w + 1) + i
+            constexpr int i = decltype(I)::value;
+            const uint32_t s0 = share_of(E * 2u * w + i), s1 = share_of(E * (2u * w + 1u) + i);
+            const uint32_t c0 = ((m0 >> i) & 1u) && s0 != 0xFFFFFFFFu ? hoff(s0) : kOob16;
+            const uint32_t c1 = ((m1 >> i) & 1u) && s1 != 0xFFFFFFFFu ? hoff(s1) : kOob16;
+            const uint32_t c = hi ? c1 : c0;
+            uint32_t vo = (c == kOob16 || !lane_ok) ? kOob16 : c + off;
 #ifdef RSM_DIAG
-    if (!(p.diag & 1u))  // A/B bit 0: no scale / reveal table staging (wrong output)
+            if (p.diag & 2u) vo = kOob16;  // A/B bit 1: no point loads (wrong output)
 #endif
-    load_elem_tabs<N, 1024>(p, q, false, etv);
+            l[i] = ld(si, vo, 0u);
+            h[i] = ld(si, vo + 32u, 0u);
+            if constexpr (ZC) {  // the present cell lands in the device square as well
+                st(sq, l[i], vo, 0u);
+                st(sq, h[i], vo + 32u, 0u);
+            }
+        });
+    };
+    constexpr bool EAGER = !ZC && kDec16Eager;
+#ifdef RSM_DIAG
+    if (p.diag & 1u) {  // A/B bit 0: no scale / reveal table staging (wrong output)
+        if constexpr (EAGER) load_points(~0u, ~0u);
+    } else
+#endif
+    if constexpr (EAGER) load_elem_tabs<N, 1024>(p, q, false, etv, [&] { load_points(~0u, ~0u); });
+    else load_elem_tabs<N, 1024>(p, q, false, etv);
     const uint64_t hv = __ballot(my_p != 0u);
     const uint32_t have0 = __builtin_amdgcn_readfirstlane((uint32_t)hv);
     const uint32_t have1 = __builtin_amdgcn_readfirstlane((uint32_t)(hv >> 32));
     d16_stamp(p, 1);
-    uint32_t l[E], h[E];
-    sfor<E>([&](auto I) {  // the two halves' elements of register i: E (2 w) + i, E (2 w + 1) + i
-        constexpr int i = decltype(I)::value;
-        const uint32_t s0 = share_of(E * 2u * w + i), s1 = share_of(E * (2u * w + 1u) + i);
-        const uint32_t c0 = ((have0 >> i) & 1u) ? hoff(s0) : kOob16;
-        const uint32_t c1 = ((have1 >> i) & 1u) ? hoff(s1) : kOob16;
-        const uint32_t c = hi ? c1 : c0;
-        uint32_t vo = (c == kOob16 || !lane_ok) ? kOob16 : c + off;
-#ifdef RSM_DIAG
-        if (p.diag & 2u) vo = kOob16;  // A/B bit 1: no point loads (wrong output)
-#endif
-        l[i] = ld(si, vo, 0u);
-        h[i] = ld(si, vo + 32u, 0u);
-        if constexpr (ZC) {  // the present cell lands in the device square as well
-            st(sq, l[i], vo, 0u);
-            st(sq, h[i], vo + 32u, 0u);
-        }
-    });
+    if constexpr (!EAGER) load_points(have0, have1);
+    if constexpr (EAGER) {  // absent points enter the transform as zero
+        const uint32_t mine = hi ? have1 : have0;
+        sfor<E>([&](auto I) {
+            constexpr int i = decltype(I)::value;
+            const bool keep = (mine >> i) & 1u;
+            l[i] = keep ? l[i] : 0u;
+            h[i] = keep ? h[i] : 0u;
+        });
+    }
 #ifdef RSM_DIAG
     if (!(p.diag & 1u))
 #endif
     store_elem_tabs<N, 1024>(etab, etv);
     __syncthreads();
     d16_stamp(p, 2);
+    // the twiddle tables' loads go out now, beside the scale multiplies (the pool holds
+    // the scale tables until every wave is past them)
+    constexpr bool PF = kDec16PrefetchTw, PR = kDec16PrefetchRv;
+    uint32_t gv[PF ? grp_tab_per<G, E, 1024>() : 1];
+    if constexpr (PF) load_grp<G, E, false, 1024>(p.tw, -1, gv);
     sfor<E>([&](auto I) {  // scale by exp(err) (absent points are zero)
         constexpr int i = decltype(I)::value;
         if (((have0 | have1) >> i) & 1u) {
@@ -1666,7 +1755,8 @@ __global__ __launch_bounds__(1024, 4) void dec16h_kernel(Dec16 p) {
     });
     __syncthreads();  // every wave is past the scale tables
     // decoder skews: IFFT SKEW[-1 + b + d], FFT SKEW[b + d - 1]
-    stage_grp<G, E, false, 1024>(gtab, p.tw, -1);
+    if constexpr (PF) store_grp<G, E, 1024>(gtab, gv);
+    else stage_grp<G, E, false, 1024>(gtab, p.tw, -1);
     stage_res<R, E, 1024>(rtab, p.tw, -1);
     __syncthreads();  // twiddle tables staged
     d16_stamp(p, 3);
@@ -1688,17 +1778,26 @@ __global__ __launch_bounds__(1024, 4) void dec16h_kernel(Dec16 p) {
     xch_lanesplit<E>(l, xch, g, l32, false);
     xch_lanesplit<E>(h, xch, g, l32, false);
     d16_stamp(p, 9);
-    grp_xform<E, true, true>(l, h, gtab + g * (E - 1) * kTabW);
-    __syncthreads();  // every wave is past the twiddle tables
-    d16_stamp(p, 10);
     // the reveal recomputes its cell offsets (opaque codeword index: the compiler would
-    // otherwise keep the load phase's 64 offsets alive across the transforms)
+    // otherwise keep the load phase's 64 offsets alive across the transforms); its
+    // tables' loads go out before the group FFT, their LDS stores after it
     uint32_t qr = q, wr = w;
     asm volatile("" : "+s"(qr), "+s"(wr));
+    uint32_t rv[PR ? elem_tab_per<N, 1024>() : 1];
 #ifdef RSM_DIAG
     if (!(p.diag & 1u))
 #endif
-    stage_elem_tabs<N, 1024>(etab, p, qr, true);
+    if constexpr (PR) load_elem_tabs<N, 1024>(p, qr, true, rv);
+    grp_xform<E, true, true>(l, h, gtab + g * (E - 1) * kTabW);
+    __syncthreads();  // every wave is past the twiddle tables
+    d16_stamp(p, 10);
+#ifdef RSM_DIAG
+    if (!(p.diag & 1u))
+#endif
+    {
+        if constexpr (PR) store_elem_tabs<N, 1024>(etab, rv);
+        else stage_elem_tabs<N, 1024>(etab, p, qr, true);
+    }
     __syncthreads();  // reveal tables staged
     d16_stamp(p, 11);
     sfor<E>([&](auto I) {

@@ -87,6 +87,59 @@ __device__ __forceinline__ void gf8_muladd_ct(uint32_t& x, uint32_t y) {
     gf8_muladd_ct<L>(x, y, vconst<t.a_lo>(), vconst<t.b_lo>());
 }
 
+// Two multiplies share their selector shifts: ONE v_lshrrev_b64 per shift amount on the
+// pair (y1:y0) -- it issues at the rate of a 32-bit shift (profiles/r03_alu64.jsonl), so
+// two multiplies take 2 half-rate shifts instead of 4.  The bits y1 pushes into y0's top
+// byte are masked off with the selector bits.  Callers pair registers 2i, 2i + 1 of their
+// point arrays (an even-aligned register pair needs no copies).
+#ifdef RSM_GF8_NO_PAIR  // (diagnostic A/B builds only: every multiply shifts its own selectors)
+constexpr bool kGf8Pair = false;
+#else
+constexpr bool kGf8Pair = true;
+#endif
+struct Shift2 {
+    uint32_t b0, b1, c0, c1;  // y0 >> 3, y1 >> 3, y0 >> 6, y1 >> 6 (junk above the selector bits)
+};
+__device__ __forceinline__ Shift2 shift2(uint32_t y0, uint32_t y1) {
+    const uint64_t y = ((uint64_t)y1 << 32) | y0;
+    uint64_t s3, s6;
+    asm("v_lshrrev_b64 %0, 3, %2\n\tv_lshrrev_b64 %1, 6, %2" : "=&v"(s3), "=&v"(s6) : "v"(y));
+    return Shift2{(uint32_t)s3, (uint32_t)(s3 >> 32), (uint32_t)s6, (uint32_t)(s6 >> 32)};
+}
+// x ^= y * exp(L) from y and its pre-shifted selector sources y3 = y >> 3, y6 = y >> 6
+// (one scheduling unit, as gf8_muladd_ct)
+template <unsigned L>
+__device__ __forceinline__ void gf8_muladd_sel(uint32_t& x, uint32_t y, uint32_t y3, uint32_t y6, uint32_t ta, uint32_t tb) {
+    constexpr PermTab t = make_perm_tab(L);
+    uint32_t sa, sb, sc;
+    asm("v_and_b32 %[sa], %[m7], %[y]\n\t"
+        "v_and_b32 %[sb], %[m7], %[y3]\n\t"
+        "v_and_b32 %[sc], %[m3], %[y6]\n\t"
+        "v_perm_b32 %[sa], %[ahi], %[ta], %[sa]\n\t"
+        "v_perm_b32 %[sb], %[bhi], %[tb], %[sb]\n\t"
+        "v_perm_b32 %[sc], %[cc], %[cc], %[sc]\n\t"
+        "v_bitop3_b32 %[x], %[x], %[sa], %[sb] bitop3:0x96\n\t"
+        "v_xor_b32 %[x], %[x], %[sc]"
+        : [x] "+v"(x), [sa] "=&v"(sa), [sb] "=&v"(sb), [sc] "=&v"(sc)
+        : [y] "v"(y), [y3] "v"(y3), [y6] "v"(y6), [ta] "v"(ta), [tb] "v"(tb), [m7] "i"(0x07070707),
+          [m3] "i"(0x03030303), [ahi] "s"(t.a_hi), [bhi] "s"(t.b_hi), [cc] "s"(t.c));
+}
+// x0 ^= y0 * exp(L0), x1 ^= y1 * exp(L1) (tables ta0/tb0, ta1/tb1 as gf8_muladd_ct's)
+template <unsigned L0, unsigned L1>
+__device__ __forceinline__ void gf8_muladd2_ct(uint32_t& x0, uint32_t& x1, uint32_t y0, uint32_t y1, uint32_t ta0,
+                                               uint32_t tb0, uint32_t ta1, uint32_t tb1) {
+    const Shift2 q = shift2(y0, y1);
+    gf8_muladd_sel<L0>(x0, y0, q.b0, q.c0, ta0, tb0);
+    gf8_muladd_sel<L1>(x1, y1, q.b1, q.c1, ta1, tb1);
+}
+template <unsigned L0, unsigned L1>
+__device__ __forceinline__ void gf8_muladd2_ct(uint32_t& x0, uint32_t& x1, uint32_t y0, uint32_t y1) {
+    constexpr PermTab t0 = make_perm_tab(L0), t1 = make_perm_tab(L1);
+    const uint32_t ta0 = vconst<t0.a_lo>(), tb0 = vconst<t0.b_lo>();
+    if constexpr (L0 == L1) gf8_muladd2_ct<L0, L1>(x0, x1, y0, y1, ta0, tb0, ta0, tb0);
+    else gf8_muladd2_ct<L0, L1>(x0, x1, y0, y1, ta0, tb0, vconst<t1.a_lo>(), vconst<t1.b_lo>());
+}
+
 // Runtime (wave-uniform) log constant: tables for all 256 logs in constant memory.
 struct PermTabAll {
     PermTab t[256];
@@ -128,6 +181,19 @@ __device__ __forceinline__ void fft2(uint32_t& x, uint32_t& y) {
     if constexpr (L != 255u) gf8_muladd_ct<L>(x, y);
     y ^= x;
 }
+// the same for two butterflies of one block whose y registers form a pair (shift2)
+template <unsigned L>
+__device__ __forceinline__ void ifft2x2(uint32_t& x0, uint32_t& x1, uint32_t& y0, uint32_t& y1) {
+    y0 ^= x0;
+    y1 ^= x1;
+    if constexpr (L != 255u) gf8_muladd2_ct<L, L>(x0, x1, y0, y1);
+}
+template <unsigned L>
+__device__ __forceinline__ void fft2x2(uint32_t& x0, uint32_t& x1, uint32_t& y0, uint32_t& y1) {
+    if constexpr (L != 255u) gf8_muladd2_ct<L, L>(x0, x1, y0, y1);
+    y0 ^= x0;
+    y1 ^= x1;
+}
 
 // Inverse transform over N points, layer d = 1, 2, ..., N/2; block b uses
 // SKEW[OFF + b + d]  (encoder: OFF = m - 1; decoder: OFF = -1).
@@ -142,6 +208,15 @@ __device__ __forceinline__ void ifft_layers(uint32_t (&w)[N]) {
                 constexpr unsigned L = kGf8.skew[OFF + b + d];
                 if constexpr (L == 255u) {
                     static_for<d>([&](auto Q) { w[b + decltype(Q)::value + d] ^= w[b + decltype(Q)::value]; });
+                } else if constexpr (d >= 2 && kGf8Pair) {  // butterfly pairs: y registers i + d, i + d + 1
+                    constexpr PermTab t = make_perm_tab(L);
+                    const uint32_t ta = vconst<t.a_lo>(), tb = vconst<t.b_lo>();
+                    static_for<d / 2>([&](auto Q) {
+                        constexpr int i = b + 2 * decltype(Q)::value;
+                        w[i + d] ^= w[i];
+                        w[i + 1 + d] ^= w[i + 1];
+                        gf8_muladd2_ct<L, L>(w[i], w[i + 1], w[i + d], w[i + 1 + d], ta, tb, ta, tb);
+                    });
                 } else {
                     constexpr PermTab t = make_perm_tab(L);
                     const uint32_t ta = vconst<t.a_lo>(), tb = vconst<t.b_lo>();
@@ -169,6 +244,15 @@ __device__ __forceinline__ void fft_layers(uint32_t (&w)[N]) {
                 constexpr unsigned L = kGf8.skew[OFF + b + d];
                 if constexpr (L == 255u) {
                     static_for<d>([&](auto Q) { w[b + decltype(Q)::value + d] ^= w[b + decltype(Q)::value]; });
+                } else if constexpr (d >= 2 && kGf8Pair) {  // butterfly pairs: y registers i + d, i + d + 1
+                    constexpr PermTab t = make_perm_tab(L);
+                    const uint32_t ta = vconst<t.a_lo>(), tb = vconst<t.b_lo>();
+                    static_for<d / 2>([&](auto Q) {
+                        constexpr int i = b + 2 * decltype(Q)::value;
+                        gf8_muladd2_ct<L, L>(w[i], w[i + 1], w[i + d], w[i + 1 + d], ta, tb, ta, tb);
+                        w[i + d] ^= w[i];
+                        w[i + 1 + d] ^= w[i + 1];
+                    });
                 } else {
                     constexpr PermTab t = make_perm_tab(L);
                     const uint32_t ta = vconst<t.a_lo>(), tb = vconst<t.b_lo>();
@@ -547,8 +631,16 @@ __device__ __forceinline__ void split_high(uint32_t (&v)[PW]) {
                 if constexpr (((h / sd) & 1) == 0) {
                     constexpr int b = 2 * d * (h / (2 * sd));
                     constexpr unsigned L = kGf8.skew[b + d - 1];
-                    if constexpr (FFT) fft2<L>(v[h], v[h + sd]);
-                    else ifft2<L>(v[h], v[h + sd]);
+                    if constexpr (sd >= 2 && kGf8Pair) {  // pairs h, h + 1 of one block (shift2)
+                        if constexpr ((h & 1) == 0) {
+                            if constexpr (FFT) fft2x2<L>(v[h], v[h + 1], v[h + sd], v[h + sd + 1]);
+                            else ifft2x2<L>(v[h], v[h + 1], v[h + sd], v[h + sd + 1]);
+                        }
+                    } else if constexpr (FFT) {
+                        fft2<L>(v[h], v[h + sd]);
+                    } else {
+                        ifft2<L>(v[h], v[h + sd]);
+                    }
                 }
             });
         }
@@ -562,6 +654,18 @@ __device__ __forceinline__ uint32_t gf8_mul_tab(uint32_t y, const PermTab& t) {
     const uint32_t sc = (y >> 6) & 0x03030303u;
     return xor3(__builtin_amdgcn_perm(t.a_hi, t.a_lo, sa), __builtin_amdgcn_perm(t.b_hi, t.b_lo, sb),
                 __builtin_amdgcn_perm(t.c, t.c, sc));
+}
+
+// two points at once, sharing their selector shifts (shift2)
+__device__ __forceinline__ void gf8_mul_tab2(uint32_t& y0, uint32_t& y1, const PermTab& t0, const PermTab& t1) {
+    const Shift2 q = shift2(y0, y1);
+    const uint32_t a0 = y0 & 0x07070707u, a1 = y1 & 0x07070707u;
+    const uint32_t b0 = q.b0 & 0x07070707u, b1 = q.b1 & 0x07070707u;
+    const uint32_t c0 = q.c0 & 0x03030303u, c1 = q.c1 & 0x03030303u;
+    y0 = xor3(__builtin_amdgcn_perm(t0.a_hi, t0.a_lo, a0), __builtin_amdgcn_perm(t0.b_hi, t0.b_lo, b0),
+              __builtin_amdgcn_perm(t0.c, t0.c, c0));
+    y1 = xor3(__builtin_amdgcn_perm(t1.a_hi, t1.a_lo, a1), __builtin_amdgcn_perm(t1.b_hi, t1.b_lo, b1),
+              __builtin_amdgcn_perm(t1.c, t1.c, c1));
 }
 
 // bits [o, o + 64) of the 256-bit presence mask (zeros past the end)
@@ -644,11 +748,21 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
     // are still in flight (vmcnt retires in order: presence loads queued behind the
     // points made the locator wait for every point, 6.5 of 26 us per task,
     // profiles/r03_trace_decode.jsonl)
+    // (diagnostic A/B, RSM_DIAG with ds.delay == kDecFloor: the setup-free floor of a
+    // pre-pass design -- no presence loads, no error locator: a zero locator and every
+    // other point present (BenchmarkRepair's count), wrong
+    // output -- the time a decode kernel would take if a separate
+    // per-codeword pre-pass had resolved presence and locator before it)
+#ifdef RSM_DIAG
+    const bool floor = WE && ds.delay == kDecFloor;
+#else
+    constexpr bool floor = false;
+#endif
     uint32_t pv[4];
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
         const uint32_t e = g * 64u + lane;
-        pv[g] = e < Wd ? ds.presence[cell0 + e * cell_step] : 0u;
+        pv[g] = e < Wd ? (floor ? ((e + vec) & 1u) : ds.presence[cell0 + e * cell_step]) : 0u;
     }
     // wave 0's error-locator weights and the 256 multiply tables (5 KiB, staged into
     // LDS for the per-point gathers below), also ahead of the points
@@ -668,7 +782,7 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
     asm volatile("" ::: "memory");
 #ifdef RSM_DIAG
     if constexpr (!ZC) {
-        if (ds.delay && blockIdx.x >= gridDim.x / 2u) {  // A/B: stagger the two halves' loads
+        if (ds.delay && ds.delay != kDecFloor && blockIdx.x >= gridDim.x / 2u) {  // A/B: stagger the two halves' loads
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
             while (__builtin_amdgcn_s_memrealtime() - t0 < ds.delay) __builtin_amdgcn_s_sleep(2);
         }
@@ -696,7 +810,8 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
     // the staged table of its own points
     uint32_t er_packed = 0;  // (WE) this wave's copy of the locator, 4 entries per lane
     if constexpr (WE) {
-        uint32_t er[4];
+        uint32_t er[4] = {0u, 0u, 0u, 0u};
+        if (!floor) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint32_t i = lane * 4u + j;
@@ -710,6 +825,7 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
 #pragma unroll
         for (int j = 0; j < 4; ++j) er[j] = (er[j] * lw[j]) % 255u;
         fwht256(er, lane);
+        }
         er_packed = er[0] | (er[1] << 8) | (er[2] << 16) | (er[3] << 24);
     } else if (w == 0) {
         uint32_t er[4];
@@ -753,7 +869,8 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
     static_for<PW>([&](auto J) {
         constexpr int j = decltype(J)::value;
         if constexpr (WE) v[j] = ((have >> j) & 1ull) ? gf8_mul_rt(v[j], err_of(PW * w + j)) : 0u;
-        else v[j] = gf8_mul_tab(v[j], ptab[0][PW * w + j]);
+        else if constexpr (ZC || !kGf8Pair) v[j] = gf8_mul_tab(v[j], ptab[0][PW * w + j]);  // (paired: spills at NW = 4)
+        else if constexpr ((j & 1) == 0) gf8_mul_tab2(v[j], v[j + 1], ptab[0][PW * w + j], ptab[0][PW * w + j + 1]);
     });
     // 2. IFFT layers 1..PW/2 (per-wave twiddles)
     split_low<NW, PW, false>(v, w);
@@ -797,15 +914,27 @@ __device__ __forceinline__ void decode_split_task(const DecodeSet& ds, uint32_t 
     const __amdgpu_buffer_rsrc_t rm = make_rsrc((mirror ? ds.mirror : ds.base) + hcell);
     uint32_t sbase = pbase, sstep = pstep;
     asm volatile("" : "+s"(sbase), "+s"(sstep));
-    static_for<PW>([&](auto J) {
-        constexpr int j = decltype(J)::value;
+    static_for<PW / 2>([&](auto J2) {  // points j, j + 1 (gf8_mul_tab2: shared selector shifts)
+        constexpr int j = 2 * decltype(J2)::value;
         const uint32_t e = PW * w + j;
-        const uint32_t so = ((reveal >> j) & 1ull) ? sbase + (uint32_t)j * sstep : kOob;
-        uint32_t x;
-        if constexpr (WE) x = ((reveal >> j) & 1ull) ? gf8_mul_rt(v[j], 255u - err_of(e)) : 0u;
-        else x = gf8_mul_tab(v[j], ptab[1][e]);
-        __builtin_amdgcn_raw_buffer_store_b32(x, rs, off, so, 0);
-        if (mirror) __builtin_amdgcn_raw_buffer_store_b32(x, rm, off, so, 0);
+        uint32_t x[2];
+        if constexpr (WE) {
+            x[0] = ((reveal >> j) & 1ull) ? gf8_mul_rt(v[j], 255u - err_of(e)) : 0u;
+            x[1] = ((reveal >> (j + 1)) & 1ull) ? gf8_mul_rt(v[j + 1], 255u - err_of(e + 1)) : 0u;
+        } else if constexpr (ZC || !kGf8Pair) {
+            x[0] = gf8_mul_tab(v[j], ptab[1][e]);
+            x[1] = gf8_mul_tab(v[j + 1], ptab[1][e + 1]);
+        } else {
+            x[0] = v[j];
+            x[1] = v[j + 1];
+            gf8_mul_tab2(x[0], x[1], ptab[1][e], ptab[1][e + 1]);
+        }
+        static_for<2>([&](auto U) {
+            constexpr int u = decltype(U)::value;
+            const uint32_t so = ((reveal >> (j + u)) & 1ull) ? sbase + (uint32_t)(j + u) * sstep : kOob;
+            __builtin_amdgcn_raw_buffer_store_b32(x[u], rs, off, so, 0);
+            if (mirror) __builtin_amdgcn_raw_buffer_store_b32(x[u], rm, off, so, 0);
+        });
     });
     if constexpr (!ZC) dec_stamp(ds, 7);
 }
@@ -866,8 +995,16 @@ __device__ __forceinline__ void enc_split_high(uint32_t (&v)[PW]) {
                 if constexpr (((h / sd) & 1) == 0) {
                     constexpr int b = 2 * d * (h / (2 * sd));
                     constexpr unsigned L = kGf8.skew[(FFT ? -1 : 127) + b + d];
-                    if constexpr (FFT) fft2<L>(v[h], v[h + sd]);
-                    else ifft2<L>(v[h], v[h + sd]);
+                    if constexpr (sd >= 2 && kGf8Pair) {  // pairs h, h + 1 of one block (shift2)
+                        if constexpr ((h & 1) == 0) {
+                            if constexpr (FFT) fft2x2<L>(v[h], v[h + 1], v[h + sd], v[h + sd + 1]);
+                            else ifft2x2<L>(v[h], v[h + 1], v[h + sd], v[h + sd + 1]);
+                        }
+                    } else if constexpr (FFT) {
+                        fft2<L>(v[h], v[h + sd]);
+                    } else {
+                        ifft2<L>(v[h], v[h + sd]);
+                    }
                 }
             });
         }
@@ -882,7 +1019,13 @@ __device__ __forceinline__ void enc_split_mid(uint32_t (&v)[PW]) {
     constexpr unsigned L = log_of_sum8(kGf8.skew[127 + 64], kGf8.skew[-1 + 64]);
     static_for<PW>([&](auto H) {
         constexpr int h = decltype(H)::value;
-        if constexpr (((h / sd) & 1) == 0) {
+        if constexpr (kGf8Pair && sd >= 2 && ((h / sd) & 1) == 0 && (h & 1) == 0) {  // pairs h, h + 1 (shift2)
+            v[h + sd] ^= v[h];
+            v[h + sd + 1] ^= v[h + 1];
+            if constexpr (L != 255u) gf8_muladd2_ct<L, L>(v[h], v[h + 1], v[h + sd], v[h + sd + 1]);
+            v[h + sd] ^= v[h];
+            v[h + sd + 1] ^= v[h + 1];
+        } else if constexpr ((!kGf8Pair || sd < 2) && ((h / sd) & 1) == 0) {
             v[h + sd] ^= v[h];
             if constexpr (L != 255u) gf8_muladd_ct<L>(v[h], v[h + sd]);
             v[h + sd] ^= v[h];
@@ -1204,7 +1347,7 @@ constexpr bool kDecWaveErr = false;
 #ifdef RSM_DIAG
 static std::atomic<uint32_t> g_dec8_mode{0};  // 1: the other locator form (A/B)
 void set_dec8_diag_mode(uint32_t m) { g_dec8_mode.store(m); }
-static bool dec8_wave_err() { return g_dec8_mode.load() == 1 ? !kDecWaveErr : kDecWaveErr; }
+static bool dec8_wave_err() { return g_dec8_mode.load() >= 1 ? !kDecWaveErr : kDecWaveErr; }
 #else
 void set_dec8_diag_mode(uint32_t) {}
 static bool dec8_wave_err() { return kDecWaveErr; }
@@ -1225,7 +1368,7 @@ hipError_t launch_decode_gf8(const DecodeSet& ds0, hipStream_t st) {
     DecodeSet ds = ds0;
 #ifdef RSM_DIAG
     ds.trace = g_dec_trace.load();
-    ds.delay = g_dec_delay.load();
+    ds.delay = g_dec8_mode.load() == 2 ? kDecFloor : g_dec_delay.load();  // mode 2: the setup-free floor
 #else
     ds.trace = nullptr;
     ds.delay = 0;

@@ -121,7 +121,6 @@ __global__ __launch_bounds__(256) void tree_root_kernel(const uint32_t* __restri
     // tree U of the workgroup (wave U / TPW, its tree U % TPW)
     auto tlvl = [&](uint32_t U) { return lds_raw + (size_t)U * tree_lds_words(W); };
     auto tsub = [&](uint32_t U) { return tlvl(U) + (W / 2) * 8u; };
-    auto lvl = [&](uint32_t u) { return tlvl(wv * TPW + u); };
     auto sub = [&](uint32_t u) { return tsub(wv * TPW + u); };
     const uint32_t n = W;
     auto leaf_at = [&](uint32_t tree, uint32_t pos, uint32_t (&d)[8]) {

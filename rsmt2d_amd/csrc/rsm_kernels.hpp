@@ -95,6 +95,8 @@ struct DecodeSet {
     uint64_t pitch;
 };
 constexpr int kDecTraceWords = 8;
+// DecodeSet::delay value of the diagnostic setup-free floor (rsm_diag_set_dec8_mode(2))
+constexpr uint32_t kDecFloor = 0xFFFFFFFFu;
 void set_dec_diag_trace(uint32_t* d);
 uint32_t* dec_diag_trace_ptr();  // (diagnostic builds; the GF(2^16) single-pass decoders stamp kDec16TraceWords)
 constexpr int kDec16TraceWords = 16;

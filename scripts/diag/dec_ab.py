@@ -58,7 +58,8 @@ def main():
             chk(D.rsm_diag_set_dec16_five_pass(1 if v == 1 else 0))
             chk(D.rsm_diag_set_dec16_mode(0 if v == 1 else v))
             return 0
-        def set8(v):  # DECAB_V8: 0 production, 1 the other locator form, >= 100: load delay v - 100 ticks
+        def set8(v):  # DECAB_V8: 0 production, 1 the other locator form, 2 the setup-free floor of a
+            # pre-pass design (wrong output: timing only), >= 100: load delay v - 100 ticks
             chk(D.rsm_diag_set_dec8_mode(v if v < 100 else 0))
             return D.rsm_diag_set_dec_delay(v - 100 if v >= 100 else 0)
         setter = set16 if k > 128 else set8

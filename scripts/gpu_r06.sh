@@ -41,6 +41,23 @@ for s in ${STEPS:-smoke tests}; do
              step gf16ab 300 python3 scripts/diag/gf16_ab.py || exit 15 ;;
     repairtrace) step repair_trace 300 rocprofv3 --kernel-trace --memory-copy-trace -d "$PWD/$OUT/rtrace" -o run --output-format csv -- python3 scripts/diag/repair_trace.py ${RT_REPS:-6} || exit 16 ;;
     repab) step repair_ab 400 python3 scripts/diag/repair_ab.py || exit 17 ;;
+    singlepmc)  # counters of the single-square latency form (encode_gf8_split_kernel<8>)
+         i=0
+         for C in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_ACTIVE_INST_VALU" \
+                  "SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_SCA" \
+                  "SQ_INST_LEVEL_VMEM SQ_INSTS_SMEM SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM_RD GRBM_GUI_ACTIVE GRBM_COUNT"; do
+           i=$((i+1))
+           step single_sq$i 120 rocprofv3 --pmc $C -d "$PWD/$OUT/single_sq$i" -o run --output-format csv -- python3 scripts/diag/run_single.py 20 || exit 21
+         done
+         step single_stats 120 rocprofv3 --kernel-trace --stats -d "$PWD/$OUT/single_prof" -o run --output-format csv -- python3 scripts/diag/run_single.py 200 || exit 22
+         python3 scripts/sq_summary.py $OUT/single_sq.json $OUT/single_sq1 $OUT/single_sq2 $OUT/single_sq3 > $OUT/single_sq_summary.log 2>&1 ;;
+    decfloor) DECAB_KS=128 DECAB_V8=${DECAB_V8:-0,2,1} step decfloor 300 python3 scripts/diag/dec_ab.py || exit 23 ;;
+    gf8ab)  # GF(2^8) byte-table kernels: this build's diagnostic library against librsmt2d_hip_diag_ab.so
+         for rep in 1 2; do
+           for lib in rsmt2d_amd/librsmt2d_hip_diag.so rsmt2d_amd/librsmt2d_hip_diag_ab.so; do
+             RSM_DIAG_LIB=$lib step gf8ab_$(basename $lib .so)_$rep 300 python3 scripts/diag/gf8_ab.py || exit 24
+           done
+         done ;;
     lutprobe) step lutprobe 120 scripts/diag/lutprobe ${LUT_ITERS:-4096} || exit 18 ;;
     selab)  # same-box A/B of the production GF(2^16) kernels: this build's diagnostic library
             # against the variant build librsmt2d_hip_diag_ab.so (make ab AB_FLAGS=...)
