@@ -483,6 +483,124 @@ __device__ __forceinline__ void grp_xform_g(uint32_t (&l)[E], uint32_t (&h)[E], 
         });
     });
 }
+// Software-pipelined table reads (round 6): the NEXT block's table is read while this
+// block's butterflies run, the wait sits after them.  tab_issue_at puts the five
+// ds_read_b128 in flight without a wait; tab_wait waits for them and, through its "+v"
+// operands, is the point from which the compiler may read them.  The caller pins each
+// block's butterfly outputs before the wait (their asm operands), so the wait cannot be
+// hoisted above the butterflies it is meant to overlap.  Two table buffers alternate by
+// block parity (compile-time), so no table is copied.
+typedef uint32_t tab_v4 __attribute__((ext_vector_type(4)));
+struct Tab5 {
+    tab_v4 q[5];
+};
+template <int OFF>
+__device__ __forceinline__ void tab_issue_at(uint32_t base, Tab5& t) {
+    static_assert(OFF >= 0 && OFF + 64 < 65536, "ds_read offset field");
+    asm volatile(
+        "ds_read_b128 %0, %5 offset:%6\n\t"
+        "ds_read_b128 %1, %5 offset:%7\n\t"
+        "ds_read_b128 %2, %5 offset:%8\n\t"
+        "ds_read_b128 %3, %5 offset:%9\n\t"
+        "ds_read_b128 %4, %5 offset:%10"
+        : "=&v"(t.q[0]), "=&v"(t.q[1]), "=&v"(t.q[2]), "=&v"(t.q[3]), "=&v"(t.q[4])
+        : "v"(base), "i"(OFF), "i"(OFF + 16), "i"(OFF + 32), "i"(OFF + 48), "i"(OFF + 64)
+        : "memory");
+}
+__device__ __forceinline__ void tab_wait(Tab5& t) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(t.q[0]), "+v"(t.q[1]), "+v"(t.q[2]), "+v"(t.q[3]), "+v"(t.q[4]) :: "memory");
+}
+__device__ __forceinline__ void tab_unpack(const Tab5& t, uint32_t (&c)[kTabW]) {
+    sfor<5>([&](auto Q) {
+        constexpr int q = decltype(Q)::value;
+        c[4 * q] = t.q[q].x; c[4 * q + 1] = t.q[q].y; c[4 * q + 2] = t.q[q].z; c[4 * q + 3] = t.q[q].w;
+    });
+}
+// block n (execution order) of the first NLAY layers of a P-point transform (layer L:
+// P / 2 / 2^L blocks; IFFT ascending, FFT descending): its layer and its block
+template <int P, int NLAY, bool FFT>
+constexpr int pipe_layer(int n) {
+    for (int k = 0; k < NLAY; ++k) {
+        const int L = FFT ? NLAY - 1 - k : k, nb = P / 2 / (1 << L);
+        if (n < nb) return L;
+        n -= nb;
+    }
+    return -1;
+}
+template <int P, int NLAY, bool FFT>
+constexpr int pipe_block(int n) {
+    for (int k = 0; k < NLAY; ++k) {
+        const int L = FFT ? NLAY - 1 - k : k, nb = P / 2 / (1 << L);
+        if (n < nb) return n;
+        n -= nb;
+    }
+    return -1;
+}
+// grp_xform with pipelined table reads (E - 1 blocks, tables at wtab slot E - (E >> L) + block)
+template <int E, bool FFT>
+__device__ __forceinline__ void grp_xform_pipe(uint32_t (&l)[E], uint32_t (&h)[E], const uint32_t* wtab) {
+    constexpr int NB = E - 1, NL = ilog2c(E);
+    const uint32_t base = (uint32_t)(uintptr_t)wtab;
+    Tab5 ta, tb;
+    {
+        constexpr int L0 = pipe_layer<E, NL, FFT>(0), B0 = pipe_block<E, NL, FFT>(0);
+        tab_issue_at<(E - (E >> L0) + B0) * kTabW * 4>(base, ta);
+        tab_wait(ta);
+    }
+    sfor<NB>([&](auto N) {
+        constexpr int n = decltype(N)::value;
+        constexpr int L = pipe_layer<E, NL, FFT>(n), bk = pipe_block<E, NL, FFT>(n), d = 1 << L;
+        Tab5& cur = (n & 1) ? tb : ta;
+        Tab5& nxt = (n & 1) ? ta : tb;
+        if constexpr (n + 1 < NB) {
+            constexpr int L1 = pipe_layer<E, NL, FFT>(n + 1), B1 = pipe_block<E, NL, FFT>(n + 1);
+            tab_issue_at<(E - (E >> L1) + B1) * kTabW * 4>(base, nxt);
+        }
+        uint32_t c[kTabW];
+        tab_unpack(cur, c);
+        sfor<d>([&](auto Q) {
+            constexpr int i = bk * 2 * d + decltype(Q)::value;
+            if constexpr (FFT) fft2v(l[i], h[i], l[i + d], h[i + d], c);
+            else ifft2v(l[i], h[i], l[i + d], h[i + d], c);
+            asm volatile("" : "+v"(l[i]), "+v"(h[i]), "+v"(l[i + d]), "+v"(h[i + d]));
+        });
+        if constexpr (n + 1 < NB) tab_wait(nxt);
+    });
+}
+// rtab slot of residue block n: IFFT slots 0..R-2, FFT R-1..2R-3 (stage_res)
+template <int R, bool FFT>
+constexpr int res_pipe_slot(int n) {
+    constexpr int NL = ilog2c(R) - 1;
+    const int L = pipe_layer<R, NL, FFT>(n), b = pipe_block<R, NL, FFT>(n);
+    return (FFT ? R - 1 : 0) + (R - (R >> L)) + b;
+}
+// res_xform (one residue per lane group, E == R, MERGED: the top layer is res_mid) with
+// pipelined table reads: IFFT slots 0..R-2, FFT slots R-1..2R-3 of rtab
+template <int R, bool FFT>
+__device__ __forceinline__ void res_xform_pipe(uint32_t (&l)[R], uint32_t (&h)[R], const uint32_t* rtab) {
+    constexpr int NL = ilog2c(R) - 1, NB = R - 2;  // layers dj = 1 .. R/4 (the merged top excluded)
+    const uint32_t base = (uint32_t)(uintptr_t)rtab;
+    Tab5 ta, tb;
+    tab_issue_at<res_pipe_slot<R, FFT>(0) * kTabW * 4>(base, ta);
+    tab_wait(ta);
+    sfor<NB>([&](auto N) {
+        constexpr int n = decltype(N)::value;
+        constexpr int L = pipe_layer<R, NL, FFT>(n), bk = pipe_block<R, NL, FFT>(n), dj = 1 << L;
+        Tab5& cur = (n & 1) ? tb : ta;
+        Tab5& nxt = (n & 1) ? ta : tb;
+        if constexpr (n + 1 < NB) tab_issue_at<res_pipe_slot<R, FFT>(n + 1) * kTabW * 4>(base, nxt);
+        uint32_t c[kTabW];
+        tab_unpack(cur, c);
+        sfor<dj>([&](auto Q) {
+            constexpr int j = bk * 2 * dj + decltype(Q)::value;
+            if constexpr (FFT) fft2v(l[j], h[j], l[j + dj], h[j + dj], c);
+            else ifft2v(l[j], h[j], l[j + dj], h[j + dj], c);
+            asm volatile("" : "+v"(l[j]), "+v"(h[j]), "+v"(l[j + dj]), "+v"(h[j + dj]));
+        });
+        if constexpr (n + 1 < NB) tab_wait(nxt);
+    });
+}
+
 // Residue-layout register of (residue s of the wave, j): s R + j (the full-buffer
 // exchange), or -- IL, the half-buffer exchange -- (E / R) j + s, so that the
 // registers a wave sends in one pass of xch_plane_half are exactly the ones it
@@ -805,7 +923,9 @@ __device__ __forceinline__ void xch_part(uint32_t (&v)[E], uint32_t (*xch)[XL], 
 // PF: the next task's points are loaded while the current one transforms
 // XL: lanes per exchange pass (32: production, two workgroups per CU; 8: the 49 KiB form,
 // enc16h3_kernel, three workgroups per CU at 80 registers)
-template <bool JIT, bool PF, int XL>
+// PIPE (round 6, diagnostic form 21): twiddle tables read one block ahead (grp_xform_pipe /
+// res_xform_pipe) instead of just in time
+template <bool JIT, bool PF, int XL, bool PIPE = false>
 __device__ __forceinline__ void enc16h_body(const Enc16& p) {
     constexpr int M = 256, E = 16, G = 16, R = 16, THREADS = 512;
     constexpr int GT = G * (E - 1) * kTabW;
@@ -861,15 +981,19 @@ __device__ __forceinline__ void enc16h_body(const Enc16& p) {
         } else {
             load_task(task, l, h);
         }
-        grp_xform<E, false, JIT>(l, h, tI);
+        if constexpr (PIPE) grp_xform_pipe<E, false>(l, h, tI);
+        else grp_xform<E, false, JIT>(l, h, tI);
         xch_part<E, XL>(l, xch, g, l32, true);
         xch_part<E, XL>(h, xch, g, l32, true);
-        res_xform<E, R, false, true, JIT>(l, h, rtab);
+        if constexpr (PIPE) res_xform_pipe<R, false>(l, h, rtab);
+        else res_xform<E, R, false, true, JIT>(l, h, rtab);
         res_mid<E, R>(l, h, p.mid);
-        res_xform<E, R, true, true, JIT>(l, h, rtab);
+        if constexpr (PIPE) res_xform_pipe<R, true>(l, h, rtab);
+        else res_xform<E, R, true, true, JIT>(l, h, rtab);
         xch_part<E, XL>(l, xch, g, l32, false);
         xch_part<E, XL>(h, xch, g, l32, false);
-        grp_xform<E, true, JIT>(l, h, tF);
+        if constexpr (PIPE) grp_xform_pipe<E, true>(l, h, tF);
+        else grp_xform<E, true, JIT>(l, h, tF);
         const auto out = rsrc(p.cs.out_base + rel);
         sfor<E>([&](auto I) {
             constexpr int i = decltype(I)::value;
@@ -881,9 +1005,9 @@ __device__ __forceinline__ void enc16h_body(const Enc16& p) {
     }
 }
 
-template <bool JIT, bool PF = false>
+template <bool JIT, bool PF = false, bool PIPE = false>
 __global__ __launch_bounds__(512, 4) void enc16h_kernel(Enc16 p) {
-    enc16h_body<JIT, PF, 32>(p);
+    enc16h_body<JIT, PF, 32, PIPE>(p);
 }
 // three workgroups per CU: 6 waves per SIMD (80 registers), 49 KiB of LDS each
 __global__ __launch_bounds__(512, 6) void enc16h3_kernel(Enc16 p) {
@@ -910,7 +1034,8 @@ __device__ __forceinline__ uint32_t swapped_elem(uint32_t w, int r, uint32_t hh)
 }
 
 // PF: the next task's points are loaded while the current one transforms (32 more registers)
-template <bool JIT, bool PF = false>
+// PIPE (round 6, diagnostic form 21): twiddle tables read one block ahead
+template <bool JIT, bool PF = false, bool PIPE = false>
 __global__ __launch_bounds__(1024, 4) void enc16h512_kernel(Enc16 p) {
     constexpr int M = 512, E = 16, G = 32, R = 16, THREADS = 1024;
     constexpr int GT = G * (E - 1) * kTabW, WT = 16 * kTabW, RT = 2 * (R - 1) * kTabW;
@@ -978,7 +1103,8 @@ __global__ __launch_bounds__(1024, 4) void enc16h512_kernel(Enc16 p) {
         } else {
             load_task(task, l, h);
         }
-        grp_xform<E, false, JIT>(l, h, tI);
+        if constexpr (PIPE) grp_xform_pipe<E, false>(l, h, tI);
+        else grp_xform<E, false, JIT>(l, h, tI);
         {  // d = 16
             sfor<E / 2>([&](auto P) {
                 constexpr int i = 2 * decltype(P)::value;
@@ -1019,9 +1145,11 @@ __global__ __launch_bounds__(1024, 4) void enc16h512_kernel(Enc16 p) {
         };
         to_res(l);
         to_res(h);
-        res_xform<R, R, false, true, JIT>(l, h, rtab);
+        if constexpr (PIPE) res_xform_pipe<R, false>(l, h, rtab);
+        else res_xform<R, R, false, true, JIT>(l, h, rtab);
         res_mid<R, R>(l, h, p.mid);
-        res_xform<R, R, true, true, JIT>(l, h, rtab);
+        if constexpr (PIPE) res_xform_pipe<R, true>(l, h, rtab);
+        else res_xform<R, R, true, true, JIT>(l, h, rtab);
         to_grp(l);
         to_grp(h);
         {  // d = 16, then back to the plain group arrangement
@@ -1038,7 +1166,8 @@ __global__ __launch_bounds__(1024, 4) void enc16h512_kernel(Enc16 p) {
                 swap_halves(h[i], h[i + 1]);
             });
         }
-        grp_xform<E, true, JIT>(l, h, tF);
+        if constexpr (PIPE) grp_xform_pipe<E, true>(l, h, tF);
+        else grp_xform<E, true, JIT>(l, h, tF);
         const auto out = rsrc(p.cs.out_base + rel);
         sfor<E>([&](auto I) {
             constexpr int i = decltype(I)::value;
@@ -2120,6 +2249,15 @@ hipError_t run_encode(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st) {
                 hipLaunchKernelGGL((enc16h512_kernel<true, true>), dim3(gh), dim3(1024), 0, st, ph);
                 return hipGetLastError();
             }
+            case 21: {  // round 6: the production form with tables read one block ahead
+                Enc16 ph = p;
+                ph.chunks = (cs.S + 255) / 256;
+                const uint64_t th = (uint64_t)cs.count * ph.chunks;
+                if (th >= (1ull << 31)) return hipErrorInvalidValue;
+                const uint32_t gh = th > g.cus ? g.cus : (uint32_t)th;
+                hipLaunchKernelGGL((enc16h512_kernel<true, false, true>), dim3(gh), dim3(1024), 0, st, ph);
+                return hipGetLastError();
+            }
             case 16: {
                 Enc16 ph = p;
                 ph.chunks = (cs.S + 255) / 256;
@@ -2153,6 +2291,7 @@ hipError_t run_encode(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st) {
             const uint32_t gh3 = th > 3ull * g.cus ? 3u * g.cus : (uint32_t)th;
             if (form == 20) hipLaunchKernelGGL(enc16h3_kernel, dim3(gh3), dim3(512), 0, st, ph);
             else if (form == 19) hipLaunchKernelGGL((enc16h_kernel<true, true>), dim3(gh), dim3(512), 0, st, ph);
+            else if (form == 21) hipLaunchKernelGGL((enc16h_kernel<true, false, true>), dim3(gh), dim3(512), 0, st, ph);
             else if (form == 14) hipLaunchKernelGGL(enc16h_kernel<false>, dim3(gh), dim3(512), 0, st, ph);
             else hipLaunchKernelGGL(enc16h_kernel<true>, dim3(gh), dim3(512), 0, st, ph);
             return hipGetLastError();
