@@ -238,8 +238,8 @@ def test_single_launch_at_bench_scale(lib):
     (rsm_dev_equal), over several rounds.  The parity quadrants are re-poisoned
     before every launch, so a Q1-column set that read a stale or unfinished Q1 (the
     inter-workgroup hand-off of extend_gf8_bs128q_kernel) could not match by
-    accident; the two-launch references are themselves oracle-checked at their
-    first and last square.  Reference: extendeddatasquare.go:154-227."""
+    accident; the two-launch references are themselves oracle-checked, every square
+    of every buffer (1,536 squares).  Reference: extendeddatasquare.go:154-227."""
     ctx = R.device_context(0)
     k, S, B, NS = 128, 512, 512, 3
     W = 2 * k
@@ -256,9 +256,15 @@ def test_single_launch_at_bench_scale(lib):
             R._check(lib.rsm_extend_squares_phase_dev(ctx, ref[i].ptr, k, S, B, 1, None))
             R._check(lib.rsm_extend_squares_phase_dev(ctx, ref[i].ptr, k, S, B, 2, None))
             R._check(lib.rsm_sync(ctx))
-            for j in (0, B - 1):
+            # every reference square against the oracle (the AVX-512 + GFNI build of the
+            # restatement where the host has it -- pinned to the scalar oracle by
+            # tests/test_oracle.py -- else the first and last square with the scalar one)
+            gfni = oracle.gfni_supported()
+            for j in (range(B) if gfni else (0, B - 1)):
                 got = ref[i].download(sq, j * sq).reshape(W, W, S)
-                assert np.array_equal(got, oracle.extend_square(got[:k, :k].copy(), nthreads=8)), (i, j)
+                ods = got[:k, :k].copy()
+                want = oracle.extend_square_gfni(ods, nthreads=16) if gfni else oracle.extend_square(ods, nthreads=8)
+                assert np.array_equal(got, want), (i, j)
         for s in st:
             R._check(lib.rsm_stream_create(ctx, ctypes.byref(s)))
         eq = ctypes.c_int()
