@@ -923,8 +923,8 @@ __device__ __forceinline__ void xch_part(uint32_t (&v)[E], uint32_t (*xch)[XL], 
 // PF: the next task's points are loaded while the current one transforms
 // XL: lanes per exchange pass (32: production, two workgroups per CU; 8: the 49 KiB form,
 // enc16h3_kernel, three workgroups per CU at 80 registers)
-// PIPE (round 6, diagnostic form 21): twiddle tables read one block ahead (grp_xform_pipe /
-// res_xform_pipe) instead of just in time
+// PIPE (production since round 6; PIPE = false is diagnostic form 22): twiddle tables read
+// one block ahead (grp_xform_pipe / res_xform_pipe) instead of just in time
 template <bool JIT, bool PF, int XL, bool PIPE = false>
 __device__ __forceinline__ void enc16h_body(const Enc16& p) {
     constexpr int M = 256, E = 16, G = 16, R = 16, THREADS = 512;
@@ -995,9 +995,15 @@ __device__ __forceinline__ void enc16h_body(const Enc16& p) {
         if constexpr (PIPE) grp_xform_pipe<E, true>(l, h, tF);
         else grp_xform<E, true, JIT>(l, h, tF);
         const auto out = rsrc(p.cs.out_base + rel);
+        // the store offsets are recomputed here from opaque copies (the compiler would
+        // otherwise keep the load phase's 16 per-lane offsets alive across the transform)
+        uint32_t slo = lo, slim = lim;
+#ifndef RSM_ENC16_HOISTED_OFFSETS  // (diagnostic A/B builds: the round-5 hoisted offsets)
+        asm volatile("" : "+v"(slo), "+v"(slim));
+#endif
         sfor<E>([&](auto I) {
             constexpr int i = decltype(I)::value;
-            const uint32_t v = (uint32_t)i < lim ? lo : kOob16;
+            const uint32_t v = (uint32_t)i < slim ? slo : kOob16;
             const uint32_t so = oo + (2u * E * w + i < k ? (2u * E * w + i) * es : 0u);
             st(out, l[i], v, so);
             st(out, h[i], v + 32u, so);
@@ -1034,7 +1040,8 @@ __device__ __forceinline__ uint32_t swapped_elem(uint32_t w, int r, uint32_t hh)
 }
 
 // PF: the next task's points are loaded while the current one transforms (32 more registers)
-// PIPE (round 6, diagnostic form 21): twiddle tables read one block ahead
+// PIPE (production since round 6; PIPE = false is diagnostic form 22): twiddle tables
+// read one block ahead
 template <bool JIT, bool PF = false, bool PIPE = false>
 __global__ __launch_bounds__(1024, 4) void enc16h512_kernel(Enc16 p) {
     constexpr int M = 512, E = 16, G = 32, R = 16, THREADS = 1024;
@@ -1169,9 +1176,15 @@ __global__ __launch_bounds__(1024, 4) void enc16h512_kernel(Enc16 p) {
         if constexpr (PIPE) grp_xform_pipe<E, true>(l, h, tF);
         else grp_xform<E, true, JIT>(l, h, tF);
         const auto out = rsrc(p.cs.out_base + rel);
+        // the store offsets are recomputed here from opaque copies (the compiler would
+        // otherwise keep the load phase's 16 per-lane offsets alive across the transform)
+        uint32_t slo = lo, slim = lim;
+#ifndef RSM_ENC16_HOISTED_OFFSETS  // (diagnostic A/B builds: the round-5 hoisted offsets)
+        asm volatile("" : "+v"(slo), "+v"(slim));
+#endif
         sfor<E>([&](auto I) {
             constexpr int i = decltype(I)::value;
-            const uint32_t v = (uint32_t)i < lim ? lo : kOob16;
+            const uint32_t v = (uint32_t)i < slim ? slo : kOob16;
             const uint32_t so = oo + (2u * E * w + i < k ? (2u * E * w + i) * es : 0u);
             st(out, l[i], v, so);
             st(out, h[i], v + 32u, so);
@@ -2226,7 +2239,19 @@ hipError_t run_encode(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st) {
         // the merged middle pair, 16 the half-wave form with compiler-scheduled table
         // reads (0.505-0.510)
         switch (enc16_form()) {
-            case 0: {
+            case 0:      // production since round 6: the half-wave form with tables read one
+            case 21: {   // block ahead (form 21 in round 6's A/B: c5 0.451-0.466 against
+                         // 0.466-0.469 ms for just-in-time tables, now form 22;
+                         // profiles/r06i_gf16_pipe_ab.jsonl)
+                Enc16 ph = p;
+                ph.chunks = (cs.S + 255) / 256;
+                const uint64_t th = (uint64_t)cs.count * ph.chunks;
+                if (th >= (1ull << 31)) return hipErrorInvalidValue;
+                const uint32_t gh = th > g.cus ? g.cus : (uint32_t)th;
+                hipLaunchKernelGGL((enc16h512_kernel<true, false, true>), dim3(gh), dim3(1024), 0, st, ph);
+                return hipGetLastError();
+            }
+            case 22: {  // the round-4/5 production form: just-in-time table reads
                 Enc16 ph = p;
                 ph.chunks = (cs.S + 255) / 256;
                 const uint64_t th = (uint64_t)cs.count * ph.chunks;
@@ -2247,15 +2272,6 @@ hipError_t run_encode(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st) {
                 if (th >= (1ull << 31)) return hipErrorInvalidValue;
                 const uint32_t gh = th > g.cus ? g.cus : (uint32_t)th;
                 hipLaunchKernelGGL((enc16h512_kernel<true, true>), dim3(gh), dim3(1024), 0, st, ph);
-                return hipGetLastError();
-            }
-            case 21: {  // round 6: the production form with tables read one block ahead
-                Enc16 ph = p;
-                ph.chunks = (cs.S + 255) / 256;
-                const uint64_t th = (uint64_t)cs.count * ph.chunks;
-                if (th >= (1ull << 31)) return hipErrorInvalidValue;
-                const uint32_t gh = th > g.cus ? g.cus : (uint32_t)th;
-                hipLaunchKernelGGL((enc16h512_kernel<true, false, true>), dim3(gh), dim3(1024), 0, st, ph);
                 return hipGetLastError();
             }
             case 16: {
@@ -2291,9 +2307,12 @@ hipError_t run_encode(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st) {
             const uint32_t gh3 = th > 3ull * g.cus ? 3u * g.cus : (uint32_t)th;
             if (form == 20) hipLaunchKernelGGL(enc16h3_kernel, dim3(gh3), dim3(512), 0, st, ph);
             else if (form == 19) hipLaunchKernelGGL((enc16h_kernel<true, true>), dim3(gh), dim3(512), 0, st, ph);
-            else if (form == 21) hipLaunchKernelGGL((enc16h_kernel<true, false, true>), dim3(gh), dim3(512), 0, st, ph);
             else if (form == 14) hipLaunchKernelGGL(enc16h_kernel<false>, dim3(gh), dim3(512), 0, st, ph);
-            else hipLaunchKernelGGL(enc16h_kernel<true>, dim3(gh), dim3(512), 0, st, ph);
+            else if (form == 22) hipLaunchKernelGGL(enc16h_kernel<true>, dim3(gh), dim3(512), 0, st, ph);
+            // production since round 6 (and form 21): tables read one block ahead; c4
+            // 0.400-0.410 against 0.409-0.422 ms for just-in-time tables (form 22,
+            // profiles/r06i_gf16_pipe_ab.jsonl)
+            else hipLaunchKernelGGL((enc16h_kernel<true, false, true>), dim3(gh), dim3(512), 0, st, ph);
             return hipGetLastError();
         }
     }

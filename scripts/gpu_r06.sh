@@ -64,6 +64,14 @@ for s in ${STEPS:-smoke tests}; do
              RSM_DIAG_LIB=$lib REPAB_KS=${REPAB_KS:-128,256,512} step repab_$(basename $lib .so)_$rep 300 python3 scripts/diag/repair_ab.py || exit 25
            done
          done ;;
+    gf16ab2)  # GF(2^16) encoder forms (GF16AB_FORMS / GF16AB_C4FORMS): this build's diagnostic library
+              # against librsmt2d_hip_diag_ab.so
+         for rep in 1 2; do
+           for lib in rsmt2d_amd/librsmt2d_hip_diag.so rsmt2d_amd/librsmt2d_hip_diag_ab.so; do
+             RSM_DIAG_LIB=$lib GF16AB_FORMS=${GF16AB_FORMS:-0,21} GF16AB_C4FORMS=${GF16AB_C4FORMS:-0,21} GF16AB_REPS=2 \
+               step gf16ab2_$(basename $lib .so)_$rep 300 python3 scripts/diag/gf16_ab.py || exit 26
+           done
+         done ;;
     lutprobe) step lutprobe 120 scripts/diag/lutprobe ${LUT_ITERS:-4096} || exit 18 ;;
     selab)  # same-box A/B of the production GF(2^16) kernels: this build's diagnostic library
             # against the variant build librsmt2d_hip_diag_ab.so (make ab AB_FLAGS=...)
