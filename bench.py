@@ -477,12 +477,13 @@ def bench_c5_c_abi(G, L, R, steps, k=512, S=512):
     return out
 
 
-def bench_c5_g8_projection(ctx, buf, L, R, k, S, G=8, reps=20):
+def bench_c5_g8_projection(ctx, buf, L, R, k, S, G=8, reps=20, device=0):
     """One rank's compute at G = 8 GPUs, timed on this one GPU (the
     row-sharded schedule of rsm_multi_extend_dev, extendeddatasquare.go:204-207):
-    rsm_extend_rows_dev of k/G Q0 rows (the row pass of one shard) and
-    rsm_extend_cols_dev of 2k/G columns (its column slice after the exchange), device
-    events around `reps` back-to-back calls each.  The exchange is NOT measured (no
+    rsm_extend_rows_blocks_dev of k/G Q0 rows (the row pass of one shard, writing the
+    all-to-all send blocks itself: no pack pass) and rsm_extend_cols_dev of 2k/G columns
+    (its column slice after the exchange), device events around `reps` back-to-back calls
+    each; the plain row pass (rsm_extend_rows_dev) is timed beside it.  The exchange is NOT measured (no
     multi-GPU node here): its bytes per GPU are reported, and `exchange_est_ms` prices
     them at the 7 xGMI links' 153 GB/s peak each (a lower bound on the exchange)."""
     import ctypes
@@ -492,8 +493,11 @@ def bench_c5_g8_projection(ctx, buf, L, R, k, S, G=8, reps=20):
     R._check(L.rsm_event_create(ctx, ctypes.byref(e1)))
     ms = ctypes.c_float()
     times = {}
+    send = R.DeviceBuffer((k // G) * W * S, device)
     try:
-        for name, fn in (("rows", lambda: L.rsm_extend_rows_dev(ctx, buf.ptr, k, S, 0, k // G, None)),
+        for name, fn in (("rows", lambda: L.rsm_extend_rows_blocks_dev(ctx, buf.ptr, k, S, 0, k // G, send.ptr, G,
+                                                                        None)),
+                         ("rows_plain", lambda: L.rsm_extend_rows_dev(ctx, buf.ptr, k, S, 0, k // G, None)),
                          ("cols", lambda: L.rsm_extend_cols_dev(ctx, buf.ptr, k, S, 0, W // G, None))):
             R._check(fn())
             R._check(L.rsm_event_record(ctx, e0, None))
@@ -506,12 +510,13 @@ def bench_c5_g8_projection(ctx, buf, L, R, k, S, G=8, reps=20):
     finally:
         L.rsm_event_destroy(e0)
         L.rsm_event_destroy(e1)
+        send.free()
     ag = (G - 1) * (k // G) * W * S     # all-gather of the top half: received per GPU
     a2a = (G - 1) * (k // G) * (W // G) * S  # all-to-all of column blocks: received per GPU
     link = 7 * 153e9
     comp = times["rows"] + times["cols"]
     return {"label": "projection, exchange not measured: one rank's compute at G = 8 on one GPU",
-            "rows_ms": round(times["rows"], 4), "rows": k // G, "row_tasks": (k // G) * ((S + 255) // 256),
+            "rows_ms": round(times["rows"], 4), "rows_plain_ms": round(times["rows_plain"], 4), "rows": k // G, "row_tasks": (k // G) * ((S + 255) // 256),
             "cols_ms": round(times["cols"], 4), "cols": W // G,
             "compute_ms": round(comp, 4),
             "allgather_received_bytes_per_gpu": ag, "alltoall_received_bytes_per_gpu": a2a,
@@ -541,7 +546,7 @@ def bench_c5(world, rank, local, dist, steps, L, R):
             R._check(L.rsm_extend_squares_dev(ctx, buf.ptr, k, S, 1, None))
         R._check(L.rsm_sync(ctx))
         dt = (time.perf_counter() - t0) / steps
-        g8 = bench_c5_g8_projection(ctx, buf, L, R, k, S)
+        g8 = bench_c5_g8_projection(ctx, buf, L, R, k, S, device=local)
         buf.free()
         # the C-ABI multi-GPU entry point with a clique of one
         multi = bench_c5_c_abi(1, L, R, steps)

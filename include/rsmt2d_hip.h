@@ -135,6 +135,14 @@ int rsm_extend_rows_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_si
                         uint32_t nrows, void* stream);
 int rsm_extend_cols_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size, uint32_t col0,
                         uint32_t ncols, void* stream);
+/* The row pass of rows [row0, row0+nrows) (as rsm_extend_rows_dev) that also leaves the
+ * extended rows split into `nblocks` column blocks of 2k/nblocks columns each: block h
+ * at d_blocks + h*nrows*(2k/nblocks)*S, row pitch (2k/nblocks)*S -- the send buffer of
+ * the all-to-all multi-GPU schedule (rank h receives block h), with no copy pass where the
+ * encoder stores the blocks itself (GF(2^16), k <= 512, k and the block width multiples
+ * of 32; other shapes: the row pass, then strided device copies).  Asynchronous. */
+int rsm_extend_rows_blocks_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size, uint32_t row0,
+                               uint32_t nrows, void* d_blocks, uint32_t nblocks, void* stream);
 /* Generic device batch of `count` codewords (k data shares -> k parity shares each,
  * the Encode of leopard.go:28-45 for every codeword): data share e of codeword q is
  * at d_in + q*cw_stride + e*share_stride, its parity share e is written at
@@ -192,9 +200,12 @@ int rsm_multi_host_free(rsm_multi* m, void* p);
  * column pass); pageable memory also works (staged by HIP).  Synchronous. */
 int rsm_multi_extend_square_inplace(rsm_multi* m, uint8_t* eds, uint32_t k, uint32_t share_size, int schedule);
 /* Device-resident form: d_eds[g] is a full [2k][2k][S] buffer on GPU g holding Q0
- * rows of shard g; afterwards it holds shard g's rows of the top half and its
- * column slice [g 2k/G, (g+1) 2k/G) of the whole square (all-gather: the whole top
- * half as well).  Asynchronous on the context streams; rsm_multi_sync waits. */
+ * rows of shard g; afterwards it holds shard g's rows of the top half and the bottom
+ * half [Q2|Q3] of its column slice [g 2k/G, (g+1) 2k/G) (all-gather: the whole top half
+ * as well; all-to-all over the copy passes -- GF(2^8), k > 512 or blocks under 32 rows or
+ * columns -- also the other shards' rows of its column slice; the copy-free all-to-all
+ * leaves those in the clique's receive staging, where its column pass read them).
+ * Asynchronous on the context streams; rsm_multi_sync waits. */
 int rsm_multi_extend_dev(rsm_multi* m, void* const* d_eds, uint32_t k, uint32_t share_size, int schedule);
 int rsm_multi_sync(rsm_multi* m);
 

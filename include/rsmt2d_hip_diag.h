@@ -82,6 +82,15 @@ int rsm_diag_queue_check(rsm_ctx* ctx, void* stream);
 int rsm_diag_extend_pipeline_dev(rsm_ctx* ctx, void* d_rows_eds, void* d_cols_eds, uint32_t k, uint32_t share_size,
                                  uint32_t count, void* stream);
 
+/* The copy-free multi-GPU all-to-all (rsm_multi_extend_dev, RSM_SCHED_ALLTOALL, GF(2^16)
+ * shapes whose row and column blocks are multiples of 32) with G "GPUs" emulated on ONE
+ * context: rank g's row pass with the encoder's side output into its send staging, device
+ * copies in place of the RCCL send/recv, rank g's column pass reading the received blocks
+ * in place.  d_eds[g] is rank g's [2k][2k][S] buffer holding the Q0 rows of shard g;
+ * afterwards it holds shard g's rows of the top half and the bottom half of its column
+ * slice.  Synchronous. */
+int rsm_diag_alltoall_emulated(rsm_ctx* ctx, void* const* d_eds, int G, uint32_t k, uint32_t share_size);
+
 #ifdef __cplusplus
 }
 #endif

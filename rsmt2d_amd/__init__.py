@@ -145,6 +145,7 @@ SIGNATURES = {
     "rsm_extend_squares_dev": (_I32, [_VP, _VP, _U32, _U32, _U32, _VP]),
     "rsm_extend_squares_phase_dev": (_I32, [_VP, _VP, _U32, _U32, _U32, _I32, _VP]),
     "rsm_extend_rows_dev": (_I32, [_VP, _VP, _U32, _U32, _U32, _U32, _VP]),
+    "rsm_extend_rows_blocks_dev": (_I32, [_VP, _VP, _U32, _U32, _U32, _U32, _VP, _U32, _VP]),
     "rsm_extend_cols_dev": (_I32, [_VP, _VP, _U32, _U32, _U32, _U32, _VP]),
     "rsm_roots_dev": (_I32, [_VP, _VP, _U32, _U32, _VP, _VP]),
     "rsm_roots_squares_dev": (_I32, [_VP, _VP, _U32, _U32, _U32, _VP, _VP]),
@@ -208,6 +209,7 @@ DIAG_SIGNATURES = {
     "rsm_diag_extend_fused": (_I32, [_VP, _VP, _U32, _U32, _U32, _U32, _VP]),
     "rsm_diag_queue_check": (_I32, [_VP, _VP]),
     "rsm_diag_extend_pipeline_dev": (_I32, [_VP, _VP, _VP, _U32, _U32, _U32, _VP]),
+    "rsm_diag_alltoall_emulated": (_I32, [_VP, _VP, ctypes.c_int, _U32, _U32]),
 }
 # (A/B runs may point the DIAGNOSTIC library at a variant build; the product library
 # path is fixed)

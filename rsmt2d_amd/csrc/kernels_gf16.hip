@@ -925,7 +925,9 @@ __device__ __forceinline__ void xch_part(uint32_t (&v)[E], uint32_t (*xch)[XL], 
 // enc16h3_kernel, three workgroups per CU at 80 registers)
 // PIPE (production since round 6; PIPE = false is diagnostic form 22): twiddle tables read
 // one block ahead (grp_xform_pipe / res_xform_pipe) instead of just in time
-template <bool JIT, bool PF, int XL, bool PIPE = false>
+// SH (round 6): 0 plain, 1 / 2 the multi-GPU all-to-all's row pass with side output /
+// column pass with blocked inputs (CodewordSet::side / blk)
+template <bool JIT, bool PF, int XL, bool PIPE = false, int SH = 0>
 __device__ __forceinline__ void enc16h_body(const Enc16& p) {
     constexpr int M = 256, E = 16, G = 16, R = 16, THREADS = 512;
     constexpr int GT = G * (E - 1) * kTabW;
@@ -952,17 +954,48 @@ __device__ __forceinline__ void enc16h_body(const Enc16& p) {
         const uint32_t off = (chunk * 4u + (l32 >> 3)) * 64u + (l32 & 7u) * 4u;
         return off < S ? off + hoff : kOob16;
     };
-    auto load_task = [&](uint32_t task, uint32_t (&l)[E], uint32_t (&h)[E]) {
-        const uint32_t lo = lane_off(task);
-        const auto in = rsrc(p.cs.base + cw_rel(p.cs, task / p.chunks));
+    // all-to-all, SH = 1 (row pass): the cells of this wave -- data c = e, parity
+    // c = k + e -- also go to the send block of the GPU owning their column block
+    // (CodewordSet::side; a wave's 2E cells lie in one block: shard_fused_ok)
+    auto side_store = [&](uint32_t qq, uint32_t lo, uint32_t lm, const uint32_t (&l)[E], const uint32_t (&h)[E],
+                          uint32_t cbase) {
+        const uint32_t c0 = cbase + 2u * E * w;  // the wave's first cell
+        const uint32_t owner = c0 / p.cs.side_cols;
+        if (owner == p.cs.side_self) return;  // (wave-uniform) its own block stays in the square
+        const auto sr = rsrc(p.cs.side + (uint64_t)owner * p.cs.side_blk + (uint64_t)qq * p.cs.side_cols * S);
+        const uint32_t vs = lo == kOob16 ? kOob16 : lo - hoff + hh * (uint32_t)E * S;
+        const uint32_t cb = (c0 - owner * p.cs.side_cols) * S;
         sfor<E>([&](auto I) {
             constexpr int i = decltype(I)::value;
-            const uint32_t v = (uint32_t)i < lim ? lo : kOob16;
+            const uint32_t v = (uint32_t)i < lm ? vs : kOob16;
+            const uint32_t so = 2u * E * w + i < k ? cb + (uint32_t)i * S : 0u;
+            st(sr, l[i], v, so);
+            st(sr, h[i], v + 32u, so);
+        });
+    };
+    auto load_task = [&](uint32_t task, uint32_t (&l)[E], uint32_t (&h)[E]) {
+        const uint32_t lo = lane_off(task);
+        const uint32_t qq = task / p.chunks;
+        auto in = rsrc(p.cs.base + cw_rel(p.cs, qq));
+        uint32_t vb = lo, eb = 0u, stv = es;  // symbol e at voffset vb, soffset (e - eb) * stv
+        if constexpr (SH == 2) {  // all-to-all column pass: another GPU's rows, read in place
+            const uint32_t hb = (2u * E * w) / p.cs.blk_rows;  // (wave-uniform) row block
+            if (hb != p.cs.blk_self) {
+                in = rsrc(p.cs.blk + (uint64_t)hb * p.cs.blk_size + (uint64_t)qq * S);
+                vb = lo == kOob16 ? kOob16 : lo - hoff + hh * (uint32_t)E * p.cs.blk_pitch;
+                eb = hb * p.cs.blk_rows;
+                stv = p.cs.blk_pitch;
+            }
+        }
+        sfor<E>([&](auto I) {
+            constexpr int i = decltype(I)::value;
+            const uint32_t v = (uint32_t)i < lim ? vb : kOob16;
             // (0 for padding: an offset past the half would wrap kOob16 + so)
-            const uint32_t so = 2u * E * w + i < k ? (2u * E * w + i) * es : 0u;
+            const uint32_t so = 2u * E * w + i < k ? (2u * E * w + i - eb) * stv : 0u;
             l[i] = ld(in, v, so);
             h[i] = ld(in, v + 32u, so);
         });
+        if constexpr (SH == 1) side_store(qq, lo, lim, l, h, 0u);
     };
     uint32_t nl[E], nh[E];
     if constexpr (PF)
@@ -1008,12 +1041,13 @@ __device__ __forceinline__ void enc16h_body(const Enc16& p) {
             st(out, l[i], v, so);
             st(out, h[i], v + 32u, so);
         });
+        if constexpr (SH == 1) side_store(q, slo, slim, l, h, k);  // parity cells c = k + e
     }
 }
 
-template <bool JIT, bool PF = false, bool PIPE = false>
+template <bool JIT, bool PF = false, bool PIPE = false, int SH = 0>
 __global__ __launch_bounds__(512, 4) void enc16h_kernel(Enc16 p) {
-    enc16h_body<JIT, PF, 32, PIPE>(p);
+    enc16h_body<JIT, PF, 32, PIPE, SH>(p);
 }
 // three workgroups per CU: 6 waves per SIMD (80 registers), 49 KiB of LDS each
 __global__ __launch_bounds__(512, 6) void enc16h3_kernel(Enc16 p) {
@@ -1042,7 +1076,7 @@ __device__ __forceinline__ uint32_t swapped_elem(uint32_t w, int r, uint32_t hh)
 // PF: the next task's points are loaded while the current one transforms (32 more registers)
 // PIPE (production since round 6; PIPE = false is diagnostic form 22): twiddle tables
 // read one block ahead
-template <bool JIT, bool PF = false, bool PIPE = false>
+template <bool JIT, bool PF = false, bool PIPE = false, int SH = 0>
 __global__ __launch_bounds__(1024, 4) void enc16h512_kernel(Enc16 p) {
     constexpr int M = 512, E = 16, G = 32, R = 16, THREADS = 1024;
     constexpr int GT = G * (E - 1) * kTabW, WT = 16 * kTabW, RT = 2 * (R - 1) * kTabW;
@@ -1081,17 +1115,48 @@ __global__ __launch_bounds__(1024, 4) void enc16h512_kernel(Enc16 p) {
         const uint32_t off = (chunk * 4u + (l32 >> 3)) * 64u + (l32 & 7u) * 4u;
         return off < S ? off + hoff : kOob16;
     };
-    auto load_task = [&](uint32_t task, uint32_t (&l)[E], uint32_t (&h)[E]) {
-        const uint32_t lo = lane_off(task);
-        const auto in = rsrc(p.cs.base + cw_rel(p.cs, task / p.chunks));
+    // all-to-all, SH = 1 (row pass): the cells of this wave -- data c = e, parity
+    // c = k + e -- also go to the send block of the GPU owning their column block
+    // (CodewordSet::side; a wave's 2E cells lie in one block: shard_fused_ok)
+    auto side_store = [&](uint32_t qq, uint32_t lo, uint32_t lm, const uint32_t (&l)[E], const uint32_t (&h)[E],
+                          uint32_t cbase) {
+        const uint32_t c0 = cbase + 2u * E * w;  // the wave's first cell
+        const uint32_t owner = c0 / p.cs.side_cols;
+        if (owner == p.cs.side_self) return;  // (wave-uniform) its own block stays in the square
+        const auto sr = rsrc(p.cs.side + (uint64_t)owner * p.cs.side_blk + (uint64_t)qq * p.cs.side_cols * S);
+        const uint32_t vs = lo == kOob16 ? kOob16 : lo - hoff + hh * (uint32_t)E * S;
+        const uint32_t cb = (c0 - owner * p.cs.side_cols) * S;
         sfor<E>([&](auto I) {
             constexpr int i = decltype(I)::value;
-            const uint32_t v = (uint32_t)i < lim ? lo : kOob16;
+            const uint32_t v = (uint32_t)i < lm ? vs : kOob16;
+            const uint32_t so = 2u * E * w + i < k ? cb + (uint32_t)i * S : 0u;
+            st(sr, l[i], v, so);
+            st(sr, h[i], v + 32u, so);
+        });
+    };
+    auto load_task = [&](uint32_t task, uint32_t (&l)[E], uint32_t (&h)[E]) {
+        const uint32_t lo = lane_off(task);
+        const uint32_t qq = task / p.chunks;
+        auto in = rsrc(p.cs.base + cw_rel(p.cs, qq));
+        uint32_t vb = lo, eb = 0u, stv = es;  // symbol e at voffset vb, soffset (e - eb) * stv
+        if constexpr (SH == 2) {  // all-to-all column pass: another GPU's rows, read in place
+            const uint32_t hb = (2u * E * w) / p.cs.blk_rows;  // (wave-uniform) row block
+            if (hb != p.cs.blk_self) {
+                in = rsrc(p.cs.blk + (uint64_t)hb * p.cs.blk_size + (uint64_t)qq * S);
+                vb = lo == kOob16 ? kOob16 : lo - hoff + hh * (uint32_t)E * p.cs.blk_pitch;
+                eb = hb * p.cs.blk_rows;
+                stv = p.cs.blk_pitch;
+            }
+        }
+        sfor<E>([&](auto I) {
+            constexpr int i = decltype(I)::value;
+            const uint32_t v = (uint32_t)i < lim ? vb : kOob16;
             // (0 for padding: an offset past the half would wrap kOob16 + so)
-            const uint32_t so = 2u * E * w + i < k ? (2u * E * w + i) * es : 0u;
+            const uint32_t so = 2u * E * w + i < k ? (2u * E * w + i - eb) * stv : 0u;
             l[i] = ld(in, v, so);
             h[i] = ld(in, v + 32u, so);
         });
+        if constexpr (SH == 1) side_store(qq, lo, lim, l, h, 0u);
     };
     uint32_t nl[E], nh[E];
     if constexpr (PF)
@@ -1189,6 +1254,7 @@ __global__ __launch_bounds__(1024, 4) void enc16h512_kernel(Enc16 p) {
             st(out, l[i], v, so);
             st(out, h[i], v + 32u, so);
         });
+        if constexpr (SH == 1) side_store(q, slo, slim, l, h, k);  // parity cells c = k + e
     }
 }
 
@@ -2224,6 +2290,22 @@ hipError_t run_encode(const CodewordSet& cs, const Gf16Dev& g, hipStream_t st) {
     // one workgroup per task
     const uint32_t pgrid = tasks > g.cus ? g.cus : (uint32_t)tasks;  // persistent forms
     const uint32_t grid = M == 256 ? pgrid : (uint32_t)tasks;
+    if (cs.side || cs.blk) {  // multi-GPU all-to-all hooks: the production form with SH = 1 / 2
+        Enc16 ph = p;
+        ph.chunks = (cs.S + 255) / 256;
+        const uint64_t th = (uint64_t)cs.count * ph.chunks;
+        if (th >= (1ull << 31)) return hipErrorInvalidValue;
+        const uint32_t per_cu = M == 256 ? 2u : 1u;  // workgroups per CU of the half-wave forms
+        const uint32_t gh = th > (uint64_t)per_cu * g.cus ? per_cu * g.cus : (uint32_t)th;
+        if constexpr (M == 512) {
+            if (cs.side) hipLaunchKernelGGL((enc16h512_kernel<true, false, true, 1>), dim3(gh), dim3(1024), 0, st, ph);
+            else hipLaunchKernelGGL((enc16h512_kernel<true, false, true, 2>), dim3(gh), dim3(1024), 0, st, ph);
+        } else {
+            if (cs.side) hipLaunchKernelGGL((enc16h_kernel<true, false, true, 1>), dim3(gh), dim3(512), 0, st, ph);
+            else hipLaunchKernelGGL((enc16h_kernel<true, false, true, 2>), dim3(gh), dim3(512), 0, st, ph);
+        }
+        return hipGetLastError();
+    }
     if constexpr (M == 512) {
         if (enc16_e64()) {
             hipLaunchKernelGGL((enc16_kernel<512, 64>), dim3(grid), dim3(512), 0, st, p);

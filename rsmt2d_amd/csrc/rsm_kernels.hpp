@@ -36,6 +36,22 @@ struct CodewordSet {
                       // context's CU count or its per-pass cap (rsm_ctx_set_pass_grid)
     uint32_t wide;    // non-zero: symbols addressed with 64-bit per-symbol bases (the
                       // wide forms; the host sets it when narrow_fits() fails)
+    // Multi-GPU all-to-all (rsm_multi.cpp, round 6): honoured only by the single-pass
+    // GF(2^16) encoders (shard_fused_ok(); the host never sets them otherwise).
+    //   side (row pass): every cell c of codeword q -- data c = e, parity c = k + e --
+    //     whose column block c / side_cols is not side_self is ALSO stored at
+    //     side + (c / side_cols) * side_blk + q * side_cols * S + (c % side_cols) * S:
+    //     the per-peer send blocks, packed by the encoder instead of a copy pass;
+    //   blk (column pass): data symbol e of codeword (column) q whose row block
+    //     h = e / blk_rows is not blk_self is read from
+    //     blk + h * blk_size + (e % blk_rows) * blk_pitch + q * S -- the received blocks
+    //     in place, instead of an unpack pass.
+    uint8_t* side;
+    uint64_t side_blk;
+    uint32_t side_cols, side_self;
+    const uint8_t* blk;
+    uint64_t blk_size;
+    uint32_t blk_rows, blk_self, blk_pitch;
 };
 
 // The single-pass kernels address a codeword's symbols with 32-bit buffer offsets

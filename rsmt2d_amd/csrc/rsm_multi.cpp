@@ -39,6 +39,64 @@ int nccl_fail(ncclResult_t r, const char* what) {
     return fail(RSM_EDEVICE, "%s: %s", what, ncclGetErrorString(r));
 }
 
+// The all-to-all without copies (round 6): the row pass itself stores the cells of the
+// column blocks other GPUs own into the per-peer send blocks (CodewordSet::side), and the
+// column pass reads the received blocks in place (CodewordSet::blk) -- no pack and no
+// unpack pass.  The hooks exist in the single-pass GF(2^16) encoders (k = 129..512) and
+// need every wave's 32 cells (two lane halves of 16 elements) in one block: the row and
+// column block sizes and k multiples of 32, and the narrow (32-bit offset) addressing.
+// Other shapes (GF(2^8), k > 512, small blocks) keep the copy passes.
+bool shard_fused_ok(const rsm_ctx* ctx, uint32_t k, uint32_t S, int G) {
+    const uint32_t W = 2u * k, rk = k / (uint32_t)G, ck = W / (uint32_t)G;
+    return field_bits(k) == 16 && ceil_pow2(k) <= 512 && k % 32u == 0 && rk % 32u == 0 && ck % 32u == 0 &&
+           narrow_ok(ctx, k, (uint64_t)W * S, S) && narrow_ok(ctx, k, S, S);
+}
+
+// row pass of rows [row0, row0 + nrows) with the side output into `snd` (block h at
+// snd + h * blk: the GPU's rows x GPU h's ck columns, row pitch ck * S)
+int rows_with_side(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, uint32_t row0, uint32_t nrows, uint8_t* snd,
+                   uint64_t blk, uint32_t ck, uint32_t self) {
+    const uint64_t W = 2ull * k;
+    CodewordSet cs{};
+    cs.base = d_eds + row0 * W * S;
+    cs.cw_stride = W * S;
+    cs.elem_stride = S;
+    cs.out_offset = (uint64_t)k * S;
+    cs.per_square = nrows;
+    cs.count = nrows;
+    cs.k = k;
+    cs.S = S;
+    cs.pass = 0;
+    cs.side = snd;
+    cs.side_blk = blk;
+    cs.side_cols = ck;
+    cs.side_self = self;
+    return launch_encode(ctx, cs, ctx->stream);
+}
+
+// column pass of columns [col0, col0 + ncols) whose rows of other GPUs come from the
+// received blocks `rcv` (block h at rcv + h * blk: GPU h's rk rows x these columns)
+int cols_with_blocks(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, uint32_t col0, uint32_t ncols,
+                     const uint8_t* rcv, uint64_t blk, uint32_t rk, uint32_t self) {
+    const uint64_t W = 2ull * k;
+    CodewordSet cs{};
+    cs.base = d_eds + col0 * S;
+    cs.cw_stride = S;
+    cs.elem_stride = W * S;
+    cs.out_offset = (uint64_t)k * W * S;
+    cs.per_square = ncols;
+    cs.count = ncols;
+    cs.k = k;
+    cs.S = S;
+    cs.pass = 1;
+    cs.blk = rcv;
+    cs.blk_size = blk;
+    cs.blk_rows = rk;
+    cs.blk_self = self;
+    cs.blk_pitch = ncols * S;
+    return launch_encode(ctx, cs, ctx->stream);
+}
+
 // Steps 1-3 over device-resident squares d_eds[g] (each a full [2k][2k][S] buffer
 // on GPU g whose Q0 rows of shard g are valid).  Leaves on GPU g: its rows of the
 // top half and its column slice of the whole square (all-gather: the whole top
@@ -51,10 +109,28 @@ int extend_sharded(rsm_multi* m, uint8_t* const* d_eds, uint32_t k, uint32_t S, 
     const int G = m->n;
     const size_t W = 2ull * k, row = W * S;
     const uint32_t rk = k / G, ck = (uint32_t)(W / G);
-    // 1. row pass
+    const size_t blk = (size_t)rk * ck * S;  // all-to-all block: rk rows x ck columns
+    // the all-to-all without copies where the encoders have the hooks (shard_fused_ok)
+    const bool fused = G > 1 && schedule == RSM_SCHED_ALLTOALL && shard_fused_ok(m->ctx[0], k, S, G);
+    if (G > 1 && schedule == RSM_SCHED_ALLTOALL) {
+        hipError_t e;
+        for (int g = 0; g < G; ++g) {
+            if (int rc = use_device(m->ctx[g])) return rc;
+            if ((e = m->pack[0][g].ensure(blk * G)) != hipSuccess || (e = m->pack[1][g].ensure(blk * G)) != hipSuccess)
+                return hip_fail(e, "hipMalloc (all-to-all staging)");
+        }
+    }
+    // 1. row pass (fused all-to-all: each GPU's crossing column blocks straight into its
+    //    send staging)
     for (int g = 0; g < G; ++g) {
         if (int rc = use_device(m->ctx[g])) return rc;
-        if (int rc = rsm_extend_rows_dev(m->ctx[g], d_eds[g], k, S, g * rk, rk, nullptr)) return rc;
+        if (fused) {
+            if (int rc = rows_with_side(m->ctx[g], static_cast<uint8_t*>(d_eds[g]), k, S, g * rk, rk,
+                                        static_cast<uint8_t*>(m->pack[0][g].ptr), blk, ck, (uint32_t)g))
+                return rc;
+        } else if (int rc = rsm_extend_rows_dev(m->ctx[g], d_eds[g], k, S, g * rk, rk, nullptr)) {
+            return rc;
+        }
         if (rows_done) {
             if (hipError_t e = hipEventRecord(rows_done[g], m->ctx[g]->stream)) return hip_fail(e, "hipEventRecord");
         }
@@ -75,13 +151,11 @@ int extend_sharded(rsm_multi* m, uint8_t* const* d_eds, uint32_t k, uint32_t S, 
         }
         if ((r = ncclGroupEnd()) != ncclSuccess) return nccl_fail(r, "ncclGroupEnd");
     } else {
-        // block (h rows) x (g columns): rk rows x ck*S bytes, packed contiguously
-        const size_t blk = (size_t)rk * ck * S;
+        // block (h rows) x (g columns): rk rows x ck*S bytes, packed contiguously -- by the
+        // row pass itself (fused) or by a copy pass here
         hipError_t e;
-        for (int g = 0; g < G; ++g) {
+        for (int g = 0; g < G && !fused; ++g) {
             if (int rc = use_device(m->ctx[g])) return rc;
-            if ((e = m->pack[0][g].ensure(blk * G)) != hipSuccess || (e = m->pack[1][g].ensure(blk * G)) != hipSuccess)
-                return hip_fail(e, "hipMalloc (all-to-all staging)");
             uint8_t* snd = static_cast<uint8_t*>(m->pack[0][g].ptr);
             const uint8_t* mine = d_eds[g] + (size_t)g * rk * row;
             for (int h = 0; h < G; ++h) {
@@ -104,7 +178,7 @@ int extend_sharded(rsm_multi* m, uint8_t* const* d_eds, uint32_t k, uint32_t S, 
         ncclResult_t r2 = ncclGroupEnd();
         if (r != ncclSuccess) return nccl_fail(r, "ncclSend/ncclRecv");
         if (r2 != ncclSuccess) return nccl_fail(r2, "ncclGroupEnd");
-        for (int g = 0; g < G; ++g) {
+        for (int g = 0; g < G && !fused; ++g) {
             if (int rc = use_device(m->ctx[g])) return rc;
             const uint8_t* rcv = static_cast<const uint8_t*>(m->pack[1][g].ptr);
             for (int h = 0; h < G; ++h) {
@@ -116,10 +190,18 @@ int extend_sharded(rsm_multi* m, uint8_t* const* d_eds, uint32_t k, uint32_t S, 
             }
         }
     }
-    // 3. column pass of each GPU's column slice
+    // 3. column pass of each GPU's column slice (fused all-to-all: the other GPUs' rows read
+    //    in place from the receive staging; the square's top half then holds only this
+    //    GPU's rows)
     for (int g = 0; g < G; ++g) {
         if (int rc = use_device(m->ctx[g])) return rc;
-        if (int rc = rsm_extend_cols_dev(m->ctx[g], d_eds[g], k, S, g * ck, ck, nullptr)) return rc;
+        if (fused) {
+            if (int rc = cols_with_blocks(m->ctx[g], static_cast<uint8_t*>(d_eds[g]), k, S, g * ck, ck,
+                                          static_cast<const uint8_t*>(m->pack[1][g].ptr), blk, rk, (uint32_t)g))
+                return rc;
+        } else if (int rc = rsm_extend_cols_dev(m->ctx[g], d_eds[g], k, S, g * ck, ck, nullptr)) {
+            return rc;
+        }
     }
     return RSM_OK;
 }
@@ -312,5 +394,49 @@ int rsm_multi_extend_square_inplace(rsm_multi* m, uint8_t* eds, uint32_t k, uint
     const int rs = sync_all(m);
     return rc ? rc : rs;
 }
+
+#ifdef RSM_DIAG
+// Diagnostic / test hook: the copy-free all-to-all of extend_sharded with G "GPUs" on ONE
+// device (a context), so the encoders' side output and blocked inputs run on the hardware
+// without a multi-GPU node: rank g's row pass stores its crossing column blocks into its
+// send staging, device copies stand in for the RCCL send/recv, and rank g's column pass
+// reads the received blocks in place.  d_eds[g]: rank g's full square buffer (Q0 rows of
+// shard g valid).  Synchronous.
+int rsm_diag_alltoall_emulated(rsm_ctx* ctx, void* const* d_eds, int G, uint32_t k, uint32_t share_size) {
+    if (!ctx || !d_eds || G <= 1 || k == 0 || k % (uint32_t)G != 0)
+        return fail(RSM_EINVAL, "rsm_diag_alltoall_emulated: bad arguments");
+    if (int rc = validate_chunk_size(share_size)) return rc;
+    if (!shard_fused_ok(ctx, k, share_size, G)) return fail(RSM_EUNSUPPORTED, "rsm_diag_alltoall_emulated: shape");
+    if (int rc = use_device(ctx)) return rc;
+    const uint64_t S = share_size, W = 2ull * k;
+    const uint32_t rk = k / G, ck = (uint32_t)(W / G);
+    const uint64_t blk = (uint64_t)rk * ck * S;
+    void *snd = nullptr, *rcv = nullptr;
+    hipError_t e;
+    if ((e = hipMalloc(&snd, blk * G * G)) != hipSuccess) return hip_fail(e, "hipMalloc (emulated send staging)");
+    if ((e = hipMalloc(&rcv, blk * G * G)) != hipSuccess) {
+        (void)hipFree(snd);
+        return hip_fail(e, "hipMalloc (emulated receive staging)");
+    }
+    uint8_t* sb = static_cast<uint8_t*>(snd);
+    uint8_t* rb = static_cast<uint8_t*>(rcv);
+    int rc = RSM_OK;
+    for (int g = 0; g < G && rc == RSM_OK; ++g)
+        rc = rows_with_side(ctx, static_cast<uint8_t*>(d_eds[g]), k, share_size, g * rk, rk, sb + (uint64_t)g * G * blk, blk, ck,
+                            (uint32_t)g);
+    for (int g = 0; g < G && rc == RSM_OK; ++g)  // "GPU g sends its block h to GPU h"
+        for (int h = 0; h < G && rc == RSM_OK; ++h)
+            if (h != g && (e = hipMemcpyAsync(rb + ((uint64_t)h * G + g) * blk, sb + ((uint64_t)g * G + h) * blk, blk,
+                                              hipMemcpyDeviceToDevice, ctx->stream)) != hipSuccess)
+                rc = hip_fail(e, "emulated exchange");
+    for (int g = 0; g < G && rc == RSM_OK; ++g)
+        rc = cols_with_blocks(ctx, static_cast<uint8_t*>(d_eds[g]), k, share_size, g * ck, ck, rb + (uint64_t)g * G * blk,
+                              blk, rk, (uint32_t)g);
+    if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess && rc == RSM_OK) rc = hip_fail(e, "hipStreamSynchronize");
+    (void)hipFree(snd);
+    (void)hipFree(rcv);
+    return rc;
+}
+#endif
 
 }  // extern "C"

@@ -230,6 +230,9 @@ int launch_encode(rsm_ctx* ctx, const CodewordSet& cs0, hipStream_t st) {
     // then span one half of the codeword, k symbols es bytes apart (narrow_fits)
     CodewordSet cs = rebased(cs0);
     cs.wide = narrow_ok(ctx, cs.k, cs.elem_stride, cs.S) ? 0u : 1u;
+    // the all-to-all hooks (rsm_multi.cpp) exist in the single-pass GF(2^16) encoders only
+    if ((cs.side || cs.blk) && (field_bits(cs.k) != 16 || gf16_generic(cs.k) || cs.wide))
+        return fail(RSM_EUNSUPPORTED, "encode: multi-GPU side output / blocked input need the single-pass GF(2^16) form");
     hipError_t e;
     if (field_bits(cs.k) == 8) {
         if (cs.wide) {
@@ -996,6 +999,48 @@ int rsm_extend_rows_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_si
     cs.S = share_size;
     cs.pass = 0;
     return launch_encode(ctx, cs, pick(ctx, stream));
+}
+
+int rsm_extend_rows_blocks_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size, uint32_t row0,
+                               uint32_t nrows, void* d_blocks, uint32_t nblocks, void* stream) {
+    if (!ctx || !d_eds || !d_blocks || k == 0 || nblocks == 0 || (2 * k) % nblocks != 0 || row0 + nrows > 2 * k)
+        return fail(RSM_EINVAL, "rsm_extend_rows_blocks_dev: bad arguments");
+    if (int rc = validate_chunk_size(share_size)) return rc;
+    if (nrows == 0) return RSM_OK;
+    if (int rc = use_device(ctx)) return rc;
+    const uint64_t W = 2ull * k, S = share_size;
+    const uint32_t cb = (uint32_t)(W / nblocks);
+    const uint64_t blk = (uint64_t)nrows * cb * S;
+    uint8_t* rows = static_cast<uint8_t*>(d_eds) + row0 * W * S;
+    uint8_t* blocks = static_cast<uint8_t*>(d_blocks);
+    hipStream_t st = pick(ctx, stream);
+    // the single-pass GF(2^16) encoders store every cell a second time into its block (the
+    // side output; every wave's 32 cells lie in one block when k and the block width are
+    // multiples of 32): no copy pass
+    if (field_bits(k) == 16 && !gf16_generic(k) && k % 32u == 0 && cb % 32u == 0 && narrow_ok(ctx, k, S, S)) {
+        CodewordSet cs{};
+        cs.base = rows;
+        cs.cw_stride = W * S;
+        cs.elem_stride = S;
+        cs.out_offset = k * S;
+        cs.per_square = nrows;
+        cs.count = nrows;
+        cs.k = k;
+        cs.S = share_size;
+        cs.pass = 0;
+        cs.side = blocks;
+        cs.side_blk = blk;
+        cs.side_cols = cb;
+        cs.side_self = ~0u;  // no block stays behind: all of them go to the exchange
+        return launch_encode(ctx, cs, st);
+    }
+    // other shapes: the row pass, then one strided device copy per block
+    if (int rc = rsm_extend_rows_dev(ctx, d_eds, k, share_size, row0, nrows, st)) return rc;
+    for (uint32_t h = 0; h < nblocks; ++h)
+        if (hipError_t e = hipMemcpy2DAsync(blocks + h * blk, (size_t)cb * S, rows + (uint64_t)h * cb * S, W * S,
+                                            (size_t)cb * S, nrows, hipMemcpyDeviceToDevice, st))
+            return hip_fail(e, "rsm_extend_rows_blocks_dev: block copy");
+    return RSM_OK;
 }
 
 int rsm_extend_cols_dev(rsm_ctx* ctx, void* d_eds, uint32_t k, uint32_t share_size, uint32_t col0, uint32_t ncols,

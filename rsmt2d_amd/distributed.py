@@ -76,8 +76,12 @@ class TransposeShardedExtender:
       top    [k][w][S]   receives columns [g*w, (g+1)*w) of the whole top half [Q0|Q1]
       bottom [k][w][S]   the column pass writes the same columns of [Q2|Q3]
     Bytes received per rank: (G-1)/G * k*w*S  (config 5, G = 8: 28 MiB) instead of the
-    all-gather's (G-1)/G * k*2k*S (224 MiB).  The send buffer packs, for every
-    destination d, this rank's rows restricted to d's columns (one strided copy)."""
+    all-gather's (G-1)/G * k*2k*S (224 MiB).  The send buffer holds, for every
+    destination d, this rank's rows restricted to d's columns: written by the row pass
+    itself when `encode_rows` carries `writes_blocks = True` (it is then called as
+    encode_rows(rows, send); the HIP backend's rsm_extend_rows_blocks_dev), else packed
+    by one strided copy after it.  The received blocks are `top` in row order already,
+    so the column pass reads them in place: no unpack either."""
 
     def __init__(self, k: int, share_size: int, encode_rows: Callable, encode_batch: Callable,
                  after_local: Optional[Callable] = None, before_local: Optional[Callable] = None, *,
@@ -91,15 +95,23 @@ class TransposeShardedExtender:
         self._enc_rows, self._enc_batch = encode_rows, encode_batch
         self._after_local = after_local or (lambda: None)
         self._before_local = before_local or (lambda: None)
+        self._send = None
 
     def extend(self, rows: torch.Tensor, top: torch.Tensor, bottom: torch.Tensor) -> None:
         k, S, G = self.k, self.S, self.world
         n, w = k // G, 2 * k // G
         assert rows.shape == (n, 2 * k, S) and top.shape == (k, w, S) and bottom.shape == (k, w, S)
         assert rows.is_contiguous() and top.is_contiguous() and bottom.is_contiguous()
-        self._enc_rows(rows)                                     # Q0 rows -> Q1 rows (in place)
-        self._after_local()
-        send = rows.view(n, G, w, S).transpose(0, 1).contiguous()  # [G][n][w][S]: block d -> rank d
+        if getattr(self._enc_rows, "writes_blocks", False):
+            send = self._send
+            if send is None or send.shape != (G, n, w, S) or send.device != rows.device:
+                send = self._send = torch.empty((G, n, w, S), dtype=torch.uint8, device=rows.device)
+            self._enc_rows(rows, send)                           # Q0 -> Q1 rows, and their blocks
+            self._after_local()
+        else:
+            self._enc_rows(rows)                                 # Q0 rows -> Q1 rows (in place)
+            self._after_local()
+            send = rows.view(n, G, w, S).transpose(0, 1).contiguous()  # [G][n][w][S]: block d -> rank d
         dist.all_to_all_single(top.view(-1), send.view(-1), group=self.group)
         self._before_local()
         self._enc_batch(top, bottom)                             # my w columns: [Q0|Q1] -> [Q2|Q3]
@@ -137,9 +149,12 @@ def hip_transpose_backend(device: int = 0):
     L = library()
     ctx = device_context(device)
 
-    def rows(r):
+    def rows(r, send):
         n, W, S = r.shape
-        _check(L.rsm_extend_rows_dev(ctx, r.data_ptr(), W // 2, S, 0, n, None))
+        assert send.is_contiguous() and send.numel() == r.numel()
+        _check(L.rsm_extend_rows_blocks_dev(ctx, r.data_ptr(), W // 2, S, 0, n, send.data_ptr(), send.shape[0], None))
+
+    rows.writes_blocks = True
 
     def batch(top, bottom):
         k, w, S = top.shape

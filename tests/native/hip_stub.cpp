@@ -110,9 +110,22 @@ static hipError_t oracle_codewords(const CodewordSet& cs) {
         uint8_t* out = cs.out_base ? cs.out_base : cs.base;
         for (uint32_t e = 0; e < cs.k; ++e) {
             d[e] = cs.base + rel + (uint64_t)e * cs.elem_stride;
+            // the all-to-all column pass: another GPU's rows from the received block
+            if (cs.blk && e / cs.blk_rows != cs.blk_self)
+                d[e] = cs.blk + (uint64_t)(e / cs.blk_rows) * cs.blk_size + (uint64_t)(e % cs.blk_rows) * cs.blk_pitch +
+                       (uint64_t)q * cs.S;
             p[e] = out + rel + cs.out_offset + (uint64_t)e * cs.elem_stride;
         }
         if (leo_encode(cs.k, cs.S, d.data(), p.data()) != 0) return hipErrorInvalidValue;
+        if (cs.side)  // the all-to-all row pass: cells of other GPUs' column blocks into their send blocks
+            for (uint32_t c = 0; c < 2 * cs.k; ++c) {
+                const uint32_t owner = c / cs.side_cols;
+                if (owner == cs.side_self) continue;
+                const uint8_t* src = c < cs.k ? d[c] : p[c - cs.k];
+                memcpy(cs.side + (uint64_t)owner * cs.side_blk + (uint64_t)q * cs.side_cols * cs.S +
+                           (uint64_t)(c % cs.side_cols) * cs.S,
+                       src, cs.S);
+            }
     }
     return hipSuccess;
 }

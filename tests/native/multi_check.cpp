@@ -9,7 +9,9 @@
 //   2. rsm_multi_extend_dev (per-GPU buffers holding only their Q0 rows), both
 //      schedules: on GPU g its rows of the top half, its column slice of the
 //      whole square and (all-gather) the whole top half, bit-exact -- the
-//      all-to-all pack/unpack offsets and the in-place all-gather layout;
+//      all-to-all pack/unpack offsets, the copy-free all-to-all (GF(2^16) k = 256 /
+//      512: the encoders' side output and blocked inputs, emulated by the stub's
+//      oracle launches) and the in-place all-gather layout;
 //   3. concurrency (run under ThreadSanitizer by the test): threads extending
 //      through one shared clique and through cliques of their own.
 #include <cstdint>
@@ -100,7 +102,11 @@ void check_case(int G, uint32_t k, uint32_t S, uint64_t seed) {
             const uint8_t* p = static_cast<const uint8_t*>(d[g]);
             CHECK(same_rect(p, want.data(), row, (size_t)g * rk, (size_t)(g + 1) * rk, 0, row),
                   "G=%d k=%u sched=%d gpu %d: its rows of the top half", G, k, sched, g);
-            CHECK(same_rect(p, want.data(), row, 0, W, (size_t)g * ck * S, (size_t)(g + 1) * ck * S),
+            // the bottom half of its column slice; the top half's other rows too unless the
+            // copy-free all-to-all left them in the receive staging (GF(2^16), blocks >= 32)
+            const bool fused = G > 1 && sched == RSM_SCHED_ALLTOALL && k > 128 && k <= 512 && k % 32 == 0 &&
+                               rk % 32 == 0 && ck % 32 == 0;
+            CHECK(same_rect(p, want.data(), row, fused ? k : 0, W, (size_t)g * ck * S, (size_t)(g + 1) * ck * S),
                   "G=%d k=%u sched=%d gpu %d: its column slice", G, k, sched, g);
             if (sched == RSM_SCHED_ALLGATHER)
                 CHECK(same_rect(p, want.data(), row, 0, k, 0, row), "G=%d k=%u gpu %d: all-gathered top half", G, k, g);
@@ -153,10 +159,18 @@ void hammer() {
 }
 }  // namespace
 
-int main() {
+int main(int argc, char** argv) {
+    const bool quick = argc > 1 && strcmp(argv[1], "quick") == 0;  // (the TSan run: small shapes only)
     for (int G : {2, 4, 8})
         for (uint32_t k : {8u, 64u}) check_case(G, k, 64, g_seed + G * 131 + k);
     check_case(2, 256, 64, 4242);  // GF(2^16) (2k > 256) through the same exchange
+    // the all-to-all without copies (shard_fused_ok: GF(2^16), blocks of >= 32 rows / columns):
+    // the row pass's side output and the column pass's blocked inputs
+    check_case(4, 256, 64, 4343);
+    if (!quick) {
+        check_case(8, 256, 128, 4444);
+        check_case(8, 512, 64, 4545);  // config 5's shape over 8 GPUs
+    }
     check_case(1, 8, 64, 99);      // the clique of one (what the GPU test runs)
     hammer();
     if (g_fail) {

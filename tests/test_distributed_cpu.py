@@ -101,6 +101,18 @@ def _oracle_row_block(rows):
             a[r, k + i] = np.frombuffer(p, np.uint8)
 
 
+def _oracle_row_blocks(rows, send):
+    """The writes_blocks contract (rsm_extend_rows_blocks_dev): the row pass, and the
+    extended rows split into send[h] = rows restricted to column block h."""
+    _oracle_row_block(rows)
+    G = send.shape[0]
+    n, W, S = rows.shape
+    send.copy_(rows.view(n, G, W // G, S).transpose(0, 1))
+
+
+_oracle_row_blocks.writes_blocks = True
+
+
 def _oracle_batch(top, bottom):
     import oracle
     k, w, S = top.shape
@@ -111,13 +123,13 @@ def _oracle_batch(top, bottom):
             b[i, c] = np.frombuffer(p, np.uint8)
 
 
-def _worker_transpose(rank, world, port, k, S, q):
+def _worker_transpose(rank, world, port, k, S, q, blocks=False):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=world)
         from rsmt2d_amd.distributed import TransposeShardedExtender
         ods = np.random.default_rng(11).integers(0, 256, (k, k, S), dtype=np.uint8)
-        ext = TransposeShardedExtender(k, S, _oracle_row_block, _oracle_batch)
+        ext = TransposeShardedExtender(k, S, _oracle_row_blocks if blocks else _oracle_row_block, _oracle_batch)
         r0, r1 = ext.rows
         c0, c1 = ext.cols
         rows = torch.zeros((r1 - r0, 2 * k, S), dtype=torch.uint8)
@@ -139,14 +151,15 @@ def _worker_transpose(rank, world, port, k, S, q):
         q.put(repr(e))
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_transpose_sharded_matches_reference(world):
+@pytest.mark.parametrize("world,blocks", [(2, False), (4, False), (4, True)])
+def test_transpose_sharded_matches_reference(world, blocks):
     """Option B (all-to-all of column slices): every rank ends with its exact column
-    slice of the reference EDS (top and bottom) and its extended rows."""
+    slice of the reference EDS (top and bottom) and its extended rows -- with the send
+    blocks packed after the row pass, or written by it (writes_blocks)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker_transpose, args=(r, world, port, 8, 64, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker_transpose, args=(r, world, port, 8, 64, q, blocks)) for r in range(world)]
     for p in procs:
         p.start()
     res = q.get(timeout=180)

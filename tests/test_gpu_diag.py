@@ -119,3 +119,44 @@ def test_split_one_launch_form(dl, k, S):
     for p in (src, a, b):
         dl.rsm_dev_free(ctx, p)
     dl.rsm_ctx_destroy(ctx)
+
+
+@pytest.mark.parametrize("G,k,S", [(2, 192, 64), (2, 256, 192), (4, 256, 512), (4, 384, 128), (8, 256, 64),
+                                   (8, 512, 128)])
+def test_alltoall_without_copies(dl, G, k, S):
+    """The copy-free all-to-all of rsm_multi_extend_dev (RSM_SCHED_ALLTOALL) with G ranks
+    emulated on one GPU: the row pass's side output into the send blocks and the column
+    pass's blocked input from the receive blocks leave every rank's rows of the top half
+    and the bottom half of its column slice equal to the single-GPU extension (and the
+    oracle).  Every rank's buffer holds garbage outside its own Q0 rows, so a read of
+    another rank's rows from the square instead of the received blocks shows up."""
+    W = 2 * k
+    row = W * S
+    n = W * row
+    rk, ck = k // G, W // G
+    ctx = _ctx(dl)
+    src = _buf(dl, ctx, n)
+    R._check_with(dl, dl.rsm_dev_fill_random(ctx, src, n, 7 * G + k))
+    R._check_with(dl, dl.rsm_sync(ctx))
+    ranks = []
+    for g in range(G):
+        b = _buf(dl, ctx, n)
+        R._check_with(dl, dl.rsm_dev_fill_random(ctx, b, n, 1000 + g))
+        R._check_with(dl, dl.rsm_sync(ctx))
+        R._check_with(dl, dl.rsm_memcpy(ctx, b + g * rk * row, src + g * rk * row, rk * row, 2))
+        ranks.append(b)
+    R._check_with(dl, dl.rsm_extend_squares_dev(ctx, src, k, S, 1, None))
+    arr = (ctypes.c_void_p * G)(*ranks)
+    R._check_with(dl, dl.rsm_diag_alltoall_emulated(ctx, arr, G, k, S))
+    R._check_with(dl, dl.rsm_sync(ctx))
+    want = _down(dl, ctx, src, n).reshape(W, W, S)
+    if k * S <= 192 * 64:
+        assert np.array_equal(want, oracle.extend_square(want[:k, :k].copy(), nthreads=8))
+    for g, b in enumerate(ranks):
+        got = _down(dl, ctx, b, n).reshape(W, W, S)
+        assert np.array_equal(got[g * rk:(g + 1) * rk], want[g * rk:(g + 1) * rk]), f"rank {g}: top-half rows"
+        sl = slice(g * ck, (g + 1) * ck)
+        assert np.array_equal(got[k:, sl], want[k:, sl]), f"rank {g}: bottom half of its column slice"
+    for p in [src] + ranks:
+        dl.rsm_dev_free(ctx, p)
+    dl.rsm_ctx_destroy(ctx)

@@ -88,7 +88,7 @@ torch.cuda.set_device(0)
 dist.init_process_group("nccl")
 from rsmt2d_amd.distributed import TransposeShardedExtender, hip_transpose_backend
 import oracle
-k, S = 128, 512
+k, S = {k}, 512
 ods = np.random.default_rng(4).integers(0, 256, (k, k, S), dtype=np.uint8)
 rows = torch.zeros((k, 2 * k, S), dtype=torch.uint8, device="cuda")
 rows[:, :k] = torch.from_numpy(ods).cuda()
@@ -104,8 +104,42 @@ print("TRANSPOSE_OK" if ok else "TRANSPOSE_MISMATCH")
 """
 
 
-def test_transpose_sharded_extender_rccl_world1():
+@pytest.mark.parametrize("k", [128, 256])
+def test_transpose_sharded_extender_rccl_world1(k):
+    """k = 128: row pass + block copy (GF(2^8)); k = 256: the encoder writes the send block."""
     pytest.importorskip("torch")
-    r = subprocess.run([sys.executable, "-c", SCRIPT_T.format(root=ROOT)], capture_output=True, text=True,
+    r = subprocess.run([sys.executable, "-c", SCRIPT_T.format(root=ROOT, k=k)], capture_output=True, text=True,
                        timeout=300)
     assert "TRANSPOSE_OK" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("k,S,row0,nrows,nblocks", [(256, 512, 64, 32, 8), (512, 512, 0, 64, 8), (192, 128, 48, 48, 4),
+                                                    (256, 64, 0, 256, 16), (256, 64, 0, 40, 32), (128, 512, 16, 16, 8),
+                                                    (100, 320, 10, 25, 4), (1024, 64, 128, 128, 8)])
+def test_extend_rows_blocks_dev(lib, k, S, row0, nrows, nblocks):
+    """rsm_extend_rows_blocks_dev == rsm_extend_rows_dev plus the rows cut into column
+    blocks (the all-to-all send buffer): encoder side output (GF(2^16), k <= 512, k and
+    block width multiples of 32) and the copy form (GF(2^8); 16-column blocks; k > 512).
+    The block buffer starts as garbage, so a cell the encoder fails to store shows up."""
+    W = 2 * k
+    n = W * W * S
+    cb = W // nblocks
+    a, b = R.DeviceBuffer(n), R.DeviceBuffer(n)
+    blocks = R.DeviceBuffer(nrows * W * S)
+    a.fill_random(k + nrows)
+    blocks.fill_random(5)
+    R._check(lib.rsm_sync(a.ctx))
+    R._check(lib.rsm_memcpy(a.ctx, b.ptr, a.ptr, n, 2))
+    R._check(lib.rsm_extend_rows_dev(a.ctx, a.ptr, k, S, row0, nrows, None))
+    R._check(lib.rsm_extend_rows_blocks_dev(b.ctx, b.ptr, k, S, row0, nrows, blocks.ptr, nblocks, None))
+    R._check(lib.rsm_sync(a.ctx))
+    want = a.download().reshape(W, W, S)
+    assert (b.download().reshape(W, W, S) == want).all()
+    got = blocks.download().reshape(nblocks, nrows, cb, S)
+    mine = want[row0:row0 + nrows]
+    for h in range(nblocks):
+        assert (got[h] == mine[:, h * cb:(h + 1) * cb]).all(), h
+    if k * S <= 256 * 64:  # the rows against the oracle (each row depends on its own Q0 cells only)
+        assert (oracle.extend_square(want[:k, :k].copy(), nthreads=8)[row0:row0 + nrows] == mine).all()
+    for x in (a, b, blocks):
+        x.free()

@@ -58,7 +58,7 @@ def test_multi_gpu_exchange_bit_exact(tmp):
 
 def test_multi_gpu_exchange_under_tsan(tmp):
     exe = _build(tmp, san=True)
-    r = subprocess.run([exe], capture_output=True, timeout=900,
+    r = subprocess.run([exe, "quick"], capture_output=True, timeout=900,
                        env=dict(os.environ, TSAN_OPTIONS="halt_on_error=1 exitcode=66 second_deadlock_stack=1"))
     err = r.stderr.decode(errors="replace")
     assert r.returncode == 0, err[-6000:]
