@@ -30,7 +30,7 @@ int rsm_diag_set_trace(void* d_trace);
  * workgroup of every following GF(2^8) decode launch; NULL = off. */
 int rsm_diag_set_dec_trace(void* d_trace);
 /* Waves per (codeword, 256-B chunk) of the two launches of the latency-form extension
- * (2, 4 or 8 each; production 8 / 8). */
+ * (2, 4, 8 or 16 each; 0 = the production choice: 16 for one square, 8 for batches). */
 int rsm_diag_set_split_waves(int first, int second);
 /* One square in the latency form: 1 = one launch with a device-side wait (A/B only:
  * slower), 0 = two launches (production). */

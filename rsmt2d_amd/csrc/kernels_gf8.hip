@@ -986,9 +986,9 @@ constexpr unsigned log_of_sum8(unsigned L1, unsigned L2) {
 }
 template <int NW, int PW, bool FFT>
 __device__ __forceinline__ void enc_split_high(uint32_t (&v)[PW]) {
-    static_for<6>([&](auto LG) {  // d = PW .. 32: the top layer d = 64 is enc_split_mid
+    static_for<6>([&](auto LG) {  // d = max(PW, NW) .. 32: the top layer d = 64 is enc_split_mid
         constexpr int d = FFT ? (32 >> decltype(LG)::value) : (1 << decltype(LG)::value);
-        if constexpr (d >= PW) {
+        if constexpr (d >= PW && d >= NW) {
             constexpr int sd = d / NW;
             static_for<PW>([&](auto H) {
                 constexpr int h = decltype(H)::value;
@@ -1153,11 +1153,198 @@ __global__ __launch_bounds__(64 * NW) void encode_gf8_split_kernel(SplitEncPlan 
         }
     }
 }
-// waves per (codeword, chunk): production 8 for both launches (single square 21.1 us
-// against 25.3 at 4 / 4, profiles/r03_single.jsonl); diagnostic builds take
-// rsm_diag_set_split_waves (A/B of 2 / 4 / 8 per launch)
+// ---------------------------------------------------------------------------
+// 16-wave latency form (round 6, diagnostic A/B: rsm_diag_set_split_waves 16): PW = 8
+// points per wave, so each wave's chain of butterflies is half as long and a launch
+// has twice the waves to hide its latencies.  Three register bits cannot hold the
+// layer bits 3..6 in one window, so there are three layouts:
+//   S: wave w, register j: e = 8w + j                         IFFT d = 1, 2, 4; FFT 4, 2, 1
+//   M: wave w, register r: e = (w & 7) + 64 (w >> 3) + 8 m(r)  IFFT d = 8; FFT d = 8
+//      m(r) = e bits 3..5 = r bits (1, 0, 2): the two d = 8 butterflies of a register
+//      quad have adjacent y registers, so they share their selector shifts
+//   L: wave w, register h: e = w + 16 h                       IFFT d = 16, 32, the merged
+//                                                             d = 64 pair, FFT 32, 16
+// Four LDS exchanges through two alternating [128][64] buffers: one barrier each (a
+// buffer is rewritten only after the barrier of the exchange in between, which every
+// wave reaches after its reads of that buffer).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ constexpr uint32_t split16_m(int r) {
+    return 8u * (uint32_t)(((r >> 1) & 1) | ((r & 1) << 1) | (r & 4));
+}
+// d = 8 in M: quads (R, R+1 | R+2, R+3), x = e bit 3 clear; U = w >> 3 (e bit 6)
+template <int U, bool FFT>
+__device__ __forceinline__ void split16_layer8(uint32_t (&v)[8]) {
+    static_for<2>([&](auto B2) {
+        constexpr int R = 4 * decltype(B2)::value;
+        constexpr int blk = 64 * U + 32 * decltype(B2)::value;  // block start for e bit 4 = 0; + 16 for bit 4 = 1
+        constexpr unsigned L0 = kGf8.skew[(FFT ? -1 : 127) + blk + 8];
+        constexpr unsigned L1 = kGf8.skew[(FFT ? -1 : 127) + blk + 16 + 8];
+        if constexpr (!FFT) {
+            v[R + 2] ^= v[R];
+            v[R + 3] ^= v[R + 1];
+        }
+        if constexpr (L0 != 255u && L1 != 255u) {
+            gf8_muladd2_ct<L0, L1>(v[R], v[R + 1], v[R + 2], v[R + 3]);
+        } else {
+            if constexpr (L0 != 255u) gf8_muladd_ct<L0>(v[R], v[R + 2]);
+            if constexpr (L1 != 255u) gf8_muladd_ct<L1>(v[R + 1], v[R + 3]);
+        }
+        if constexpr (FFT) {
+            v[R + 2] ^= v[R];
+            v[R + 3] ^= v[R + 1];
+        }
+    });
+}
+
+// S-layout twiddles of the 16-wave form as per-wave runtime tables (round 6, A/B): one
+// code path for all 16 waves instead of 16 compile-time variants (~16x the S-layout
+// code), to test whether the short launches wait on instruction-cache misses.  Wave w's tables (scalar loads, SGPR operands): [dir]
+// [d = 1: blocks 0..3 | d = 2: blocks 0..1 | d = 4], an all-zero table for SKEW = 255.
+struct Split16Tw {
+    PermTab t[2][7];
+};
+struct Split16TwAll {
+    Split16Tw w[16];
+};
+constexpr Split16TwAll make_split16_tw() {
+    Split16TwAll a{};
+    for (int w = 0; w < 16; ++w)
+        for (int dir = 0; dir < 2; ++dir)
+            for (int lg = 0; lg < 3; ++lg) {
+                const int d = 1 << lg;
+                for (int B = 0; B < 8 / (2 * d); ++B) {
+                    const int ti = lg == 0 ? B : (lg == 1 ? 4 + B : 6);
+                    const unsigned L = kGf8.skew[(dir ? 8 * w - 1 : 127 + 8 * w) + 2 * d * B + d];
+                    a.w[w].t[dir][ti] = L == 255u ? PermTab{} : make_perm_tab(L);
+                }
+            }
+    return a;
+}
+__constant__ Split16TwAll d_split16_tw = make_split16_tw();
+
+// x ^= y * t with a wave-uniform runtime table t (SGPRs) and its VGPR halves ta / tb, from
+// y and its pre-shifted selector sources (as gf8_muladd_sel)
+__device__ __forceinline__ void gf8_muladd_sel_rt(uint32_t& x, uint32_t y, uint32_t y3, uint32_t y6, const PermTab& t,
+                                                  uint32_t ta, uint32_t tb) {
+    uint32_t sa, sb, sc;
+    asm("v_and_b32 %[sa], %[m7], %[y]\n\t"
+        "v_and_b32 %[sb], %[m7], %[y3]\n\t"
+        "v_and_b32 %[sc], %[m3], %[y6]\n\t"
+        "v_perm_b32 %[sa], %[ahi], %[ta], %[sa]\n\t"
+        "v_perm_b32 %[sb], %[bhi], %[tb], %[sb]\n\t"
+        "v_perm_b32 %[sc], %[cc], %[cc], %[sc]\n\t"
+        "v_bitop3_b32 %[x], %[x], %[sa], %[sb] bitop3:0x96\n\t"
+        "v_xor_b32 %[x], %[x], %[sc]"
+        : [x] "+v"(x), [sa] "=&v"(sa), [sb] "=&v"(sb), [sc] "=&v"(sc)
+        : [y] "v"(y), [y3] "v"(y3), [y6] "v"(y6), [ta] "v"(ta), [tb] "v"(tb), [m7] "i"(0x07070707),
+          [m3] "i"(0x03030303), [ahi] "s"(t.a_hi), [bhi] "s"(t.b_hi), [cc] "s"(t.c));
+}
+// S layout, all three layers of one direction, with wave w's runtime tables
+template <bool FFT>
+__device__ __forceinline__ void split16_low_rt(uint32_t (&v)[8], const Split16Tw& tw) {
+    static_for<3>([&](auto LGi) {
+        constexpr int lg = FFT ? 2 - decltype(LGi)::value : decltype(LGi)::value;
+        constexpr int d = 1 << lg;
+        static_for<8 / (2 * d)>([&](auto B) {
+            constexpr int b = decltype(B)::value * 2 * d;
+            constexpr int ti = lg == 0 ? decltype(B)::value : (lg == 1 ? 4 + decltype(B)::value : 6);
+            const PermTab t = tw.t[FFT ? 1 : 0][ti];
+            const uint32_t ta = t.a_lo, tb = t.b_lo;
+            if constexpr (d == 1) {
+                if constexpr (!FFT) v[b + 1] ^= v[b];
+                const uint32_t y = v[b + 1];
+                gf8_muladd_sel_rt(v[b], y, y >> 3, y >> 6, t, ta, tb);
+                if constexpr (FFT) v[b + 1] ^= v[b];
+            } else {
+                static_for<d / 2>([&](auto Q) {
+                    constexpr int i = b + 2 * decltype(Q)::value;
+                    if constexpr (!FFT) {
+                        v[i + d] ^= v[i];
+                        v[i + 1 + d] ^= v[i + 1];
+                    }
+                    const Shift2 q = shift2(v[i + d], v[i + 1 + d]);
+                    gf8_muladd_sel_rt(v[i], v[i + d], q.b0, q.c0, t, ta, tb);
+                    gf8_muladd_sel_rt(v[i + 1], v[i + 1 + d], q.b1, q.c1, t, ta, tb);
+                    if constexpr (FFT) {
+                        v[i + d] ^= v[i];
+                        v[i + 1 + d] ^= v[i + 1];
+                    }
+                });
+            }
+        });
+    });
+}
+// Measured slower than the 16 compile-time variants (21.8 against 21.1 us per square, same
+// box, profiles/r06o_split16_ab.jsonl): the instruction cache was not what the short
+// launches wait on.  Diagnostic A/B builds only.
+#ifdef RSM_SPLIT16_RT
+constexpr bool kSplit16Rt = true;
+#else
+constexpr bool kSplit16Rt = false;
+#endif
+
+__global__ __launch_bounds__(1024, 8) void encode_gf8_split16_kernel(SplitEncPlan p) {
+    constexpr int NW = 16, PW = 8;
+    __shared__ uint32_t xch[2][128][64];
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t task = blockIdx.x;
+    const uint32_t kind = task < p.n0 ? 0u : 1u;
+    task -= kind == 0u ? 0u : p.n0;
+    const CodewordSet& cs = p.cs[kind];
+    const uint32_t chunks = cs.chunks;
+    const uint32_t q = task / chunks;
+    const uint32_t chunk = task - q * chunks;
+    const uint32_t off0 = chunk * 256u + lane * 4u;
+    const uint32_t off = off0 < cs.S ? off0 : kOob;
+    const uint64_t rel = cw_rel(cs, q);
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(cs.base + rel);
+    const __amdgpu_buffer_rsrc_t ro = make_rsrc(cs.out_base + rel);
+    const uint32_t k = cs.k, es = (uint32_t)cs.elem_stride, oo = (uint32_t)cs.out_offset;
+    const uint32_t mb = (w & 7u) + 64u * (w >> 3);  // M layout: e of register r = mb + split16_m(r)
+    uint32_t v[PW];
+    static_for<PW>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        const uint32_t e = PW * w + j;
+        v[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, off, e < k ? e * es : kOob, 0);
+    });
+    if constexpr (kSplit16Rt) split16_low_rt<false>(v, d_split16_tw.w[w]);  // S: IFFT d = 1, 2, 4
+    else enc_split_low<NW, PW, false>(v, w);
+    static_for<PW>([&](auto J) { xch[0][PW * w + decltype(J)::value][lane] = v[decltype(J)::value]; });
+    __syncthreads();
+    static_for<PW>([&](auto R) { v[decltype(R)::value] = xch[0][mb + split16_m(decltype(R)::value)][lane]; });
+    if (w < 8u) split16_layer8<0, false>(v);  // M: IFFT d = 8
+    else split16_layer8<1, false>(v);
+    static_for<PW>([&](auto R) { xch[1][mb + split16_m(decltype(R)::value)][lane] = v[decltype(R)::value]; });
+    __syncthreads();
+    static_for<PW>([&](auto H) { v[decltype(H)::value] = xch[1][w + NW * decltype(H)::value][lane]; });
+    enc_split_high<NW, PW, false>(v);  // L: IFFT d = 16, 32; merged d = 64; FFT 32, 16
+    enc_split_mid<NW, PW>(v);
+    enc_split_high<NW, PW, true>(v);
+    static_for<PW>([&](auto H) { xch[0][w + NW * decltype(H)::value][lane] = v[decltype(H)::value]; });
+    __syncthreads();
+    static_for<PW>([&](auto R) { v[decltype(R)::value] = xch[0][mb + split16_m(decltype(R)::value)][lane]; });
+    if (w < 8u) split16_layer8<0, true>(v);  // M: FFT d = 8
+    else split16_layer8<1, true>(v);
+    static_for<PW>([&](auto R) { xch[1][mb + split16_m(decltype(R)::value)][lane] = v[decltype(R)::value]; });
+    __syncthreads();
+    static_for<PW>([&](auto J) { v[decltype(J)::value] = xch[1][PW * w + decltype(J)::value][lane]; });
+    if constexpr (kSplit16Rt) split16_low_rt<true>(v, d_split16_tw.w[w]);  // S: FFT d = 4, 2, 1
+    else enc_split_low<NW, PW, true>(v, w);
+    static_for<PW>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        const uint32_t e = PW * w + j;
+        __builtin_amdgcn_raw_buffer_store_b32(v[j], ro, off, e < k ? oo + e * es : kOob, 0);
+    });
+}
+
+// waves per (codeword, chunk): chosen by the caller -- 16 (encode_gf8_split16_kernel) for
+// one square and the per-codeword codec, 8 for batches (8 against 4: single square 21.1
+// against 25.3 us, profiles/r03_single.jsonl; 16 against 8: DESIGN.md §4 latency form,
+// round 6); diagnostic builds take rsm_diag_set_split_waves (A/B of 2 / 4 / 8 / 16 per
+// launch; 0 = the caller's choice)
 #ifdef RSM_DIAG
-static std::atomic<int> g_split_nw[2] = {8, 8};
+static std::atomic<int> g_split_nw[2] = {0, 0};
 static std::atomic<bool> g_split_fused{false};
 void set_split_diag_waves(int first, int second) {
     g_split_nw[0].store(first);
@@ -1176,16 +1363,21 @@ static hipError_t launch_split(const SplitEncPlan& p, uint32_t tasks, int nw, hi
     switch (nw) {
         case 2: hipLaunchKernelGGL(encode_gf8_split_kernel<2>, dim3(tasks), dim3(128), 0, st, p); break;
         case 8: hipLaunchKernelGGL(encode_gf8_split_kernel<8>, dim3(tasks), dim3(512), 0, st, p); break;
+        case 16:  // (no fused form: the 16-wave kernel takes up to two sets, no hand-off)
+            if (p.fused) hipLaunchKernelGGL(encode_gf8_split_kernel<8>, dim3(tasks), dim3(512), 0, st, p);
+            else hipLaunchKernelGGL(encode_gf8_split16_kernel, dim3(tasks), dim3(1024), 0, st, p);
+            break;
         default: hipLaunchKernelGGL(encode_gf8_split_kernel<4>, dim3(tasks), dim3(256), 0, st, p); break;
     }
     return hipGetLastError();
 }
-static int split_waves(int launch) {
+static int split_waves(int launch, int nw) {
 #ifdef RSM_DIAG
-    return g_split_nw[launch].load();
+    const int n = g_split_nw[launch].load();
+    return n ? n : nw;
 #else
     (void)launch;
-    return 8;
+    return nw;
 #endif
 }
 static void split_set(SplitEncPlan& p, int i, const CodewordSet& c, uint32_t& n) {
@@ -1194,14 +1386,14 @@ static void split_set(SplitEncPlan& p, int i, const CodewordSet& c, uint32_t& n)
     n = p.cs[i].count * p.cs[i].chunks;
 }
 
-hipError_t launch_encode_gf8_split(const CodewordSet& a, const CodewordSet* b, hipStream_t st) {
+hipError_t launch_encode_gf8_split(const CodewordSet& a, const CodewordSet* b, hipStream_t st, int nw) {
     if (ceil_pow2(a.k) != 128 || (b && ceil_pow2(b->k) != 128)) return hipErrorInvalidValue;
     SplitEncPlan p{};
     split_set(p, 0, a, p.n0);
     if (b) split_set(p, 1, *b, p.n1);
     const uint64_t tasks = (uint64_t)p.n0 + p.n1;
     if (tasks == 0) return hipSuccess;
-    return launch_split(p, (uint32_t)tasks, split_waves(b ? 0 : 1), st);
+    return launch_split(p, (uint32_t)tasks, split_waves(b ? 0 : 1, nw), st);
 }
 
 hipError_t launch_extend_gf8_split_fused(const CodewordSet& rows, const CodewordSet& c0, const CodewordSet& c1,
@@ -1216,7 +1408,7 @@ hipError_t launch_extend_gf8_split_fused(const CodewordSet& rows, const Codeword
     p.fused = 1;
     const uint64_t tasks = (uint64_t)p.n0 + p.n1 + p.n2;
     if (tasks == 0 || p.n2 == 0) return hipErrorInvalidValue;
-    return launch_split(p, (uint32_t)tasks, split_waves(0), st);
+    return launch_split(p, (uint32_t)tasks, split_waves(0, 8), st);
 }
 
 // ---------------------------------------------------------------------------

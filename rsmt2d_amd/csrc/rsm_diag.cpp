@@ -58,7 +58,7 @@ int rsm_diag_set_trace(void* d_trace) {
 }
 
 int rsm_diag_set_split_waves(int first, int second) {
-    auto ok = [](int n) { return n == 2 || n == 4 || n == 8; };
+    auto ok = [](int n) { return n == 0 || n == 2 || n == 4 || n == 8 || n == 16; };  // 0: production choice
     if (!ok(first) || !ok(second)) return RSM_EINVAL;
     set_split_diag_waves(first, second);
     return RSM_OK;

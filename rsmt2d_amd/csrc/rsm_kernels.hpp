@@ -137,7 +137,9 @@ hipError_t launch_decode_gf8(const DecodeSet& ds, hipStream_t st);
 // (kernels_gf8.hip encode_gf8_split_kernel): NW waves per (codeword, 256-B chunk) on
 // byte tables, every CU busy.  Launches the codewords of `a` and, if b != nullptr,
 // those of `b` in the same grid.
-hipError_t launch_encode_gf8_split(const CodewordSet& a, const CodewordSet* b, hipStream_t st);
+// nw: waves per (codeword, 256-byte chunk), 8 or 16 (kSplitWavesOne)
+hipError_t launch_encode_gf8_split(const CodewordSet& a, const CodewordSet* b, hipStream_t st, int nw);
+constexpr int kSplitWavesOne = 16;  // one square / one codeword: the 16-wave latency form
 void set_split_diag_waves(int first, int second);  // diagnostic builds only
 void set_split_diag_fused(bool on);                  // diagnostic builds only
 void set_enc16_diag_e64(int mode);                   // diagnostic builds only

@@ -463,8 +463,12 @@ int extend_squares_split(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, u
     }
     // launch 1 = rows + Q0 columns, launch 2 = Q1 columns (moving half of the Q0
     // columns into launch 2 measured 25.9 against 21.9 us per square, r03m)
-    if ((e = launch_encode_gf8_split(rows, &c0, st)) != hipSuccess) return hip_fail(e, "split extension (launch 1)");
-    if ((e = launch_encode_gf8_split(c1, nullptr, st)) != hipSuccess) return hip_fail(e, "split extension (launch 2)");
+    // waves per task: 16 for one square (shorter per-wave chains, twice the waves to hide
+    // the latencies of a launch that runs one wave of tasks), 8 for batches (issue-bound:
+    // the 16-wave form's two extra exchanges cost more than they hide)
+    const int nw = count == 1 ? kSplitWavesOne : 8;
+    if ((e = launch_encode_gf8_split(rows, &c0, st, nw)) != hipSuccess) return hip_fail(e, "split extension (launch 1)");
+    if ((e = launch_encode_gf8_split(c1, nullptr, st, nw)) != hipSuccess) return hip_fail(e, "split extension (launch 2)");
     return RSM_OK;
 }
 
@@ -760,7 +764,7 @@ int rsm_encode(rsm_ctx* ctx, const uint8_t* const* data, uint32_t k, uint32_t sh
             cs.S = share_size;
             cs.pass = 1;
             if (field_bits(k) == 8) {
-                if ((e = launch_encode_gf8_split(cs, nullptr, L.stream)) != hipSuccess)
+                if ((e = launch_encode_gf8_split(cs, nullptr, L.stream, kSplitWavesOne)) != hipSuccess)
                     return hip_fail(e, "encode kernel launch");
             } else if (int rc = launch_encode(ctx, cs, L.stream)) {
                 return rc;

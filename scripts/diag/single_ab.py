@@ -2,7 +2,7 @@
 small batches of k = 128, S = 512 squares -- the split encoder's waves per task in
 each of its two launches, and the batch size where the queue-driven launch overtakes
 it (rsm_ctx_set_split_max).  One JSON line per configuration.
-usage: python3 scripts/diag/single_ab.py
+usage: [SINGLE_AB="0,8,8 0,16,16 ..."] python3 scripts/diag/single_ab.py  (fused,waves1,waves2 triples)
 """
 import ctypes
 import json
@@ -45,7 +45,9 @@ def main():
         return round(ms.value / n * 1e3, 2)
 
     chk(D.rsm_ctx_set_split_max(ctx, 64, None))
-    for fused, a, b in ((0, 8, 8), (0, 4, 4), (1, 8, 8), (0, 8, 8)):
+    configs = [tuple(int(x) for x in c.split(",")) for c in os.environ["SINGLE_AB"].split()] \
+        if os.environ.get("SINGLE_AB") else [(0, 8, 8), (0, 4, 4), (1, 8, 8), (0, 8, 8)]
+    for fused, a, b in configs:
         chk(D.rsm_diag_set_split_fused(fused))
         chk(D.rsm_diag_set_split_waves(a, b))
         got = dev_us(1, 200)
@@ -53,7 +55,15 @@ def main():
         ok = matches_two_launch(D, ctx, sq, k)
         print(json.dumps({"fused": fused, "waves": [a, b], "count": 1, "us": got, "ok": ok}), flush=True)
     chk(D.rsm_diag_set_split_fused(0))
-    chk(D.rsm_diag_set_split_waves(8, 8))
+    if os.environ.get("SINGLE_SWEEP"):  # waves per task x batch size (latency form only)
+        for a, b in ((8, 8), (16, 16), (8, 8), (16, 16)):
+            chk(D.rsm_diag_set_split_waves(a, b))
+            for c in (1, 2, 4, 8, 12):
+                got = dev_us(c, 100 if c < 8 else 40)
+                print(json.dumps({"waves": [a, b], "count": c, "us": got, "us_per_sq": round(got / c, 2)}), flush=True)
+        chk(D.rsm_diag_set_split_waves(0, 0))
+        return
+    chk(D.rsm_diag_set_split_waves(0, 0))
     for c in (1, 2, 4, 8, 16, 24, 32):
         chk(D.rsm_ctx_set_split_max(ctx, 64, None))
         sp = dev_us(c, 30)

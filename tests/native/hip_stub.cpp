@@ -172,7 +172,7 @@ hipError_t launch_extend_gf8_split_fused(const CodewordSet&, const CodewordSet&,
                                          uint32_t*, hipStream_t) {
     return hipErrorInvalidValue;
 }
-hipError_t launch_encode_gf8_split(const CodewordSet& a, const CodewordSet* b, hipStream_t st) {
+hipError_t launch_encode_gf8_split(const CodewordSet& a, const CodewordSet* b, hipStream_t st, int) {
     if (hipError_t e = launch_encode_gf8(a, st)) return e;
     return b ? launch_encode_gf8(*b, st) : hipSuccess;
 }

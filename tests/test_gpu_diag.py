@@ -160,3 +160,26 @@ def test_alltoall_without_copies(dl, G, k, S):
     for p in [src] + ranks:
         dl.rsm_dev_free(ctx, p)
     dl.rsm_ctx_destroy(ctx)
+
+
+@pytest.mark.parametrize("k,S,count,waves", [(128, 512, 1, (16, 16)), (100, 320, 1, (16, 8)), (128, 512, 3, (8, 16)),
+                                              (65, 64, 2, (16, 16))])
+def test_split16_latency_form(dl, k, S, count, waves):
+    """The 16-wave latency form (three layouts, four exchanges; diagnostic) == the oracle."""
+    W = 2 * k
+    n = W * W * S * count
+    ctx = _ctx(dl)
+    a = _buf(dl, ctx, n)
+    R._check_with(dl, dl.rsm_dev_fill_random(ctx, a, n, 1600 + k))
+    R._check_with(dl, dl.rsm_sync(ctx))
+    try:
+        R._check_with(dl, dl.rsm_diag_set_split_waves(*waves))
+        R._check_with(dl, dl.rsm_extend_squares_dev(ctx, a, k, S, count, None))
+        R._check_with(dl, dl.rsm_sync(ctx))
+    finally:
+        R._check_with(dl, dl.rsm_diag_set_split_waves(0, 0))
+    got = _down(dl, ctx, a, n).reshape(count, W, W, S)
+    for c in range(count):
+        assert np.array_equal(got[c], oracle.extend_square(got[c, :k, :k].copy(), nthreads=8)), c
+    dl.rsm_dev_free(ctx, a)
+    dl.rsm_ctx_destroy(ctx)
