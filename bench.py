@@ -780,7 +780,7 @@ def bench_single_square(local, L, R, k=128, S=512, reps=200):
     return {"workload": f"one k={k} S={S} square, device-resident (count = 1)",
             "single_square_us": round(t_dev * 1e6, 2), "host_observed_us_p50": round(pct(lat, 0.5) * 1e6, 1),
             "frac": round(4 * k * k * S / t_dev / 1e9 / HBM_PEAK_GBS, 4),
-            "kernel": "encode_gf8_split_kernel<8> x 2 launches (latency form)",
+            "kernel": "encode_gf8_split16_kernel x 2 launches (latency form, 16 waves per task; batches: encode_gf8_split_kernel<8>)",
             "queue_form_us": round(t_queue, 2), "count_sweep_us": sweep,
             "note": "device time per launch of back-to-back launches on one stream; host_observed = "
                     "rsm_extend_squares_dev + rsm_sync round trip; queue_form = the single queue-driven "

@@ -1,7 +1,8 @@
 """A short single-square workload for counter passes (the shape one cgo
 ComputeExtendedDataSquare call sees, extendeddatasquare.go:50-77): N device-resident
 extensions of ONE k = 128, S = 512 square (rsm_extend_squares_dev with count = 1: the
-latency form, two launches of encode_gf8_split_kernel<8>).
+latency form, two launches of encode_gf8_split16_kernel; RUN_SINGLE_WAVES picks the
+form in the diagnostic library).
 usage: [RUN_SINGLE_WAVES=16,16] python3 scripts/diag/run_single.py [N]
 """
 import os

@@ -122,7 +122,7 @@ def test_split_one_launch_form(dl, k, S):
 
 
 @pytest.mark.parametrize("G,k,S", [(2, 192, 64), (2, 256, 192), (4, 256, 512), (4, 384, 128), (8, 256, 64),
-                                   (8, 512, 128)])
+                                   (8, 512, 128), (8, 512, 512), (2, 512, 256)])
 def test_alltoall_without_copies(dl, G, k, S):
     """The copy-free all-to-all of rsm_multi_extend_dev (RSM_SCHED_ALLTOALL) with G ranks
     emulated on one GPU: the row pass's side output into the send blocks and the column
