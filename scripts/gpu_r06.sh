@@ -41,7 +41,7 @@ for s in ${STEPS:-smoke tests}; do
              step gf16ab 300 python3 scripts/diag/gf16_ab.py || exit 15 ;;
     repairtrace) step repair_trace 300 rocprofv3 --kernel-trace --memory-copy-trace -d "$PWD/$OUT/rtrace" -o run --output-format csv -- python3 scripts/diag/repair_trace.py ${RT_REPS:-6} || exit 16 ;;
     repab) step repair_ab 400 python3 scripts/diag/repair_ab.py || exit 17 ;;
-    singlepmc)  # counters of the single-square latency form (encode_gf8_split_kernel<8>)
+    singlepmc)  # counters of the single-square latency form (encode_gf8_split16_kernel since r06p)
          i=0
          for C in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_ACTIVE_INST_VALU" \
                   "SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_SCA" \
