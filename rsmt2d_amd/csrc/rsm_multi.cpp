@@ -111,7 +111,8 @@ int extend_sharded(rsm_multi* m, uint8_t* const* d_eds, uint32_t k, uint32_t S, 
     const uint32_t rk = k / G, ck = (uint32_t)(W / G);
     const size_t blk = (size_t)rk * ck * S;  // all-to-all block: rk rows x ck columns
     // the all-to-all without copies where the encoders have the hooks (shard_fused_ok)
-    const bool fused = G > 1 && schedule == RSM_SCHED_ALLTOALL && shard_fused_ok(m->ctx[0], k, S, G);
+    bool fused = G > 1 && schedule == RSM_SCHED_ALLTOALL;
+    for (int g = 0; g < G && fused; ++g) fused = shard_fused_ok(m->ctx[g], k, S, G);  // (per-context limits)
     if (G > 1 && schedule == RSM_SCHED_ALLTOALL) {
         hipError_t e;
         for (int g = 0; g < G; ++g) {
