@@ -841,15 +841,15 @@ def bench_small_squares(local, L, R, S=512, ks=(4, 8, 16, 32, 64)):
 
 def gf16_square_traffic(kernel):
     """HBM bytes per square of the GF(2^16) encoder `kernel` (row + column launch) from the
-    committed counter passes (profiles/r05d_gf16_enc_pmc.json: rocprofv3 --pmc FETCH_SIZE /
+    committed counter passes (profiles/r06r_gf16_enc_pmc.json: rocprofv3 --pmc FETCH_SIZE /
     WRITE_SIZE over scripts/diag/run_gf16.py, one square per call: c4 for enc16h_kernel, c5
     for enc16h512_kernel), or None when the file lacks the kernel."""
     try:
-        rows = json.load(open(os.path.join(ROOT, "profiles", "r05d_gf16_enc_pmc.json")))["launches"]
+        rows = json.load(open(os.path.join(ROOT, "profiles", "r06r_gf16_enc_pmc.json")))["launches"]
     except (OSError, ValueError, KeyError):
         return None
     t = [r["traffic_bytes"] for r in rows if f"::{kernel}<" in r["kernel"]]
-    return {"traffic_bytes_per_square": round(sum(t)), "source": "profiles/r05d_gf16_enc_pmc.json"} if len(t) == 2 else None
+    return {"traffic_bytes_per_square": round(sum(t)), "source": "profiles/r06r_gf16_enc_pmc.json"} if len(t) == 2 else None
 
 
 def bench_c4(local, L, R, steps, B=2, k=256, S=2048):
