@@ -57,7 +57,8 @@ int rsm_diag_set_dec16_mode(uint32_t mode);
 int rsm_diag_set_dec_delay(uint32_t ticks);
 /* GF(2^8) split decoder A/B: 1 = the other error-locator form than production (every
  * wave computing the locator itself with scalar-loaded tables, or wave 0 staging the
- * per-point tables in LDS for all waves); 2 = the setup-free floor of a pre-pass design
+ * per-point tables in LDS for all waves; production takes the first for launches of at
+ * most 64 tasks, the second for larger ones); 2 = the setup-free floor of a pre-pass design
  * (no presence loads and no error locator in the kernel: a zero locator and every other
  * point present -- wrong output, timing only); 0 = production. */
 int rsm_diag_set_dec8_mode(uint32_t mode);

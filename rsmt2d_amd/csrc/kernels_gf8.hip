@@ -1535,14 +1535,23 @@ static hipError_t launch_dec(const DecodeSet& ds, hipStream_t st) {
 }
 
 // The split decoder's locator: per wave (WE) or wave 0 + LDS tables (round 4 form).
-constexpr bool kDecWaveErr = false;
+// Sweeps (hundreds of tasks, VALU-bound) share wave 0's locator: the per-wave copies
+// measured slower (33.3-34.1 against 30.5-31.2 us, profiles/r05d_dec_ab.jsonl).  A few
+// tasks (the codec's one codeword, a fraud-proof row: latency-bound, the CU otherwise
+// idle) take the per-wave form, no wave waiting on wave 0 and its barrier: codec Decode
+// p50 -1.1 us (profiles/r06s_codec_dec_ab.jsonl).
+constexpr uint64_t kDecWaveErrTasks = 64;
 #ifdef RSM_DIAG
-static std::atomic<uint32_t> g_dec8_mode{0};  // 1: the other locator form (A/B)
+static std::atomic<uint32_t> g_dec8_mode{0};  // 1: the other locator form (A/B), 2: the floor form
 void set_dec8_diag_mode(uint32_t m) { g_dec8_mode.store(m); }
-static bool dec8_wave_err() { return g_dec8_mode.load() >= 1 ? !kDecWaveErr : kDecWaveErr; }
+static bool dec8_wave_err(uint64_t tasks) {
+    const uint32_t m = g_dec8_mode.load();
+    if (m == 2) return true;  // the setup-free floor runs on the per-wave form
+    return (tasks <= kDecWaveErrTasks) != (m == 1);
+}
 #else
 void set_dec8_diag_mode(uint32_t) {}
-static bool dec8_wave_err() { return kDecWaveErr; }
+static bool dec8_wave_err(uint64_t tasks) { return tasks <= kDecWaveErrTasks; }
 #endif
 #ifdef RSM_DIAG
 static std::atomic<uint32_t*> g_dec_trace{nullptr};
@@ -1574,7 +1583,7 @@ hipError_t launch_decode_gf8(const DecodeSet& ds0, hipStream_t st) {
             hipLaunchKernelGGL(decode_gf8_split_zc_kernel<4>, dim3(grid), dim3(256), 0, st, ds);
         } else {
             constexpr int NW = kSplitWaves;
-            if (dec8_wave_err())
+            if (dec8_wave_err(tasks))
                 hipLaunchKernelGGL((decode_gf8_split_kernel<NW, true>), dim3((uint32_t)tasks), dim3(64 * NW), 0, st, ds);
             else
                 hipLaunchKernelGGL((decode_gf8_split_kernel<NW, false>), dim3((uint32_t)tasks), dim3(64 * NW), 0, st, ds);
