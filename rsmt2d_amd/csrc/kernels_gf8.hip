@@ -980,21 +980,23 @@ __global__ __launch_bounds__(64 * NW, NW / 2) void decode_gf8_split_zc_kernel(De
 // Same butterflies as encode_gf8_kernel<128> (klauspost leopard8
 // ifftDITEncoder8 / fftDIT8), so the same parity; LDS [128 points][64 lanes] dwords.
 // ---------------------------------------------------------------------------
+constexpr int ilog2_ct(int x) { return x <= 1 ? 0 : 1 + ilog2_ct(x / 2); }
 constexpr unsigned log_of_sum8(unsigned L1, unsigned L2) {
     const unsigned a = L1 == 255u ? 0u : kGf8.exp[L1], b = L2 == 255u ? 0u : kGf8.exp[L2];
     return (a ^ b) == 0u ? 255u : kGf8.log[a ^ b];
 }
-template <int NW, int PW, bool FFT>
+template <int NW, int PW, bool FFT, int M = 128>
 __device__ __forceinline__ void enc_split_high(uint32_t (&v)[PW]) {
-    static_for<6>([&](auto LG) {  // d = max(PW, NW) .. 32: the top layer d = 64 is enc_split_mid
-        constexpr int d = FFT ? (32 >> decltype(LG)::value) : (1 << decltype(LG)::value);
+    constexpr int NL = ilog2_ct(M) - 1;  // layers d = 1 .. M/4
+    static_for<NL>([&](auto LG) {  // d = max(PW, NW) .. M/4: the top layer d = M/2 is enc_split_mid
+        constexpr int d = FFT ? ((M / 4) >> decltype(LG)::value) : (1 << decltype(LG)::value);
         if constexpr (d >= PW && d >= NW) {
             constexpr int sd = d / NW;
             static_for<PW>([&](auto H) {
                 constexpr int h = decltype(H)::value;
                 if constexpr (((h / sd) & 1) == 0) {
                     constexpr int b = 2 * d * (h / (2 * sd));
-                    constexpr unsigned L = kGf8.skew[(FFT ? -1 : 127) + b + d];
+                    constexpr unsigned L = kGf8.skew[(FFT ? -1 : M - 1) + b + d];
                     if constexpr (sd >= 2 && kGf8Pair) {  // pairs h, h + 1 of one block (shift2)
                         if constexpr ((h & 1) == 0) {
                             if constexpr (FFT) fft2x2<L>(v[h], v[h + 1], v[h + sd], v[h + sd + 1]);
@@ -1013,10 +1015,10 @@ __device__ __forceinline__ void enc_split_high(uint32_t (&v)[PW]) {
 // The last IFFT layer and the first FFT layer (d = 64) join the same pairs: one
 // multiply by exp(L1) + exp(L2) instead of two (bs8.hpp mid2, by linearity):
 // y ^= x; x ^= y * (exp L1 + exp L2); y ^= x.
-template <int NW, int PW>
+template <int NW, int PW, int M = 128>
 __device__ __forceinline__ void enc_split_mid(uint32_t (&v)[PW]) {
-    constexpr int sd = 64 / NW;
-    constexpr unsigned L = log_of_sum8(kGf8.skew[127 + 64], kGf8.skew[-1 + 64]);
+    constexpr int sd = (M / 2) / NW;
+    constexpr unsigned L = log_of_sum8(kGf8.skew[M - 1 + M / 2], kGf8.skew[-1 + M / 2]);
     static_for<PW>([&](auto H) {
         constexpr int h = decltype(H)::value;
         if constexpr (kGf8Pair && sd >= 2 && ((h / sd) & 1) == 0 && (h & 1) == 0) {  // pairs h, h + 1 (shift2)
@@ -1032,13 +1034,13 @@ __device__ __forceinline__ void enc_split_mid(uint32_t (&v)[PW]) {
         }
     });
 }
-template <int NW, int PW, bool FFT>
+template <int NW, int PW, bool FFT, int M = 128>
 __device__ __forceinline__ void enc_split_low(uint32_t (&v)[PW], uint32_t w) {
     static_for<NW>([&](auto Wc) {
         constexpr int W = decltype(Wc)::value;
         if (w == (uint32_t)W) {
             if constexpr (FFT) fft_layers<PW, PW * W - 1>(v);
-            else ifft_layers<PW, 127 + PW * W>(v);
+            else ifft_layers<PW, M - 1 + PW * W>(v);
         }
     });
 }
@@ -1338,6 +1340,58 @@ __global__ __launch_bounds__(1024, 8) void encode_gf8_split16_kernel(SplitEncPla
     });
 }
 
+// ---------------------------------------------------------------------------
+// Latency form for M = 32 and 64 (17 <= k <= 64, round 6): one NW-wave workgroup per
+// (codeword, 256-byte chunk) with the layouts of encode_gf8_split_kernel (S: e = PW w + j,
+// L: e = NW h + w, the top pair merged), so one square's codewords spread over NW times
+// the waves of the byte-table kernel's one-wave-per-task form, whose single wave per
+// SIMD runs the whole transform as one dependent chain.  No fused form.
+// ---------------------------------------------------------------------------
+template <int M, int NW>
+__global__ __launch_bounds__(64 * NW) void encode_gf8_splitm_kernel(SplitEncPlan p) {
+    constexpr int PW = M / NW;
+    static_assert(PW * NW == M && PW >= NW, "split encoder shape");
+    __shared__ uint32_t xch[M][64];
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t task = blockIdx.x;
+    const uint32_t kind = task < p.n0 ? 0u : 1u;
+    task -= kind == 0u ? 0u : p.n0;
+    const CodewordSet& cs = p.cs[kind];
+    const uint32_t chunks = cs.chunks;
+    const uint32_t q = task / chunks;
+    const uint32_t chunk = task - q * chunks;
+    const uint32_t off0 = chunk * 256u + lane * 4u;
+    const uint32_t off = off0 < cs.S ? off0 : kOob;
+    const uint64_t rel = cw_rel(cs, q);
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(cs.base + rel);
+    const __amdgpu_buffer_rsrc_t ro = make_rsrc(cs.out_base + rel);
+    const uint32_t k = cs.k, es = (uint32_t)cs.elem_stride, oo = (uint32_t)cs.out_offset;
+    uint32_t v[PW];
+    static_for<PW>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        const uint32_t e = PW * w + j;
+        v[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, off, e < k ? e * es : kOob, 0);
+    });
+    enc_split_low<NW, PW, false, M>(v, w);
+    static_for<PW>([&](auto J) { xch[PW * w + decltype(J)::value][lane] = v[decltype(J)::value]; });
+    __syncthreads();
+    static_for<PW>([&](auto H) { v[decltype(H)::value] = xch[NW * decltype(H)::value + w][lane]; });
+    enc_split_high<NW, PW, false, M>(v);
+    enc_split_mid<NW, PW, M>(v);
+    enc_split_high<NW, PW, true, M>(v);
+    __syncthreads();
+    static_for<PW>([&](auto H) { xch[NW * decltype(H)::value + w][lane] = v[decltype(H)::value]; });
+    __syncthreads();
+    static_for<PW>([&](auto J) { v[decltype(J)::value] = xch[PW * w + decltype(J)::value][lane]; });
+    enc_split_low<NW, PW, true, M>(v, w);
+    static_for<PW>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        const uint32_t e = PW * w + j;
+        __builtin_amdgcn_raw_buffer_store_b32(v[j], ro, off, e < k ? oo + e * es : kOob, 0);
+    });
+}
+
 // waves per (codeword, chunk): chosen by the caller -- 16 (encode_gf8_split16_kernel) for
 // one square and the per-codeword codec, 8 for batches (8 against 4: single square 21.1
 // against 25.3 us, profiles/r03_single.jsonl; 16 against 8: DESIGN.md §4 latency form,
@@ -1387,12 +1441,21 @@ static void split_set(SplitEncPlan& p, int i, const CodewordSet& c, uint32_t& n)
 }
 
 hipError_t launch_encode_gf8_split(const CodewordSet& a, const CodewordSet* b, hipStream_t st, int nw) {
-    if (ceil_pow2(a.k) != 128 || (b && ceil_pow2(b->k) != 128)) return hipErrorInvalidValue;
+    const uint32_t M = ceil_pow2(a.k);
+    if ((M != 32 && M != 64 && M != 128) || (b && ceil_pow2(b->k) != M)) return hipErrorInvalidValue;
     SplitEncPlan p{};
     split_set(p, 0, a, p.n0);
     if (b) split_set(p, 1, *b, p.n1);
     const uint64_t tasks = (uint64_t)p.n0 + p.n1;
     if (tasks == 0) return hipSuccess;
+    if (M == 64) {  // (nw: 8 waves of 8 points; the only shape with PW >= NW and more than 4 waves)
+        hipLaunchKernelGGL((encode_gf8_splitm_kernel<64, 8>), dim3((uint32_t)tasks), dim3(512), 0, st, p);
+        return hipGetLastError();
+    }
+    if (M == 32) {  // 4 waves of 8 points
+        hipLaunchKernelGGL((encode_gf8_splitm_kernel<32, 4>), dim3((uint32_t)tasks), dim3(256), 0, st, p);
+        return hipGetLastError();
+    }
     return launch_split(p, (uint32_t)tasks, split_waves(b ? 0 : 1, nw), st);
 }
 

@@ -439,7 +439,11 @@ int extend_squares_queue(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, u
 // encoder (NW waves per codeword chunk), so each phase spreads over every CU instead
 // of the queue kernel's 64 + 32 sets of ~16 us each.
 int extend_squares_split(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, uint32_t count, hipStream_t st) {
-    if (field_bits(k) != 8 || ceil_pow2(k) != 128 || count == 0) return RSM_EUNSUPPORTED;
+    const uint32_t M = ceil_pow2(k);
+    if (field_bits(k) != 8 || count == 0) return RSM_EUNSUPPORTED;
+    // M = 32 / 64 (round 6): the split form too (encode_gf8_splitm_kernel) for up to
+    // split_max squares; larger batches take the byte-table passes
+    if (M != 128 && M != 32 && M != 64) return RSM_EUNSUPPORTED;
     const CodewordSet rows = rows_set(d_eds, k, S, count);
     CodewordSet c0 = cols_set(d_eds, k, S, count);  // columns 0 .. k-1 (Q0 -> Q2)
     c0.per_square = k;
@@ -451,7 +455,7 @@ int extend_squares_split(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, u
     // tasks -- 3 k ceil(S / 256) workgroups of 8 waves, resident at once when they fit
     // 4 per CU (otherwise the two launches below)
     const uint64_t wgs = 3ull * k * ((S + 255) / 256);
-    if (count == 1 && wgs <= 4ull * ctx->cus && split_fused_enabled()) {
+    if (M == 128 && count == 1 && wgs <= 4ull * ctx->cus && split_fused_enabled()) {
         if (int rc = check_queue_reports(ctx, st)) return rc;
         StreamScratch& ss = stream_scratch(ctx, st);
         std::lock_guard<std::mutex> lk(ss.mu);

@@ -406,3 +406,20 @@ def test_multi_gpu_inplace_pinned_world1(lib, multi, sched):
         assert np.array_equal(eds, oracle.extend_square(ods, nthreads=8))
     finally:
         R._check(lib.rsm_multi_host_free(multi, p))
+
+
+@pytest.mark.parametrize("k,S,count", [(17, 64, 1), (32, 512, 1), (33, 320, 2), (50, 512, 1), (64, 512, 1),
+                                       (64, 512, 12), (64, 128, 13), (24, 1024, 5)])
+def test_small_square_latency_form(lib, k, S, count):
+    """17 <= k <= 64: up to 12 squares per call take the split latency form
+    (encode_gf8_splitm_kernel), larger batches the byte-table passes; both == oracle."""
+    W = 2 * k
+    n = W * W * S * count
+    buf = R.DeviceBuffer(n)
+    buf.fill_random(700 + k + count)
+    R._check(lib.rsm_extend_squares_dev(buf.ctx, buf.ptr, k, S, count, None))
+    R._check(lib.rsm_sync(buf.ctx))
+    got = buf.download().reshape(count, W, W, S)
+    for c in range(count):
+        assert np.array_equal(got[c], oracle.extend_square(got[c, :k, :k].copy(), nthreads=8)), c
+    buf.free()
