@@ -486,7 +486,11 @@ int extend_squares(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, uint32_
     // the latency and queue forms address the column halves with 32-bit offsets; wider
     // squares take the two passes below, whose launches pick the wide forms
     const bool narrow = narrow_ok(ctx, k, W * S, S);
-    if (phases == 3 && narrow && count <= ctx->split_max.load(std::memory_order_relaxed)) {
+    // (17 <= k <= 64: the split form wins up to 64 squares per call, profiles/r06w_small_ab.jsonl)
+    const uint32_t smax = ctx->split_max.load(std::memory_order_relaxed);
+    const uint32_t M = ceil_pow2(k);
+    const uint32_t split_limit = smax && (M == 32 || M == 64) && smax < kSplitSmallBatch ? kSplitSmallBatch : smax;
+    if (phases == 3 && narrow && count <= split_limit) {
         const int rc = extend_squares_split(ctx, d_eds, k, S, count, st);
         if (rc != RSM_EUNSUPPORTED) return rc;
     }

@@ -409,9 +409,9 @@ def test_multi_gpu_inplace_pinned_world1(lib, multi, sched):
 
 
 @pytest.mark.parametrize("k,S,count", [(17, 64, 1), (32, 512, 1), (33, 320, 2), (50, 512, 1), (64, 512, 1),
-                                       (64, 512, 12), (64, 128, 13), (24, 1024, 5)])
+                                       (64, 512, 12), (64, 128, 13), (24, 1024, 5), (32, 128, 64), (64, 64, 65)])
 def test_small_square_latency_form(lib, k, S, count):
-    """17 <= k <= 64: up to 12 squares per call take the split latency form
+    """17 <= k <= 64: up to 64 squares per call take the split latency form
     (encode_gf8_splitm_kernel), larger batches the byte-table passes; both == oracle."""
     W = 2 * k
     n = W * W * S * count
