@@ -1156,8 +1156,8 @@ __global__ __launch_bounds__(64 * NW) void encode_gf8_split_kernel(SplitEncPlan 
     }
 }
 // ---------------------------------------------------------------------------
-// 16-wave latency form (round 6, diagnostic A/B: rsm_diag_set_split_waves 16): PW = 8
-// points per wave, so each wave's chain of butterflies is half as long and a launch
+// 16-wave latency form (round 6; production for one square and the per-codeword codec,
+// kSplitWavesOne; diagnostic builds: rsm_diag_set_split_waves 16): PW = 8 points per wave, so each wave's chain of butterflies is half as long and a launch
 // has twice the waves to hide its latencies.  Three register bits cannot hold the
 // layer bits 3..6 in one window, so there are three layouts:
 //   S: wave w, register j: e = 8w + j                         IFFT d = 1, 2, 4; FFT 4, 2, 1
