@@ -59,7 +59,7 @@ int rsm_ctx_set_pass_grid(rsm_ctx* ctx, int pass, int cus, int* previous);
 /* Latency tuning: GF(2^8) extensions of up to `squares` squares per call with
  * 65 <= k <= 128 run in the latency form (two launches of the split byte-table
  * encoder over every CU) instead of the single queue-driven launch; 0 = always the
- * queue launch.  Default 12.  With 17 <= k <= 64 the latency form takes up to
+ * queue launch.  Default 12.  With 9 <= k <= 64 the latency form takes up to
  * max(squares, 64) squares per call (0: never) instead of the one-wave-per-codeword
  * byte-table passes.  *previous (may be NULL) receives the old value.  Results
  * never depend on it. */

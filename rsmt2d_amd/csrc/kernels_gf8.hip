@@ -1341,7 +1341,7 @@ __global__ __launch_bounds__(1024, 8) void encode_gf8_split16_kernel(SplitEncPla
 }
 
 // ---------------------------------------------------------------------------
-// Latency form for M = 32 and 64 (17 <= k <= 64, round 6): one NW-wave workgroup per
+// Latency form for M = 16, 32 and 64 (9 <= k <= 64, round 6): one NW-wave workgroup per
 // (codeword, 256-byte chunk) with the layouts of encode_gf8_split_kernel (S: e = PW w + j,
 // L: e = NW h + w, the top pair merged), so one square's codewords spread over NW times
 // the waves of the byte-table kernel's one-wave-per-task form, whose single wave per
@@ -1442,7 +1442,7 @@ static void split_set(SplitEncPlan& p, int i, const CodewordSet& c, uint32_t& n)
 
 hipError_t launch_encode_gf8_split(const CodewordSet& a, const CodewordSet* b, hipStream_t st, int nw) {
     const uint32_t M = ceil_pow2(a.k);
-    if ((M != 32 && M != 64 && M != 128) || (b && ceil_pow2(b->k) != M)) return hipErrorInvalidValue;
+    if ((M != 16 && M != 32 && M != 64 && M != 128) || (b && ceil_pow2(b->k) != M)) return hipErrorInvalidValue;
     SplitEncPlan p{};
     split_set(p, 0, a, p.n0);
     if (b) split_set(p, 1, *b, p.n1);
@@ -1454,6 +1454,10 @@ hipError_t launch_encode_gf8_split(const CodewordSet& a, const CodewordSet* b, h
     }
     if (M == 32) {  // 4 waves of 8 points
         hipLaunchKernelGGL((encode_gf8_splitm_kernel<32, 4>), dim3((uint32_t)tasks), dim3(256), 0, st, p);
+        return hipGetLastError();
+    }
+    if (M == 16) {  // 4 waves of 4 points
+        hipLaunchKernelGGL((encode_gf8_splitm_kernel<16, 4>), dim3((uint32_t)tasks), dim3(256), 0, st, p);
         return hipGetLastError();
     }
     return launch_split(p, (uint32_t)tasks, split_waves(b ? 0 : 1, nw), st);

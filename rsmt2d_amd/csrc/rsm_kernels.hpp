@@ -140,7 +140,7 @@ hipError_t launch_decode_gf8(const DecodeSet& ds, hipStream_t st);
 // nw: waves per (codeword, 256-byte chunk), 8 or 16 (kSplitWavesOne)
 hipError_t launch_encode_gf8_split(const CodewordSet& a, const CodewordSet* b, hipStream_t st, int nw);
 constexpr int kSplitWavesOne = 16;  // one square / one codeword: the 16-wave latency form
-constexpr uint32_t kSplitSmallBatch = 64;  // 17 <= k <= 64: squares per call for the split form (split_max > 0)
+constexpr uint32_t kSplitSmallBatch = 64;  // 9 <= k <= 64: squares per call for the split form (split_max > 0)
 void set_split_diag_waves(int first, int second);  // diagnostic builds only
 void set_split_diag_fused(bool on);                  // diagnostic builds only
 void set_enc16_diag_e64(int mode);                   // diagnostic builds only

@@ -443,7 +443,7 @@ int extend_squares_split(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, u
     if (field_bits(k) != 8 || count == 0) return RSM_EUNSUPPORTED;
     // M = 32 / 64 (round 6): the split form too (encode_gf8_splitm_kernel) for up to
     // split_max squares; larger batches take the byte-table passes
-    if (M != 128 && M != 32 && M != 64) return RSM_EUNSUPPORTED;
+    if (M != 128 && M != 16 && M != 32 && M != 64) return RSM_EUNSUPPORTED;
     const CodewordSet rows = rows_set(d_eds, k, S, count);
     CodewordSet c0 = cols_set(d_eds, k, S, count);  // columns 0 .. k-1 (Q0 -> Q2)
     c0.per_square = k;
@@ -486,10 +486,11 @@ int extend_squares(rsm_ctx* ctx, uint8_t* d_eds, uint32_t k, uint32_t S, uint32_
     // the latency and queue forms address the column halves with 32-bit offsets; wider
     // squares take the two passes below, whose launches pick the wide forms
     const bool narrow = narrow_ok(ctx, k, W * S, S);
-    // (17 <= k <= 64: the split form wins up to 64 squares per call, profiles/r06w_small_ab.jsonl)
+    // (9 <= k <= 64: the split form wins up to 64 squares per call, profiles/r06w_small_ab.jsonl,
+    // r06y_small16_ab.jsonl)
     const uint32_t smax = ctx->split_max.load(std::memory_order_relaxed);
     const uint32_t M = ceil_pow2(k);
-    const uint32_t split_limit = smax && (M == 32 || M == 64) && smax < kSplitSmallBatch ? kSplitSmallBatch : smax;
+    const uint32_t split_limit = smax && (M == 16 || M == 32 || M == 64) && smax < kSplitSmallBatch ? kSplitSmallBatch : smax;
     if (phases == 3 && narrow && count <= split_limit) {
         const int rc = extend_squares_split(ctx, d_eds, k, S, count, st);
         if (rc != RSM_EUNSUPPORTED) return rc;

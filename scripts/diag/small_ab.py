@@ -23,7 +23,7 @@ def main():
     ms = ctypes.c_float()
     S = 512
     for rep in range(2):
-        for k in (32, 64):
+        for k in [int(x) for x in os.environ.get("SMALL_KS", "32,64").split(",")]:
             W = 2 * k
             counts = [int(c) for c in os.environ.get("SMALL_COUNTS", "1,2,4,8,12").split(",")]
             for count in counts:

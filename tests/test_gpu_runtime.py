@@ -409,7 +409,8 @@ def test_multi_gpu_inplace_pinned_world1(lib, multi, sched):
 
 
 @pytest.mark.parametrize("k,S,count", [(17, 64, 1), (32, 512, 1), (33, 320, 2), (50, 512, 1), (64, 512, 1),
-                                       (64, 512, 12), (64, 128, 13), (24, 1024, 5), (32, 128, 64), (64, 64, 65)])
+                                       (64, 512, 12), (64, 128, 13), (24, 1024, 5), (32, 128, 64), (64, 64, 65),
+                                       (9, 64, 1), (16, 512, 1), (13, 192, 7), (16, 64, 70)])
 def test_small_square_latency_form(lib, k, S, count):
     """17 <= k <= 64: up to 64 squares per call take the split latency form
     (encode_gf8_splitm_kernel), larger batches the byte-table passes; both == oracle."""
