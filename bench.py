@@ -834,7 +834,9 @@ def bench_small_squares(local, L, R, S=512, ks=(4, 8, 16, 32, 64)):
     for e in (e0, e1):
         L.rsm_event_destroy(e)
     return {"workload": f"BenchmarkExtensionEncoding k = {', '.join(map(str, ks))} at S = {S} (GF(2^8))",
-            "kernel": "encode_gf8_kernel<M> (byte tables), row pass then column pass", "by_k": out,
+            "kernel": "single: encode_gf8_splitm_kernel<M, NW> latency form for k = 9..64 (two launches), "
+                      "encode_gf8_kernel<M> row pass then column pass for k <= 8; batch (more than 64 squares): "
+                      "encode_gf8_kernel<M>", "by_k": out,
             "note": "single = one square per rsm_extend_squares_dev (device time of back-to-back calls on one "
                     "stream); batch = 1 GiB of EDS per call; frac = 4 k^2 S per square / time / 8 TB/s"}
 
